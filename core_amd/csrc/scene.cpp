@@ -1,0 +1,238 @@
+// Host scene assembly, kd-tree build trigger and the procedural probe scenes.
+#include "scene.h"
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <stdexcept>
+
+namespace yk {
+
+void rec_normal(const float* t, float* n) {
+  // triangle_t::recNormal, triangle_inline.h:100-107
+  float e1x = t[3] - t[0], e1y = t[4] - t[1], e1z = t[5] - t[2];
+  float e2x = t[6] - t[0], e2y = t[7] - t[1], e2z = t[8] - t[2];
+  float x = e1y * e2z - e1z * e2y;
+  float y = e1z * e2x - e1x * e2z;
+  float z = e1x * e2y - e1y * e2x;
+  float len = x * x + y * y + z * z;  // vector3d_t::normalize, vector3d.h:249-260
+  if (len != 0) {
+    len = 1.0f / std::sqrt(len);
+    x *= len;
+    y *= len;
+    z *= len;
+  }
+  n[0] = x;
+  n[1] = y;
+  n[2] = z;
+}
+
+void Scene::finalize() {
+  // scene_t::update, scene.cc:755-782: visible non-base TRIM meshes in object
+  // id order, triangles in insertion order.
+  auto t0 = std::chrono::steady_clock::now();
+  tri_verts.clear();
+  tri_material.clear();
+  tri_normal.clear();
+  for (const Mesh& m : meshes) {
+    if (!m.visible) continue;
+    const size_t nf = m.faces.size() / 3;
+    const int np = (int)(m.points.size() / 3);
+    for (size_t f = 0; f < nf; ++f) {
+      float tv[9];
+      for (int k = 0; k < 3; ++k) {
+        int vi = m.faces[3 * f + k];
+        if (vi < 0 || vi >= np) throw std::invalid_argument("mesh face references a missing vertex");
+        tv[3 * k + 0] = m.points[3 * vi + 0];
+        tv[3 * k + 1] = m.points[3 * vi + 1];
+        tv[3 * k + 2] = m.points[3 * vi + 2];
+      }
+      tri_verts.insert(tri_verts.end(), tv, tv + 9);
+      tri_material.push_back(m.material);
+      float nrm[3];
+      rec_normal(tv, nrm);
+      tri_normal.insert(tri_normal.end(), nrm, nrm + 3);
+    }
+  }
+  const int ntris = (int)tri_material.size();
+  if (ntris == 0) throw std::invalid_argument("scene is empty");
+  build_kdtree(tri_verts.data(), ntris, tree);
+  built = true;
+  build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+namespace {
+
+inline float atof_f(double v) { return (float)v; }  // xmlparser.cc:237-239: atof -> float
+
+void add_quad(Scene& s, const double p[4][3], int mat) {
+  Mesh m;
+  for (int i = 0; i < 4; ++i)
+    for (int k = 0; k < 3; ++k) m.points.push_back(atof_f(p[i][k]));
+  m.faces = {0, 1, 2, 0, 2, 3};
+  m.material = mat;
+  s.meshes.push_back(m);
+}
+
+void add_box(Scene& s, double cx, double cz, double sx, double sz, double h, int mat) {
+  const double x0 = cx - sx, x1 = cx + sx, z0 = cz - sz, z1 = cz + sz;
+  const double v[8][3] = {{x0, 0, z0}, {x1, 0, z0}, {x1, 0, z1}, {x0, 0, z1},
+                          {x0, h, z0}, {x1, h, z0}, {x1, h, z1}, {x0, h, z1}};
+  static const int f[12][3] = {{4, 5, 6}, {4, 6, 7}, {0, 1, 5}, {0, 5, 4}, {1, 2, 6}, {1, 6, 5},
+                               {2, 3, 7}, {2, 7, 6}, {3, 0, 4}, {3, 4, 7}, {0, 2, 1}, {0, 3, 2}};
+  Mesh m;
+  for (int i = 0; i < 8; ++i)
+    for (int k = 0; k < 3; ++k) m.points.push_back(atof_f(v[i][k]));
+  for (int i = 0; i < 12; ++i)
+    for (int k = 0; k < 3; ++k) m.faces.push_back(f[i][k]);
+  m.material = mat;
+  s.meshes.push_back(m);
+}
+
+int add_mat(Scene& s, int type, float r, float g, float b, float power) {
+  yk_material m{};
+  m.type = type;
+  m.color[0] = r;
+  m.color[1] = g;
+  m.color[2] = b;
+  m.diffuse_reflect = 1.f;
+  m.emit = 0.f;
+  m.power = power;
+  m.double_sided = 0;
+  s.materials.push_back(m);
+  return (int)s.materials.size() - 1;
+}
+
+// value as the XML loader sees a "%.6f" formatted coordinate: strtod of the
+// text, then (float) (xmlparser.cc:237-239)
+inline float fmt6(double v) {
+  char buf[64];
+  std::snprintf(buf, sizeof buf, "%.6f", v);
+  return (float)std::strtod(buf, nullptr);
+}
+
+}  // namespace
+
+// Cornell probe of BASELINE.md "Probe scenes": 5 walls (10 tris), two boxes
+// (24 tris), light quad (2 tris) = 36 tris; area light with 4 samples.
+void gen_cornell(Scene& s, int resx, int resy) {
+  s = Scene();
+  const int white = add_mat(s, YK_MAT_SHINYDIFFUSE, 0.8f, 0.8f, 0.8f, 1.f);
+  const int red = add_mat(s, YK_MAT_SHINYDIFFUSE, 0.8f, 0.1f, 0.1f, 1.f);
+  const int green = add_mat(s, YK_MAT_SHINYDIFFUSE, 0.1f, 0.8f, 0.1f, 1.f);
+  const int lightm = add_mat(s, YK_MAT_LIGHT, 1.f, 1.f, 1.f, 10.f);
+  const double floor_[4][3] = {{-1, 0, -1}, {1, 0, -1}, {1, 0, 1}, {-1, 0, 1}};
+  const double ceil_[4][3] = {{-1, 2, -1}, {-1, 2, 1}, {1, 2, 1}, {1, 2, -1}};
+  const double back_[4][3] = {{-1, 0, 1}, {1, 0, 1}, {1, 2, 1}, {-1, 2, 1}};
+  const double left_[4][3] = {{-1, 0, -1}, {-1, 0, 1}, {-1, 2, 1}, {-1, 2, -1}};
+  const double right_[4][3] = {{1, 0, -1}, {1, 2, -1}, {1, 2, 1}, {1, 0, 1}};
+  const double lq[4][3] = {{-0.25, 1.98, -0.25}, {-0.25, 1.98, 0.25}, {0.25, 1.98, 0.25}, {0.25, 1.98, -0.25}};
+  add_quad(s, floor_, white);
+  add_quad(s, ceil_, white);
+  add_quad(s, back_, white);
+  add_quad(s, left_, red);
+  add_quad(s, right_, green);
+  add_box(s, -0.35, 0.3, 0.3, 0.3, 1.2, white);
+  add_box(s, 0.4, -0.3, 0.3, 0.3, 0.6, white);
+  add_quad(s, lq, lightm);
+  yk_light l{};
+  l.type = YK_LIGHT_AREA;
+  const float c[3] = {-0.25f, 1.979f, -0.25f}, p1[3] = {0.25f, 1.979f, -0.25f}, p2[3] = {-0.25f, 1.979f, 0.25f};
+  for (int k = 0; k < 3; ++k) {
+    l.corner[k] = c[k];
+    l.point1[k] = p1[k];
+    l.point2[k] = p2[k];
+    l.color[k] = 1.f;
+  }
+  l.power = 10.f;
+  l.samples = 4;
+  s.lights.push_back(l);
+  yk_camera cam{};
+  const float from[3] = {0, 1, -3.6f}, to[3] = {0, 1, 0}, up[3] = {0, 2, -3.6f};
+  for (int k = 0; k < 3; ++k) {
+    cam.from[k] = from[k];
+    cam.to[k] = to[k];
+    cam.up[k] = up[k];
+  }
+  cam.resx = resx;
+  cam.resy = resy;
+  cam.focal = 1.3f;
+  cam.aspect_ratio = 1.f;
+  cam.near_clip = 0.f;
+  cam.far_clip = -1.f;
+  s.camera = cam;
+  s.has_camera = true;
+}
+
+// 1M-triangle probe of BASELINE.md: displaced UV sphere (NU x NV grid,
+// 2*NU*(NV-1) tris) centred at (0,1.2,0) over a 2-tri 6x6 floor, 1x1 area light
+// at y=3 with 1 sample. Coordinates go through "%.6f" text like the XML.
+void gen_bumpy(Scene& s, int nu, int nv, int resx, int resy) {
+  s = Scene();
+  const int white = add_mat(s, YK_MAT_SHINYDIFFUSE, 0.8f, 0.8f, 0.8f, 1.f);
+  const int red = add_mat(s, YK_MAT_SHINYDIFFUSE, 0.8f, 0.1f, 0.1f, 1.f);
+  {
+    Mesh m;
+    const double fl[4][3] = {{-3, 0, -3}, {3, 0, -3}, {3, 0, 3}, {-3, 0, 3}};
+    for (int i = 0; i < 4; ++i)
+      for (int k = 0; k < 3; ++k) m.points.push_back(fmt6(fl[i][k]));
+    m.faces = {0, 2, 1, 0, 3, 2};
+    m.material = white;
+    s.meshes.push_back(m);
+  }
+  {
+    Mesh m;
+    m.points.reserve((size_t)nu * nv * 3);
+    const double pi = 3.141592653589793;
+    for (int j = 0; j < nv; ++j) {
+      const double th = pi * (double)j / (double)(nv - 1);
+      for (int i = 0; i < nu; ++i) {
+        const double ph = 2.0 * pi * (double)i / (double)nu;
+        const double r = 1.0 + 0.08 * std::sin(7.0 * th) * std::cos(9.0 * ph) +
+                         0.03 * std::sin(23.0 * th + 5.0 * ph);
+        const double sth = std::sin(th), cth = std::cos(th);
+        m.points.push_back(fmt6(r * sth * std::cos(ph)));
+        m.points.push_back(fmt6(1.2 + r * cth));
+        m.points.push_back(fmt6(r * sth * std::sin(ph)));
+      }
+    }
+    m.faces.reserve((size_t)nu * (nv - 1) * 6);
+    for (int j = 0; j < nv - 1; ++j)
+      for (int i = 0; i < nu; ++i) {
+        const int a = j * nu + i, b = j * nu + (i + 1) % nu, c = a + nu, d = b + nu;
+        m.faces.insert(m.faces.end(), {a, c, b, b, c, d});
+      }
+    m.material = red;
+    s.meshes.push_back(m);
+  }
+  yk_light l{};
+  l.type = YK_LIGHT_AREA;
+  const float c[3] = {-0.5f, 3.f, -0.5f}, p1[3] = {0.5f, 3.f, -0.5f}, p2[3] = {-0.5f, 3.f, 0.5f};
+  for (int k = 0; k < 3; ++k) {
+    l.corner[k] = c[k];
+    l.point1[k] = p1[k];
+    l.point2[k] = p2[k];
+    l.color[k] = 1.f;
+  }
+  l.power = 8.f;
+  l.samples = 1;
+  s.lights.push_back(l);
+  yk_camera cam{};
+  const float from[3] = {0, 1.5f, -4.f}, to[3] = {0, 1.2f, 0}, up[3] = {0, 2.5f, -4.f};
+  for (int k = 0; k < 3; ++k) {
+    cam.from[k] = from[k];
+    cam.to[k] = to[k];
+    cam.up[k] = up[k];
+  }
+  cam.resx = resx;
+  cam.resy = resy;
+  cam.focal = 1.4f;
+  cam.aspect_ratio = 1.f;
+  cam.near_clip = 0.f;
+  cam.far_clip = -1.f;
+  s.camera = cam;
+  s.has_camera = true;
+}
+
+}  // namespace yk

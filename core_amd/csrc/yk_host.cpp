@@ -1,0 +1,230 @@
+// Host half of the C-ABI (include/yk_api.h): scene assembly, kd-tree build,
+// fixture generation, error reporting. No GPU needed; exercised by the CPU
+// tests and by the oracle harness.
+#include <cstring>
+#include <exception>
+#include <new>
+#include <stdexcept>
+#include <string>
+
+#include "../../include/yk_api.h"
+#include "scene.h"
+#include "yk_internal.h"
+
+struct yk_scene {
+  yk::Scene s;
+};
+
+namespace yk {
+thread_local std::string g_last_error;
+int set_error(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+}  // namespace yk
+
+using yk::set_error;
+
+#define YK_GUARD_BEGIN try {
+#define YK_GUARD_END                                                   \
+  }                                                                    \
+  catch (const std::bad_alloc&) { return set_error(YK_ERR_ALLOC, "out of host memory"); } \
+  catch (const std::invalid_argument& e) { return set_error(YK_ERR_ARG, e.what()); }      \
+  catch (const std::exception& e) { return set_error(YK_ERR_INTERNAL, e.what()); }        \
+  catch (...) { return set_error(YK_ERR_INTERNAL, "unknown C++ exception"); }
+
+extern "C" {
+
+const char* yk_last_error(void) { return yk::g_last_error.c_str(); }
+const char* yk_version(void) { return "yk 0.1 (gfx950)"; }
+
+int yk_scene_create(yk_scene** out) {
+  if (!out) return set_error(YK_ERR_ARG, "yk_scene_create: out is NULL");
+  YK_GUARD_BEGIN
+  *out = new yk_scene();
+  return YK_OK;
+  YK_GUARD_END
+}
+
+void yk_scene_destroy(yk_scene* s) { delete s; }
+
+int yk_scene_add_material(yk_scene* s, const yk_material* m, int32_t* id_out) {
+  if (!s || !m) return set_error(YK_ERR_ARG, "yk_scene_add_material: NULL argument");
+  if (m->type != YK_MAT_SHINYDIFFUSE && m->type != YK_MAT_LIGHT)
+    return set_error(YK_ERR_UNSUPPORTED, "material type not supported by the GPU path");
+  YK_GUARD_BEGIN
+  s->s.materials.push_back(*m);
+  s->s.built = false;
+  if (id_out) *id_out = (int32_t)s->s.materials.size() - 1;
+  return YK_OK;
+  YK_GUARD_END
+}
+
+int yk_scene_add_mesh(yk_scene* s, const float* points, int32_t npoints, const int32_t* faces,
+                      int32_t nfaces, int32_t material, int32_t* obj_id_out) {
+  if (!s || (npoints > 0 && !points) || (nfaces > 0 && !faces) || npoints < 0 || nfaces < 0)
+    return set_error(YK_ERR_ARG, "yk_scene_add_mesh: bad arguments");
+  if (material < 0 || material >= (int32_t)s->s.materials.size())
+    return set_error(YK_ERR_ARG, "yk_scene_add_mesh: unknown material id");
+  for (int64_t i = 0; i < 3 * (int64_t)nfaces; ++i)
+    if (faces[i] < 0 || faces[i] >= npoints)
+      return set_error(YK_ERR_ARG, "yk_scene_add_mesh: face index out of range");
+  YK_GUARD_BEGIN
+  yk::Mesh m;
+  m.points.assign(points, points + 3 * (size_t)npoints);
+  m.faces.assign(faces, faces + 3 * (size_t)nfaces);
+  m.material = material;
+  s->s.meshes.push_back(std::move(m));
+  s->s.built = false;
+  if (obj_id_out) *obj_id_out = (int32_t)s->s.meshes.size();
+  return YK_OK;
+  YK_GUARD_END
+}
+
+int yk_scene_add_light(yk_scene* s, const yk_light* l) {
+  if (!s || !l) return set_error(YK_ERR_ARG, "yk_scene_add_light: NULL argument");
+  if (l->type != YK_LIGHT_AREA) return set_error(YK_ERR_UNSUPPORTED, "light type not supported");
+  if (l->samples < 1) return set_error(YK_ERR_ARG, "area light needs samples >= 1");
+  YK_GUARD_BEGIN
+  s->s.lights.push_back(*l);
+  return YK_OK;
+  YK_GUARD_END
+}
+
+int yk_scene_set_camera(yk_scene* s, const yk_camera* c) {
+  if (!s || !c) return set_error(YK_ERR_ARG, "yk_scene_set_camera: NULL argument");
+  if (c->resx <= 0 || c->resy <= 0) return set_error(YK_ERR_ARG, "camera resolution must be > 0");
+  s->s.camera = *c;
+  s->s.has_camera = true;
+  return YK_OK;
+}
+
+int yk_scene_build(yk_scene* s) {
+  if (!s) return set_error(YK_ERR_ARG, "yk_scene_build: NULL scene");
+  YK_GUARD_BEGIN
+  s->s.finalize();
+  return YK_OK;
+  YK_GUARD_END
+}
+
+int yk_scene_info_get(const yk_scene* s, yk_scene_info* o) {
+  if (!s || !o) return set_error(YK_ERR_ARG, "yk_scene_info_get: NULL argument");
+  std::memset(o, 0, sizeof *o);
+  const yk::Scene& S = s->s;
+  o->ntris = (int32_t)S.tri_material.size();
+  o->nmeshes = (int32_t)S.meshes.size();
+  o->nmaterials = (int32_t)S.materials.size();
+  o->nlights = (int32_t)S.lights.size();
+  if (S.built) {
+    o->nnodes = (int32_t)(S.tree.nodes.size() / 2);
+    o->nleaf_prims = (int32_t)S.tree.leaf_prims.size();
+    o->max_depth = S.tree.max_depth;
+    o->inodes = S.tree.stats.inodes;
+    o->leaves = S.tree.stats.leaves;
+    o->empty_leaves = S.tree.stats.empty_leaves;
+    o->leaf_refs = S.tree.stats.leaf_prims;
+    o->depth_limit_leaves = S.tree.stats.depth_limit_reached;
+    o->bad_split_leaves = S.tree.stats.bad_splits;
+    std::memcpy(o->bound, S.tree.bound, sizeof o->bound);
+    o->build_seconds = S.build_seconds;
+  }
+  return YK_OK;
+}
+
+int yk_scene_export(const yk_scene* s, float* tri_verts, int32_t* tri_material, float* tri_normal,
+                    uint32_t* nodes, uint32_t* leaf_prims) {
+  if (!s) return set_error(YK_ERR_ARG, "yk_scene_export: NULL scene");
+  const yk::Scene& S = s->s;
+  if (!S.built) return set_error(YK_ERR_STATE, "yk_scene_export: scene not built");
+  if (tri_verts) std::memcpy(tri_verts, S.tri_verts.data(), S.tri_verts.size() * sizeof(float));
+  if (tri_material) std::memcpy(tri_material, S.tri_material.data(), S.tri_material.size() * sizeof(int32_t));
+  if (tri_normal) std::memcpy(tri_normal, S.tri_normal.data(), S.tri_normal.size() * sizeof(float));
+  if (nodes) std::memcpy(nodes, S.tree.nodes.data(), S.tree.nodes.size() * sizeof(uint32_t));
+  if (leaf_prims) std::memcpy(leaf_prims, S.tree.leaf_prims.data(), S.tree.leaf_prims.size() * sizeof(uint32_t));
+  return YK_OK;
+}
+
+int yk_scene_get_material(const yk_scene* s, int32_t i, yk_material* out) {
+  if (!s || !out || i < 0 || i >= (int32_t)s->s.materials.size())
+    return set_error(YK_ERR_ARG, "yk_scene_get_material: bad index");
+  *out = s->s.materials[i];
+  return YK_OK;
+}
+
+int yk_scene_get_light(const yk_scene* s, int32_t i, yk_light* out) {
+  if (!s || !out || i < 0 || i >= (int32_t)s->s.lights.size())
+    return set_error(YK_ERR_ARG, "yk_scene_get_light: bad index");
+  *out = s->s.lights[i];
+  return YK_OK;
+}
+
+int yk_scene_get_camera(const yk_scene* s, yk_camera* out) {
+  if (!s || !out) return set_error(YK_ERR_ARG, "yk_scene_get_camera: NULL argument");
+  if (!s->s.has_camera) return set_error(YK_ERR_STATE, "scene has no camera");
+  *out = s->s.camera;
+  return YK_OK;
+}
+
+void yk_render_params_default(yk_render_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof *p);
+  // defaults of pathIntegrator_t::factory (pathtracer.cc:337-343) and
+  // renderEnvironment_t::createImageFilm/setupScene (environment.cc:484-490,598-654)
+  p->integrator = YK_INTEGRATOR_PATH;
+  p->raydepth = 5;
+  p->path_samples = 32;
+  p->bounces = 3;
+  p->caustic_type = YK_CAUSTIC_PATH;
+  p->width = 320;
+  p->height = 240;
+  p->aa_samples = 1;
+  p->aa_passes = 1;
+  p->filter = YK_FILTER_BOX;
+  p->aa_pixelwidth = 1.5f;
+  p->tile_size = 32;
+  p->transp_background = 1;
+}
+
+int yk_scene_generate(yk_scene* s, const char* name, int32_t p0, int32_t p1, int32_t resx,
+                      int32_t resy, yk_render_params* params_out) {
+  if (!s || !name) return set_error(YK_ERR_ARG, "yk_scene_generate: NULL argument");
+  if (resx <= 0 || resy <= 0) return set_error(YK_ERR_ARG, "yk_scene_generate: bad resolution");
+  YK_GUARD_BEGIN
+  yk_render_params p;
+  yk_render_params_default(&p);
+  p.width = resx;
+  p.height = resy;
+  p.aa_pixelwidth = 1.0f;
+  p.filter = YK_FILTER_BOX;
+  p.tile_size = 32;
+  p.aa_passes = 1;
+  p.raydepth = 2;
+  p.caustic_type = YK_CAUSTIC_NONE;
+  p.path_samples = 1;
+  std::string n(name);
+  if (n == "cornell_dl" || n == "cornell_pt") {
+    yk::gen_cornell(s->s, resx, resy);
+    if (n == "cornell_dl") {
+      p.integrator = YK_INTEGRATOR_DIRECT;
+      p.aa_samples = 4;
+    } else {
+      p.integrator = YK_INTEGRATOR_PATH;
+      p.bounces = 4;
+      p.aa_samples = 16;
+    }
+  } else if (n == "bumpy") {
+    const int nu = p0 > 0 ? p0 : 1000, nv = p1 > 0 ? p1 : 501;
+    if (nu < 3 || nv < 3) return set_error(YK_ERR_ARG, "bumpy: nu, nv must be >= 3");
+    yk::gen_bumpy(s->s, nu, nv, resx, resy);
+    p.integrator = YK_INTEGRATOR_PATH;
+    p.bounces = 3;
+    p.aa_samples = 4;
+  } else {
+    return set_error(YK_ERR_ARG, "unknown procedural scene '" + n + "'");
+  }
+  if (params_out) *params_out = p;
+  return YK_OK;
+  YK_GUARD_END
+}
+
+}  // extern "C"

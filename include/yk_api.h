@@ -1,0 +1,184 @@
+/*
+ * yk_api.h -- C-ABI boundary of the MI355X ray-scene intersection and
+ * path-integrator hot path (libyk.so).
+ *
+ * Replaces, behind the reference's own plugin API, these reference entry points
+ * (reference = inferrna/Core, TheBounty 0.1.6):
+ *   scene_t::startTriMesh/addVertex/addTriangle/endTriMesh  scene.cc:265-320,520-625
+ *   scene_t::update (prim gather + triKdTree_t build)        scene.cc:748-850
+ *   scene_t::intersect  -> triKdTree_t::Intersect            scene.cc:852-879, kdtree.cc:675-817
+ *   scene_t::isShadowed -> triKdTree_t::IntersectS           scene.cc:881-902, kdtree.cc:820-947
+ *   tiledIntegrator_t::render/renderPass/renderTile          integrator.cc:132-339
+ *   pathIntegrator_t::integrate                              pathtracer.cc:134-333
+ *   directLighting_t::integrate                              directlight.cc:112-182
+ *   imageFilm_t::addSample / flush                           imagefilm.cc:383-511
+ * The C++ plugin (plugin/yk_pathtrace_plugin.cc) binds these from inside a
+ * tiledIntegrator_t subclass registered as "pathtracing"/"directlighting".
+ *
+ * Conventions: every function returns 0 (YK_OK) or a YK_ERR_* code; the text
+ * of the last error of the calling thread is yk_last_error(). No C++ exception
+ * and no HIP error crosses this boundary. Pointers named d_* are device (HBM)
+ * pointers on the device the yk_device was opened on; all others are host.
+ */
+#ifndef YK_API_H
+#define YK_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YK_OK 0
+#define YK_ERR_ARG 1
+#define YK_ERR_STATE 2
+#define YK_ERR_HIP 3
+#define YK_ERR_UNSUPPORTED 4
+#define YK_ERR_ALLOC 5
+#define YK_ERR_INTERNAL 6
+
+/* ---- scene description (POD mirrors of the reference paraMap_t params) ---- */
+
+enum { YK_MAT_SHINYDIFFUSE = 0, YK_MAT_LIGHT = 1 };
+typedef struct yk_material {
+  int32_t type;           /* YK_MAT_*                                               */
+  float color[3];         /* "color"  shinydiffuse.cc:474,483 / simple.cc:82        */
+  float diffuse_reflect;  /* "diffuse_reflect" (shinydiffusemat, default 1)         */
+  float emit;             /* "emit" (shinydiffusemat, default 0)                    */
+  float power;            /* "power" (light_mat, default 1)                         */
+  int32_t double_sided;   /* "double_sided" (light_mat, default 0)                  */
+} yk_material;
+
+enum { YK_LIGHT_AREA = 0 };
+typedef struct yk_light { /* areaLight_t::factory, arealight.cc:171-192 */
+  int32_t type;
+  float corner[3], point1[3], point2[3];
+  float color[3];
+  float power;
+  int32_t samples;
+} yk_light;
+
+typedef struct yk_camera { /* perspectiveCam_t::factory, perspectiveCamera.cc:191-232 */
+  float from[3], to[3], up[3];
+  int32_t resx, resy;
+  float focal, aspect_ratio, near_clip, far_clip;
+} yk_camera;
+
+enum { YK_INTEGRATOR_DIRECT = 0, YK_INTEGRATOR_PATH = 1 };
+enum { YK_FILTER_BOX = 0, YK_FILTER_MITCHELL = 1, YK_FILTER_GAUSS = 2, YK_FILTER_LANCZOS = 3 };
+enum { YK_CAUSTIC_NONE = 0, YK_CAUSTIC_PATH = 1 };
+
+typedef struct yk_render_params {
+  int32_t integrator;     /* YK_INTEGRATOR_*                                         */
+  int32_t raydepth;       /* "raydepth"                                              */
+  int32_t path_samples;   /* "path_samples" (pathtracing)                            */
+  int32_t bounces;        /* "bounces" (pathtracing)                                 */
+  int32_t caustic_type;   /* "caustic_type": YK_CAUSTIC_NONE or YK_CAUSTIC_PATH      */
+  int32_t width, height;  /* render area ("width"/"height")                          */
+  int32_t xstart, ystart; /* crop offset ("xstart"/"ystart")                         */
+  int32_t aa_samples;     /* "AA_minsamples"                                         */
+  int32_t aa_passes;      /* "AA_passes" (only 1 supported)                          */
+  int32_t filter;         /* YK_FILTER_*                                             */
+  float aa_pixelwidth;    /* "AA_pixelwidth"                                         */
+  int32_t tile_size;      /* "tile_size"                                             */
+  int32_t transp_background; /* "bg_transp" (default 1)                             */
+} yk_render_params;
+
+/* one ray, 32 bytes: ray_t (ray.h:26-49) without time */
+typedef struct yk_ray {
+  float from[3];
+  float dir[3];
+  float tmin;
+  float tmax; /* < 0 means unbounded, as scene_t::intersect (scene.cc:855-856) */
+} yk_ray;
+
+/* closest-hit record, 16 bytes: prim id (scene_t::update order) + t + b1,b2
+ * (intersectData_t, surface.h:35-56); b0 = 1 - b1 - b2. prim = -1 on miss. */
+typedef struct yk_hit {
+  int32_t prim;
+  float t;
+  float b1;
+  float b2;
+} yk_hit;
+
+typedef struct yk_scene_info {
+  int32_t ntris, nmeshes, nmaterials, nlights;
+  int32_t nnodes, nleaf_prims, max_depth;
+  int32_t inodes, leaves, empty_leaves, leaf_refs, depth_limit_leaves, bad_split_leaves;
+  float bound[6];
+  double build_seconds;
+} yk_scene_info;
+
+typedef struct yk_stats {
+  uint64_t closest_rays;   /* scene_t::intersect calls (camera + bounces)          */
+  uint64_t shadow_rays;    /* scene_t::isShadowed calls                            */
+  uint64_t closest_nodes;  /* kd nodes visited by closest-hit traversal            */
+  uint64_t closest_tris;   /* triangle tests (= leaf refs read) by closest-hit     */
+  uint64_t shadow_nodes;
+  uint64_t shadow_tris;
+  uint64_t camera_samples;
+  double ms_total;         /* wall time of the render passes (device-synchronised) */
+  double ms_closest;       /* summed kernel time of the closest-hit kernels        */
+  double ms_shadow;        /* summed kernel time of the any-hit kernels            */
+  uint64_t closest_launches, shadow_launches;
+} yk_stats;
+
+typedef struct yk_scene yk_scene;   /* host scene + kd-tree (no GPU needed) */
+typedef struct yk_device yk_device; /* one GPU with an uploaded scene       */
+
+const char* yk_last_error(void);
+const char* yk_version(void);
+
+/* ---- host scene (scene_t geometry state machine + update) ---- */
+int yk_scene_create(yk_scene** out);
+void yk_scene_destroy(yk_scene* s);
+int yk_scene_add_material(yk_scene* s, const yk_material* m, int32_t* id_out);
+/* one TRIM mesh: points xyz (npoints*3), faces abc (nfaces*3); startTriMesh +
+ * addVertex* + addTriangle* + endTriMesh (scene.cc:265-320,520-625) */
+int yk_scene_add_mesh(yk_scene* s, const float* points, int32_t npoints, const int32_t* faces,
+                      int32_t nfaces, int32_t material, int32_t* obj_id_out);
+int yk_scene_add_light(yk_scene* s, const yk_light* l);
+int yk_scene_set_camera(yk_scene* s, const yk_camera* c);
+/* scene_t::update: gather prims and build the kd-tree (scene.cc:748-785) */
+int yk_scene_build(yk_scene* s);
+int yk_scene_info_get(const yk_scene* s, yk_scene_info* out);
+/* copy out flattened prims / tree; any pointer may be NULL */
+int yk_scene_export(const yk_scene* s, float* tri_verts, int32_t* tri_material, float* tri_normal,
+                    uint32_t* nodes, uint32_t* leaf_prims);
+int yk_scene_get_material(const yk_scene* s, int32_t i, yk_material* out);
+int yk_scene_get_light(const yk_scene* s, int32_t i, yk_light* out);
+int yk_scene_get_camera(const yk_scene* s, yk_camera* out);
+/* procedural probe scenes: "cornell" (36 tris) or "bumpy" (2*nu*(nv-1)+2 tris);
+ * fills the scene and the matching render params of BASELINE.md */
+int yk_scene_generate(yk_scene* s, const char* name, int32_t p0, int32_t p1, int32_t resx,
+                      int32_t resy, yk_render_params* params_out);
+void yk_render_params_default(yk_render_params* p);
+
+/* ---- device ---- */
+int yk_device_open(int32_t ordinal, yk_device** out);
+void yk_device_close(yk_device* d);
+int yk_device_upload(yk_device* d, const yk_scene* s);
+int yk_device_sync(yk_device* d);
+/* hipStream_t the kernels run on, as an opaque pointer (for external timing) */
+void* yk_device_stream(yk_device* d);
+
+/* batched ray queries on device memory; bit-exact with the reference
+ * triKdTree_t::Intersect (closest) and scene_t::isShadowed (any hit). */
+int yk_trace_closest(yk_device* d, const yk_ray* d_rays, int64_t n, yk_hit* d_hits, yk_stats* st);
+int yk_trace_shadow(yk_device* d, const yk_ray* d_rays, int64_t n, uint8_t* d_occluded, yk_stats* st);
+
+/* Render the tiles t with (t % nshards == shard) and accumulate the film
+ * sums (R,G,B,A,weight per pixel, width*height*5 floats, pixel-major) into
+ * d_film (device pointer, caller-allocated, caller-zeroed). */
+int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int32_t nshards,
+                    float* d_film, yk_stats* st);
+/* imageFilm_t::flush normalisation (+clampRGB0): film sums -> RGBA floats */
+int yk_film_resolve(yk_device* d, const yk_render_params* p, const float* d_film, float* d_rgba);
+/* convenience: whole frame on one device, RGBA float image to host memory */
+int yk_render(yk_device* d, const yk_render_params* p, float* rgba_host, yk_stats* st);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YK_API_H */
