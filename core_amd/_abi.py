@@ -1,0 +1,141 @@
+"""ctypes mirror of include/yk_api.h (the C-ABI of libyk.so).
+
+Loading rules: the product path loads ONLY core_amd/libyk.so (built in-tree by
+__graft_entry__.build()); there is no Python or CPU fallback. When torch is used
+in the same process it must be imported before this module so that libyk binds
+to the HIP runtime torch already loaded (same SONAME, libamdhip64.so.7).
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libyk.so")
+
+YK_OK = 0
+YK_MAT_SHINYDIFFUSE, YK_MAT_LIGHT = 0, 1
+YK_LIGHT_AREA = 0
+YK_INTEGRATOR_DIRECT, YK_INTEGRATOR_PATH = 0, 1
+YK_FILTER_BOX, YK_FILTER_MITCHELL, YK_FILTER_GAUSS, YK_FILTER_LANCZOS = 0, 1, 2, 3
+YK_CAUSTIC_NONE, YK_CAUSTIC_PATH = 0, 1
+
+f3 = C.c_float * 3
+
+
+class yk_material(C.Structure):
+    _fields_ = [("type", C.c_int32), ("color", f3), ("diffuse_reflect", C.c_float),
+                ("emit", C.c_float), ("power", C.c_float), ("double_sided", C.c_int32)]
+
+
+class yk_light(C.Structure):
+    _fields_ = [("type", C.c_int32), ("corner", f3), ("point1", f3), ("point2", f3),
+                ("color", f3), ("power", C.c_float), ("samples", C.c_int32)]
+
+
+class yk_camera(C.Structure):
+    _fields_ = [("from_", f3), ("to", f3), ("up", f3), ("resx", C.c_int32), ("resy", C.c_int32),
+                ("focal", C.c_float), ("aspect_ratio", C.c_float), ("near_clip", C.c_float),
+                ("far_clip", C.c_float)]
+
+
+class yk_render_params(C.Structure):
+    _fields_ = [("integrator", C.c_int32), ("raydepth", C.c_int32), ("path_samples", C.c_int32),
+                ("bounces", C.c_int32), ("caustic_type", C.c_int32), ("width", C.c_int32),
+                ("height", C.c_int32), ("xstart", C.c_int32), ("ystart", C.c_int32),
+                ("aa_samples", C.c_int32), ("aa_passes", C.c_int32), ("filter", C.c_int32),
+                ("aa_pixelwidth", C.c_float), ("tile_size", C.c_int32),
+                ("transp_background", C.c_int32)]
+
+    def copy(self):
+        p = yk_render_params()
+        C.pointer(p)[0] = self
+        return p
+
+
+class yk_ray(C.Structure):
+    _fields_ = [("from_", f3), ("dir", f3), ("tmin", C.c_float), ("tmax", C.c_float)]
+
+
+class yk_hit(C.Structure):
+    _fields_ = [("prim", C.c_int32), ("t", C.c_float), ("b1", C.c_float), ("b2", C.c_float)]
+
+
+class yk_scene_info(C.Structure):
+    _fields_ = [("ntris", C.c_int32), ("nmeshes", C.c_int32), ("nmaterials", C.c_int32),
+                ("nlights", C.c_int32), ("nnodes", C.c_int32), ("nleaf_prims", C.c_int32),
+                ("max_depth", C.c_int32), ("inodes", C.c_int32), ("leaves", C.c_int32),
+                ("empty_leaves", C.c_int32), ("leaf_refs", C.c_int32),
+                ("depth_limit_leaves", C.c_int32), ("bad_split_leaves", C.c_int32),
+                ("bound", C.c_float * 6), ("build_seconds", C.c_double)]
+
+
+class yk_stats(C.Structure):
+    _fields_ = [("closest_rays", C.c_uint64), ("shadow_rays", C.c_uint64),
+                ("closest_nodes", C.c_uint64), ("closest_tris", C.c_uint64),
+                ("shadow_nodes", C.c_uint64), ("shadow_tris", C.c_uint64),
+                ("camera_samples", C.c_uint64), ("ms_total", C.c_double),
+                ("ms_closest", C.c_double), ("ms_shadow", C.c_double),
+                ("closest_launches", C.c_uint64), ("shadow_launches", C.c_uint64)]
+
+
+P = C.c_void_p
+i32, i64, u32p = C.c_int32, C.c_int64, C.POINTER(C.c_uint32)
+fp, i32p = C.POINTER(C.c_float), C.POINTER(C.c_int32)
+
+# name -> (restype, argtypes); every symbol include/yk_api.h declares
+SIGNATURES = {
+    "yk_last_error": (C.c_char_p, []),
+    "yk_version": (C.c_char_p, []),
+    "yk_scene_create": (C.c_int, [C.POINTER(P)]),
+    "yk_scene_destroy": (None, [P]),
+    "yk_scene_add_material": (C.c_int, [P, C.POINTER(yk_material), i32p]),
+    "yk_scene_add_mesh": (C.c_int, [P, fp, i32, i32p, i32, i32, i32p]),
+    "yk_scene_add_light": (C.c_int, [P, C.POINTER(yk_light)]),
+    "yk_scene_set_camera": (C.c_int, [P, C.POINTER(yk_camera)]),
+    "yk_scene_build": (C.c_int, [P]),
+    "yk_scene_info_get": (C.c_int, [P, C.POINTER(yk_scene_info)]),
+    "yk_scene_export": (C.c_int, [P, fp, i32p, fp, u32p, u32p]),
+    "yk_scene_get_material": (C.c_int, [P, i32, C.POINTER(yk_material)]),
+    "yk_scene_get_light": (C.c_int, [P, i32, C.POINTER(yk_light)]),
+    "yk_scene_get_camera": (C.c_int, [P, C.POINTER(yk_camera)]),
+    "yk_scene_generate": (C.c_int, [P, C.c_char_p, i32, i32, i32, i32, C.POINTER(yk_render_params)]),
+    "yk_render_params_default": (None, [C.POINTER(yk_render_params)]),
+    "yk_device_open": (C.c_int, [i32, C.POINTER(P)]),
+    "yk_device_close": (None, [P]),
+    "yk_device_upload": (C.c_int, [P, P]),
+    "yk_device_sync": (C.c_int, [P]),
+    "yk_device_stream": (P, [P]),
+    "yk_trace_closest": (C.c_int, [P, P, i64, P, C.POINTER(yk_stats)]),
+    "yk_trace_shadow": (C.c_int, [P, P, i64, P, C.POINTER(yk_stats)]),
+    "yk_render_shard": (C.c_int, [P, C.POINTER(yk_render_params), i32, i32, P, C.POINTER(yk_stats)]),
+    "yk_film_resolve": (C.c_int, [P, C.POINTER(yk_render_params), P, P]),
+    "yk_render": (C.c_int, [P, C.POINTER(yk_render_params), fp, C.POINTER(yk_stats)]),
+}
+
+_lib = None
+
+
+class YkError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"yk error {code}: {msg}")
+        self.code = code
+
+
+def lib():
+    """Load libyk.so (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} missing: run __graft_entry__.build() (no fallback path exists)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(code):
+    if code != YK_OK:
+        raise YkError(code, lib().yk_last_error().decode())
+    return code

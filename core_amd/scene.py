@@ -1,0 +1,117 @@
+"""Host scene object over the C-ABI (scene_t geometry state machine + update).
+
+Mirrors the reference's scene assembly (scene.cc:265-320,520-625) and
+scene_t::update (scene.cc:748-850): meshes added in object-id order, the
+kd-tree built by the host builder. No GPU is needed for anything here.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _abi as A
+
+
+class Scene:
+    def __init__(self):
+        self._p = C.c_void_p()
+        A.check(A.lib().yk_scene_create(C.byref(self._p)))
+        self.params = None
+
+    def __del__(self):
+        try:
+            if self._p:
+                A.lib().yk_scene_destroy(self._p)
+                self._p = C.c_void_p()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._p
+
+    # -- assembly ------------------------------------------------------
+    def add_material(self, type_=A.YK_MAT_SHINYDIFFUSE, color=(1, 1, 1), diffuse_reflect=1.0, emit=0.0,
+                     power=1.0, double_sided=False):
+        m = A.yk_material(type_, A.f3(*color), diffuse_reflect, emit, power, int(double_sided))
+        mid = C.c_int32()
+        A.check(A.lib().yk_scene_add_material(self._p, C.byref(m), C.byref(mid)))
+        return mid.value
+
+    def add_mesh(self, points, faces, material):
+        pts = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)
+        fcs = np.ascontiguousarray(faces, dtype=np.int32).reshape(-1, 3)
+        oid = C.c_int32()
+        A.check(A.lib().yk_scene_add_mesh(self._p, pts.ctypes.data_as(A.fp), len(pts),
+                                          fcs.ctypes.data_as(A.i32p), len(fcs), material, C.byref(oid)))
+        return oid.value
+
+    def add_area_light(self, corner, point1, point2, color=(1, 1, 1), power=1.0, samples=4):
+        l = A.yk_light(A.YK_LIGHT_AREA, A.f3(*corner), A.f3(*point1), A.f3(*point2), A.f3(*color),
+                       power, samples)
+        A.check(A.lib().yk_scene_add_light(self._p, C.byref(l)))
+
+    def set_camera(self, from_, to, up, resx, resy, focal=1.0, aspect_ratio=1.0, near_clip=0.0,
+                   far_clip=-1.0):
+        c = A.yk_camera(A.f3(*from_), A.f3(*to), A.f3(*up), resx, resy, focal, aspect_ratio, near_clip,
+                        far_clip)
+        A.check(A.lib().yk_scene_set_camera(self._p, C.byref(c)))
+
+    def generate(self, name, resx, resy, p0=0, p1=0):
+        """Procedural probe scenes ("cornell_dl", "cornell_pt", "bumpy"); returns render params."""
+        p = A.yk_render_params()
+        A.check(A.lib().yk_scene_generate(self._p, name.encode(), p0, p1, resx, resy, C.byref(p)))
+        self.params = p
+        return p
+
+    def build(self):
+        A.check(A.lib().yk_scene_build(self._p))
+        return self.info()
+
+    # -- inspection ----------------------------------------------------
+    def info(self):
+        i = A.yk_scene_info()
+        A.check(A.lib().yk_scene_info_get(self._p, C.byref(i)))
+        return i
+
+    def export(self):
+        """Flattened prims + kd-tree as numpy arrays (the oracle's inputs)."""
+        i = self.info()
+        tv = np.empty((i.ntris, 9), np.float32)
+        tm = np.empty(i.ntris, np.int32)
+        tn = np.empty((i.ntris, 3), np.float32)
+        nodes = np.empty((i.nnodes, 2), np.uint32)
+        leaf = np.empty(max(i.nleaf_prims, 1), np.uint32)
+        A.check(A.lib().yk_scene_export(self._p, tv.ctypes.data_as(A.fp), tm.ctypes.data_as(A.i32p),
+                                        tn.ctypes.data_as(A.fp), nodes.ctypes.data_as(A.u32p),
+                                        leaf.ctypes.data_as(A.u32p)))
+        return dict(tri_verts=tv, tri_material=tm, tri_normal=tn, nodes=nodes, leaf_prims=leaf,
+                    bound=np.array(i.bound[:], np.float32))
+
+    def materials(self):
+        out = []
+        for k in range(self.info().nmaterials):
+            m = A.yk_material()
+            A.check(A.lib().yk_scene_get_material(self._p, k, C.byref(m)))
+            out.append(m)
+        return out
+
+    def lights(self):
+        out = []
+        for k in range(self.info().nlights):
+            l = A.yk_light()
+            A.check(A.lib().yk_scene_get_light(self._p, k, C.byref(l)))
+            out.append(l)
+        return out
+
+    def camera(self):
+        c = A.yk_camera()
+        A.check(A.lib().yk_scene_get_camera(self._p, C.byref(c)))
+        return c
+
+
+def probe_scene(name, resx, resy, nu=0, nv=0):
+    """Generate + build one of the BASELINE probe scenes."""
+    s = Scene()
+    p = s.generate(name, resx, resy, nu, nv)
+    s.build()
+    return s, p

@@ -1,0 +1,99 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, never by the product (core_amd/).
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = C.CDLL(_SO)
+        vp = C.c_void_p
+        L.orc_load.argtypes = [vp, vp, C.c_int32, vp, vp, vp, vp, C.c_int32, vp, C.c_int32, vp]
+        L.orc_intersect.argtypes = [vp, C.c_int64, vp, vp]
+        L.orc_shadow.argtypes = [vp, C.c_int64, vp, vp]
+        L.orc_render.argtypes = [vp, vp, vp, vp]
+        L.orc_camera_rays.argtypes = [C.c_int32] * 5 + [vp]
+        L.orc_scrhalton.restype = C.c_double
+        L.orc_scrhalton.argtypes = [C.c_int, C.c_uint]
+        for n in ("orc_ri_vdc", "orc_ri_s", "orc_ri_lp"):
+            getattr(L, n).restype = C.c_float
+            getattr(L, n).argtypes = [C.c_uint, C.c_uint]
+        L.orc_fnv.restype = C.c_uint
+        L.orc_fnv.argtypes = [C.c_uint]
+        L.orc_fsin.restype = C.c_float
+        L.orc_fsin.argtypes = [C.c_float]
+        L.orc_halton_seq.argtypes = [C.c_int, C.c_uint, C.c_int, vp]
+        L.orc_faure.argtypes = [C.c_int, vp]
+        _lib = L
+    return _lib
+
+
+class Oracle:
+    """Holds one scene; arrays are kept alive for the C side."""
+
+    def __init__(self, scene):
+        from core_amd import _abi as A
+        self._A = A
+        e = scene.export()
+        self.arrays = e
+        mats = scene.materials()
+        lights = scene.lights()
+        self._mats = (A.yk_material * max(len(mats), 1))(*mats)
+        self._lights = (A.yk_light * max(len(lights), 1))(*lights)
+        self._cam = scene.camera()
+        lib().orc_load(e["tri_verts"].ctypes.data, e["tri_material"].ctypes.data, len(e["tri_material"]),
+                       e["nodes"].ctypes.data, e["leaf_prims"].ctypes.data, e["bound"].ctypes.data,
+                       C.addressof(self._mats), len(mats), C.addressof(self._lights), len(lights),
+                       C.addressof(self._cam))
+
+    def render(self, params):
+        A = self._A
+        w, h = params.width, params.height
+        rgba = np.zeros((h, w, 4), np.float32)
+        sums = np.zeros((h, w, 5), np.float32)
+        counts = np.zeros(6, np.uint64)
+        rc = lib().orc_render(C.addressof(params), rgba.ctypes.data, sums.ctypes.data, counts.ctypes.data)
+        if rc:
+            raise RuntimeError(f"orc_render failed ({rc})")
+        return rgba, sums, dict(closest=int(counts[0]), shadow=int(counts[1]), closest_nodes=int(counts[2]),
+                                closest_tris=int(counts[3]), shadow_nodes=int(counts[4]),
+                                shadow_tris=int(counts[5]))
+
+    def intersect(self, rays):
+        """rays: (n,8) float32 [from, dir, tmin, tmax] -> (prim int32, t, b1, b2), counters"""
+        rays = np.ascontiguousarray(rays, np.float32)
+        n = len(rays)
+        hits = np.zeros((n, 4), np.float32)
+        cnt = np.zeros(2, np.uint64)
+        lib().orc_intersect(rays.ctypes.data, n, hits.ctypes.data, cnt.ctypes.data)
+        return hits.view(np.int32)[:, 0].copy(), hits[:, 1].copy(), hits[:, 2].copy(), hits[:, 3].copy(), cnt
+
+    def shadow(self, rays):
+        rays = np.ascontiguousarray(rays, np.float32)
+        n = len(rays)
+        occ = np.zeros(n, np.uint8)
+        cnt = np.zeros(2, np.uint64)
+        lib().orc_shadow(rays.ctypes.data, n, occ.ctypes.data, cnt.ctypes.data)
+        return occ, cnt
+
+    def camera_rays(self, x0, y0, w, h, spp):
+        out = np.zeros((h * w * spp, 8), np.float32)
+        lib().orc_camera_rays(x0, y0, w, h, spp, out.ctypes.data)
+        return out

@@ -1,0 +1,1094 @@
+/*
+ * yk_oracle.c -- CPU ORACLE (test infrastructure, not product code).
+ *
+ * A plain-C restatement of the reference (inferrna/Core = TheBounty 0.1.6)
+ * hot path: kd-tree traversal, Moller-Trumbore, surface reconstruction,
+ * perspective camera, QMC sequences, shinydiffuse/light_mat, area light,
+ * direct-light estimation, the pathtracing/directlighting integrators and the
+ * image-film splat. Used ONLY by tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py, as the checker the HIP path is compared with.
+ * The product never links, loads or calls this file.
+ *
+ * Reference build semantics. The reference is compiled with -O3 -ffast-math
+ * (CMakeLists.txt:239), and GCC reassociates several float expressions. Where
+ * the compiled instruction sequence differs from the C++ source text the
+ * restatement follows the compiled sequence (read from the disassembly of the
+ * survey session's build of the reference) and says "compiled form".
+ *
+ * Build: gcc -O2 -std=c99 -fno-fast-math -ffp-contract=off (see Makefile):
+ * IEEE binary32/binary64, no contraction, so each line below is one rounding.
+ *
+ * Parity pinning: see DESIGN.md "Oracle". The kd-tree this oracle walks comes
+ * from the product's host builder (a scene input, like the geometry); that
+ * builder reproduces the reference's recorded tree statistics exactly.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/yk_api.h"
+
+#define MIN_RAYDIST 0.00005f   /* CMakeLists.txt:43 YAF_MIN_RAY_DIST */
+#define SHADOW_BIAS 0.0005f    /* CMakeLists.txt:47 YAF_SHADOW_BIAS  */
+#define M_2PI_D 6.28318530717958647692
+#define M_PI_D 3.14159265358979323846
+#define M_1_PI_D 0.31830988618379067154
+#define KD_MAX_STACK 64
+
+/* BSDF flags, material.h:51-64 */
+#define BSDF_NONE 0x0000u
+#define BSDF_SPECULAR 0x0001u
+#define BSDF_GLOSSY 0x0002u
+#define BSDF_DIFFUSE 0x0004u
+#define BSDF_DISPERSIVE 0x0008u
+#define BSDF_REFLECT 0x0010u
+#define BSDF_TRANSMIT 0x0020u
+#define BSDF_FILTER 0x0040u
+#define BSDF_EMIT 0x0080u
+#define BSDF_ALL 0x007Fu
+
+typedef struct { float x, y, z; } v3;
+typedef struct { float r, g, b; } col3;
+
+static inline v3 V(float x, float y, float z) { v3 v = {x, y, z}; return v; }
+static inline v3 vsub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 vadd(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 vmul(float f, v3 b) { return V(f * b.x, f * b.y, f * b.z); } /* vector3d.h:155-158 */
+static inline v3 vneg(v3 a) { return V(-a.x, -a.y, -a.z); }
+static inline float vdot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; } /* vector3d.h:145-148 */
+static inline v3 vcross(v3 a, v3 b) { /* vector3d.h:185-188 */
+  return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+static inline float vget(v3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+static inline void vset(v3* a, int i, float f) { if (i == 0) a->x = f; else if (i == 1) a->y = f; else a->z = f; }
+/* vector3d_t::normalize, vector3d.h:249-260: len = 1.0/fSqrt(len) */
+static inline v3 vnormalize(v3 a) {
+  float len = a.x * a.x + a.y * a.y + a.z * a.z;
+  if (len != 0) {
+    len = 1.0f / sqrtf(len);
+    a.x *= len; a.y *= len; a.z *= len;
+  }
+  return a;
+}
+static inline col3 C(float r, float g, float b) { col3 c = {r, g, b}; return c; }
+static inline col3 cmul(col3 a, col3 b) { return C(a.r * b.r, a.g * b.g, a.b * b.b); }
+static inline col3 cscale(float f, col3 b) { return C(f * b.r, f * b.g, f * b.b); }
+static inline col3 cadd(col3 a, col3 b) { return C(a.r + b.r, a.g + b.g, a.b + b.b); }
+static inline int cblack(col3 c) { return c.r == 0 && c.g == 0 && c.b == 0; }
+
+/* ------------------------------------------------------------------ QMC -- */
+
+/* Faure permutations (faure_tables.cc): the standard Faure construction;
+ * faure[dim] is the permutation for base prims[dim] (dims 0..2 share base 3's). */
+static int g_prims[50];
+static double g_invprims[50];
+static int* g_faure[50];
+
+static void qmc_init(void) {
+  static int done = 0;
+  if (done) return;
+  g_prims[0] = 1;
+  int n = 1;
+  for (int c = 2; n < 50; ++c) {
+    int isp = 1;
+    for (int d = 2; d * d <= c; ++d)
+      if (c % d == 0) { isp = 0; break; }
+    if (isp) g_prims[n++] = c;
+  }
+  /* invPrims: 1/p written with 9 decimals (scr_halton.h:34-43) */
+  for (int i = 0; i < 50; ++i) {
+    char buf[64];
+    snprintf(buf, sizeof buf, "%.9f", 1.0 / g_prims[i]);
+    g_invprims[i] = strtod(buf, NULL);
+  }
+  int maxb = 230;
+  int** perm = (int**)calloc(maxb + 1, sizeof(int*));
+  perm[2] = (int*)malloc(2 * sizeof(int));
+  perm[2][0] = 0; perm[2][1] = 1;
+  for (int b = 3; b <= maxb; ++b) {
+    perm[b] = (int*)malloc(b * sizeof(int));
+    if (b % 2 == 0) {
+      int h = b / 2;
+      for (int i = 0; i < h; ++i) { perm[b][i] = 2 * perm[h][i]; perm[b][i + h] = 2 * perm[h][i] + 1; }
+    } else {
+      int c = (b - 1) / 2, k = 0;
+      for (int i = 0; i < b - 1; ++i) {
+        if (i == c) perm[b][k++] = c;
+        int v = perm[b - 1][i];
+        perm[b][k++] = v >= c ? v + 1 : v;
+      }
+    }
+  }
+  g_faure[0] = g_faure[1] = perm[3];
+  for (int d = 2; d < 50; ++d) g_faure[d] = perm[g_prims[d]];
+  done = 1;
+}
+
+/* scrHalton, scr_halton.h:47-69 */
+static double scrHalton(int dim, unsigned int n) {
+  double value = 0.0;
+  if (dim < 50) {
+    const int* sigma = g_faure[dim];
+    unsigned int base = (unsigned)g_prims[dim];
+    double f, factor, dn = (double)n;
+    f = factor = g_invprims[dim];
+    while (n > 0) {
+      value += (double)sigma[n % base] * factor;
+      dn *= f;
+      n = (unsigned int)dn;
+      factor *= f;
+    }
+  } else {
+    value = 0.5; /* ourRandom(): never reached for bounces < 12 */
+  }
+  if (value > 1.0) value = 1.0;
+  if (value < 1.0e-36) value = 1.0e-36;
+  return value;
+}
+
+typedef struct { unsigned base; double inv, value, fast; } halton;
+/* Halton(int base) + setStart, mcqmc.h:29-66 */
+static void hal_init(halton* h, int base) {
+  h->base = (unsigned)base;
+  h->inv = 1.0 / (double)base;
+  h->value = 0;
+  h->fast = 0.9999999999 - h->inv; /* folded constant of the compiled test */
+}
+static void hal_setstart(halton* h, unsigned int i) {
+  double factor = h->inv;
+  h->value = 0.0;
+  while (i > 0) {
+    h->value += (double)(i % h->base) * factor;
+    i /= h->base;
+    factor *= h->inv;
+  }
+}
+/* Halton::getNext, mcqmc.h:68-87, compiled form (doLightEstimation):
+ * "inv < 0.9999999999 - v" tested as "v < (0.9999999999 - inv)", and
+ * "v += hh + h - 1.0" evaluated as "(hh + h) + (v - 1.0)". */
+static float hal_next(halton* h) {
+  if (h->value < h->fast) {
+    h->value += h->inv;
+  } else {
+    double r = 0.9999999999 - h->value;
+    double hh, hv = h->inv;
+    do { hh = hv; hv *= h->inv; } while (hv >= r);
+#ifdef VAR_HAL_SRC
+    h->value += hh + hv - 1.0;
+#else
+    h->value = (hh + hv) + (h->value - 1.0);
+#endif
+  }
+  float f = (float)h->value;
+  if (f > 1.f) f = 1.f;
+  if (f < 0.f) f = 0.f;
+  return f;
+}
+
+#define MULT_RATIO 0.00000000023283064365386962890625
+static float clamp01(float f) { return f > 1.f ? 1.f : (f < 0.f ? 0.f : f); }
+/* RI_vdC, mcqmc.h:100-108 */
+static float RI_vdC(unsigned int bits, unsigned int r) {
+  bits = (bits << 16) | (bits >> 16);
+  bits = ((bits & 0x00ff00ffu) << 8) | ((bits & 0xff00ff00u) >> 8);
+  bits = ((bits & 0x0f0f0f0fu) << 4) | ((bits & 0xf0f0f0f0u) >> 4);
+  bits = ((bits & 0x33333333u) << 2) | ((bits & 0xccccccccu) >> 2);
+  bits = ((bits & 0x55555555u) << 1) | ((bits & 0xaaaaaaaau) >> 1);
+  return clamp01((float)((double)(bits ^ r) * MULT_RATIO));
+}
+/* RI_S, mcqmc.h:110-115 */
+static float RI_S(unsigned int i, unsigned int r) {
+  for (unsigned int v = 1u << 31; i; i >>= 1, v ^= v >> 1)
+    if (i & 1) r ^= v;
+  return clamp01((float)((double)r * MULT_RATIO));
+}
+/* RI_LP, mcqmc.h:117-122 */
+static float RI_LP(unsigned int i, unsigned int r) {
+  for (unsigned int v = 1u << 31; i; i >>= 1, v |= v >> 1)
+    if (i & 1) r ^= v;
+  return clamp01((float)((double)r * MULT_RATIO));
+}
+/* fnv_32a_buf, mcqmc.h:155-168 (little-endian byte order) */
+static unsigned int fnv_32a_buf(unsigned int value) {
+  unsigned int hash = 0x811c9dc5u;
+  for (int i = 0; i < 4; i++) {
+    hash ^= (value >> (8 * i)) & 0xffu;
+    hash *= 0x01000193u;
+  }
+  return hash;
+}
+
+/* FAST_TRIG fSin, mathOptimizations.h:249-268, compiled form (the inlined copy
+ * in shinyDiffuseMat_t::sample): "CONST_P*(x|x|-x)+x" is evaluated as
+ * "x + (|x|-1)*(CONST_P*x)", then clamped with minss/maxss. */
+static float fSin(float x) {
+  if ((double)x > M_2PI_D || (double)x < -M_2PI_D) x -= (float)((int)(x * (float)0.15915494309189533577)) * (float)M_2PI_D;
+  if ((double)x < -M_PI_D) x += (float)M_2PI_D;
+  else if ((double)x > M_PI_D) x -= (float)M_2PI_D;
+  x = ((float)1.27323954473516268615 * x) - (((float)0.40528473456935108578 * x) * fabsf(x));
+#ifdef VAR_FSIN_SRC
+  float r = 0.225f * (x * fabsf(x) - x) + x;
+#else
+  float r = x + (fabsf(x) - 1.0f) * (0.225f * x);
+#endif
+  if (r > 1.0f) r = 1.0f;
+  if (r < -1.0f) r = -1.0f;
+  return r;
+}
+static float fCos(float x) { return fSin(x + (float)1.57079632679489661923); }
+
+/* ---------------------------------------------------------------- scene -- */
+
+typedef struct {
+  int ntris;
+  const float* tv;        /* 9 floats / prim                  */
+  const int32_t* tmat;
+  v3* ng;                 /* recNormal per prim (computed here) */
+  const uint32_t* nodes;  /* 2 words / node                    */
+  const uint32_t* leaf;
+  float bound[6];
+  int nmats;
+  yk_material* mats;
+  int nlights;
+  yk_light* lights;
+  yk_camera cam;
+  /* derived area-light data, areaLight_t ctor arealight.cc:30-49 */
+  struct arealight {
+    v3 corner, c2, c3, c4, toX, toY, fnormal, normal;
+    col3 color;
+    float area, inv_area;
+    int samples;
+  } * al;
+  /* derived camera data, camera.h:41-60 + perspectiveCamera.cc:28-71 */
+  v3 cam_pos, vright, vup, vto, camZ;
+  v3 near_p, far_p;
+} oscene;
+
+static oscene G;
+
+/* counters (reference: scene_t::intersect / isShadowed calls) */
+static uint64_t g_nclosest, g_nshadow, g_nodes_c, g_tris_c, g_nodes_s, g_tris_s;
+
+static v3 tri_vert(int p, int k) {
+  const float* t = G.tv + 9 * (size_t)p + 3 * k;
+  return V(t[0], t[1], t[2]);
+}
+
+/* triangle_t::intersect, triangle_inline.h:27-64 */
+static int tri_intersect(int p, v3 from, v3 dir, float* t, float* b1, float* b2) {
+  v3 a = tri_vert(p, 0), b = tri_vert(p, 1), c = tri_vert(p, 2);
+  v3 e1 = vsub(b, a), e2 = vsub(c, a);
+  v3 pvec = vcross(dir, e2);
+  float det = vdot(e1, pvec);
+  if (det == 0.0f) return 0;
+  float inv_det = 1.0f / det;
+  v3 tvec = vsub(from, a);
+  float u = vdot(tvec, pvec) * inv_det;
+  if (u < 0.0f || u > 1.0f) return 0;
+  v3 qvec = vcross(tvec, e1);
+  float v = vdot(dir, qvec) * inv_det;
+  if (v < 0.0f || (u + v) > 1.0f) return 0;
+  *t = vdot(e2, qvec) * inv_det;
+  *b1 = u;
+  *b2 = v;
+  return 1;
+}
+
+/* bound_t::cross (Smits), bound.h:148-204 */
+static int bound_cross(v3 from, v3 dir, float* enter, float* leave, float dist) {
+  const float* bb = G.bound;
+  float lmin = -1e38f, lmax = 1e38f, ltmin, ltmax;
+  for (int ax = 0; ax < 3; ++ax) {
+    float d = vget(dir, ax);
+    if (d != 0) {
+      float invr = 1.0f / d;
+      /* compiled form: -p*invr = (a0-from)*invr (exact), and
+       * ((a1-a0)-p)*invr is simplified to (a1-from)*invr */
+      float t0 = (bb[ax] - vget(from, ax)) * invr, t1 = (bb[3 + ax] - vget(from, ax)) * invr;
+      if (invr > 0) { ltmin = t0; ltmax = t1; }
+      else { ltmin = t1; ltmax = t0; }
+      if (ax == 0) { lmin = ltmin; lmax = ltmax; }
+      else {
+        lmin = (ltmin < lmin) ? lmin : ltmin; /* std::max(ltmin,lmin) */
+        lmax = (lmax < ltmax) ? lmax : ltmax; /* std::min(ltmax,lmax) */
+      }
+      if ((lmax < 0) || (lmin > dist)) return 0;
+    }
+  }
+  if ((lmin <= lmax) && (lmax >= 0) && (lmin <= dist)) {
+    *enter = lmin;
+    *leave = lmax;
+    return 1;
+  }
+  return 0;
+}
+
+typedef struct { int node; float t; v3 pb; int prev; } kdstack;
+
+/* descend-and-leaf loop shared by Intersect / IntersectS (kdtree.cc:675-947).
+ * closest=1: accept t<Z && t>=tmin, stop when hit && Z<=exit.t
+ * closest=0: return at the first t<dist && t>=0 */
+static int kd_traverse(v3 from, v3 dir, float tmin, float dist, int closest, int* hprim, float* Z,
+                       float* hb1, float* hb2, uint64_t* nnodes, uint64_t* ntris) {
+  float a, b, t, t_hit, b1, b2;
+  if (closest) *Z = dist;
+  if (!bound_cross(from, dir, &a, &b, dist)) return 0;
+  v3 invDir = V(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+  int hit = 0;
+  kdstack stack[KD_MAX_STACK + 2];
+  int currNode = 0, farChild;
+  int enPt = 0;
+  stack[enPt].t = a;
+  if (a >= 0.0f) stack[enPt].pb = vadd(from, vmul(a, dir));
+  else stack[enPt].pb = from;
+  int exPt = 1;
+  stack[exPt].t = b;
+  stack[exPt].pb = vadd(from, vmul(b, dir));
+  stack[exPt].node = -1;
+  float cb1 = 0, cb2 = 0;
+  while (currNode != -1) {
+    if (dist < stack[enPt].t) break;
+    (*nnodes)++;
+    while ((G.nodes[2 * currNode + 1] & 3u) != 3u) {
+      int axis = (int)(G.nodes[2 * currNode + 1] & 3u);
+      float splitVal;
+      memcpy(&splitVal, &G.nodes[2 * currNode], 4);
+      int right = (int)(G.nodes[2 * currNode + 1] >> 2);
+      if (vget(stack[enPt].pb, axis) <= splitVal) {
+        if (vget(stack[exPt].pb, axis) <= splitVal) { currNode++; (*nnodes)++; continue; }
+        if (vget(stack[exPt].pb, axis) == splitVal) { currNode = right; (*nnodes)++; continue; }
+        farChild = right;
+        currNode++;
+      } else {
+        if (splitVal < vget(stack[exPt].pb, axis)) { currNode = right; (*nnodes)++; continue; }
+        farChild = currNode + 1;
+        currNode = right;
+      }
+      (*nnodes)++;
+      t = (splitVal - vget(from, axis)) * vget(invDir, axis);
+      int tmp = exPt;
+      exPt++;
+      if (exPt == enPt) exPt++;
+      static const int npAxis[2][3] = {{1, 2, 0}, {2, 0, 1}};
+      int nextAxis = npAxis[0][axis], prevAxis = npAxis[1][axis];
+      stack[exPt].prev = tmp;
+      stack[exPt].t = t;
+      stack[exPt].node = farChild;
+      vset(&stack[exPt].pb, axis, splitVal);
+      vset(&stack[exPt].pb, nextAxis, vget(from, nextAxis) + t * vget(dir, nextAxis));
+      vset(&stack[exPt].pb, prevAxis, vget(from, prevAxis) + t * vget(dir, prevAxis));
+    }
+    uint32_t w0 = G.nodes[2 * currNode], n = G.nodes[2 * currNode + 1] >> 2;
+    for (uint32_t i = 0; i < n; ++i) {
+      int p = (int)(n == 1 ? w0 : G.leaf[w0 + i]);
+      (*ntris)++;
+      if (tri_intersect(p, from, dir, &t_hit, &b1, &b2)) {
+        if (closest) {
+          if (t_hit < *Z && t_hit >= tmin) {
+            *Z = t_hit;
+            *hprim = p;
+            cb1 = b1;
+            cb2 = b2;
+            hit = 1;
+          }
+        } else if (t_hit < dist && t_hit >= 0.f) {
+          *hprim = p;
+          return 1;
+        }
+      }
+    }
+    if (closest && hit && *Z <= stack[exPt].t) {
+      *hb1 = cb1;
+      *hb2 = cb2;
+      return 1;
+    }
+    enPt = exPt;
+    currNode = stack[exPt].node;
+    exPt = stack[enPt].prev;
+  }
+  if (closest && hit) { *hb1 = cb1; *hb2 = cb2; }
+  return hit;
+}
+
+typedef struct {
+  v3 P, N, Ng, NU, NV;
+  int prim, mat;
+} surfpt;
+
+/* createCS, vector3d.h:316-334 */
+static void createCS(v3 N, v3* u, v3* v) {
+  if ((N.x == 0) && (N.y == 0)) {
+    *u = (N.z < 0) ? V(-1, 0, 0) : V(1, 0, 0);
+    *v = V(0, 1, 0);
+  } else {
+    float d = 1.0f / sqrtf(N.y * N.y + N.x * N.x);
+    *u = V(N.y * d, -N.x * d, 0);
+    *v = vcross(N, *u);
+  }
+}
+
+/* scene_t::intersect (scene.cc:852-879) + triangle_t::getSurface
+ * (triangle.cc:12-108, flat-shaded subset). Returns hit, sets ray tmax. */
+static int scene_intersect(v3 from, v3 dir, float tmin, float* tmax, surfpt* sp) {
+  g_nclosest++;
+  float dis = (*tmax < 0) ? INFINITY : *tmax, Z, b1 = 0, b2 = 0;
+  int prim = -1;
+  if (!kd_traverse(from, dir, tmin, dis, 1, &prim, &Z, &b1, &b2, &g_nodes_c, &g_tris_c)) return 0;
+  sp->P = vadd(from, vmul(Z, dir));
+  sp->Ng = G.ng[prim];
+  sp->N = sp->Ng;
+  createCS(sp->N, &sp->NU, &sp->NV);
+  sp->prim = prim;
+  sp->mat = G.tmat[prim];
+  *tmax = Z;
+  return 1;
+}
+
+/* scene_t::isShadowed, scene.cc:881-902 */
+static int scene_shadowed(v3 from, v3 dir, float tmin, float tmax) {
+  g_nshadow++;
+  v3 f = vadd(from, vmul(tmin, dir));
+  float dis = (tmax < 0) ? INFINITY : tmax - 2.0f * tmin;
+  int prim;
+  return kd_traverse(f, dir, 0.f, dis, 0, &prim, NULL, NULL, NULL, &g_nodes_s, &g_tris_s);
+}
+
+/* ------------------------------------------------------------- camera -- */
+
+static void camera_setup(void) {
+  const yk_camera* c = &G.cam;
+  v3 pos = V(c->from[0], c->from[1], c->from[2]);
+  v3 look = V(c->to[0], c->to[1], c->to[2]);
+  v3 up = V(c->up[0], c->up[1], c->up[2]);
+  float aspect = c->aspect_ratio * (float)c->resy / (float)c->resx; /* camera.h:44 */
+  v3 camY = vsub(up, pos), camZ = vsub(look, pos);
+  v3 camX = vcross(camZ, camY);
+  camY = vcross(camZ, camX);
+  camX = vnormalize(camX);
+  camY = vnormalize(camY);
+  camZ = vnormalize(camZ);
+  G.near_p = vadd(pos, vmul(c->near_clip, camZ));
+  G.far_p = vadd(pos, vmul(c->far_clip, camZ));
+  G.camZ = camZ;
+  G.cam_pos = pos;
+  /* perspectiveCam_t::setAxis, perspectiveCamera.cc:57-71 */
+  v3 vright = camX, vup = vmul(aspect, camY);
+  v3 vto = vsub(vmul(c->focal, camZ), vmul(0.5f, vadd(vup, vright)));
+  /* compiled form: "vup /= resy" -> vup *= (1.0f/resy) (reciprocal CSE) */
+  float ry = 1.0f / (float)c->resy, rx = 1.0f / (float)c->resx;
+  G.vup = V(vup.x * ry, vup.y * ry, vup.z * ry);
+  G.vright = V(vright.x * rx, vright.y * rx, vright.z * rx);
+  G.vto = vto;
+}
+
+/* perspectiveCam_t::shootRay, perspectiveCamera.cc:127-149 (no DOF) */
+static void camera_ray(float px, float py, v3* from, v3* dir, float* tmin, float* tmax) {
+  *from = G.cam_pos;
+  v3 d = vadd(vadd(vmul(px, G.vright), vmul(py, G.vup)), G.vto);
+  d = vnormalize(d);
+  *dir = d;
+  /* ray_plane_intersection, geometry.h:33-36 */
+  *tmin = vdot(G.camZ, vsub(G.near_p, *from)) / vdot(d, G.camZ);
+  *tmax = vdot(G.camZ, vsub(G.far_p, *from)) / vdot(d, G.camZ);
+}
+
+/* --------------------------------------------------------- materials -- */
+
+static const yk_material* mat_of(int m) { return &G.mats[m]; }
+
+static unsigned mat_flags(int m) {
+  const yk_material* M = mat_of(m);
+  if (M->type == YK_MAT_LIGHT) return BSDF_EMIT;
+  unsigned f = 0;
+  if (M->emit > 0.f) f |= BSDF_EMIT;
+  if (M->diffuse_reflect > 0.00001f) f |= BSDF_DIFFUSE | BSDF_REFLECT;
+  return f;
+}
+
+/* shinyDiffuseMat_t::eval (diffuse subset), shinydiffuse.cc:223-249 */
+static col3 sd_eval(const yk_material* M, const surfpt* sp, v3 wo, v3 wl, unsigned bsdfs) {
+  if (M->type == YK_MAT_LIGHT) return C(0, 0, 0);
+  v3 N = (vdot(sp->Ng, wo) < 0) ? vneg(sp->N) : sp->N;
+  if (!(bsdfs & BSDF_DIFFUSE) || M->diffuse_reflect <= 0.00001f) return C(0, 0, 0);
+  float mT = (1.f - 1.f * 0.f) * (1.f - 0.f);
+  if (vdot(N, wl) < 0.0f) return C(0, 0, 0);
+  float mD = mT * (1.f - 0.f) * M->diffuse_reflect;
+  return cscale(mD, C(M->color[0], M->color[1], M->color[2]));
+}
+
+/* SampleCosHemisphere, sample_utils.h:41-49 */
+static v3 sample_cos_hemisphere(v3 N, v3 Ru, v3 Rv, float s1, float s2) {
+  if (s1 >= 1.0f) return N;
+  float z1 = s1;
+  float z2 = (float)((double)s2 * M_2PI_D);
+  float c = fCos(z2), s = fSin(z2);
+  float sq1 = sqrtf(1.0f - z1), sqz = sqrtf(z1);
+  return vadd(vmul(sq1, vadd(vmul(c, Ru), vmul(s, Rv))), vmul(sqz, N));
+}
+
+/* shinyDiffuseMat_t::sample (diffuse-reflect component), shinydiffuse.cc:259-336 */
+static col3 sd_sample(const yk_material* M, const surfpt* sp, v3 wo, v3* wi, float s1in, float s2in,
+                      unsigned flags, float* pdf, float* W, int* ok) {
+  *ok = 1;
+  if (M->type == YK_MAT_LIGHT) { /* lightMat_t::sample, simple.cc:47-52 */
+    *pdf = 0.f;
+    *W = 0.f;
+    return C(0, 0, 0);
+  }
+  float cos_Ng_wo = vdot(sp->Ng, wo);
+  v3 N = (cos_Ng_wo < 0) ? vneg(sp->N) : sp->N;
+  float accum3 = M->diffuse_reflect * (((1.f - 0.f * 1.f) * (1.f - 0.f)) * (1.f - 0.f));
+  const unsigned cf = BSDF_DIFFUSE | BSDF_REFLECT;
+  if (M->diffuse_reflect <= 0.00001f || (flags & cf) != cf) {
+    *pdf = 0.f;
+    *ok = 0; /* W untouched, as the reference */
+    return C(1.f, 1.f, 1.f);
+  }
+  float width = accum3, sum = 0.f + width, val = sum;
+  if (sum < 0.00001f) { *pdf = 0.f; *ok = 0; return C(1.f, 1.f, 1.f); }
+  float inv_sum = 1.f / sum;
+  val *= inv_sum;
+  width *= inv_sum;
+  (void)val;
+  float s1 = s1in / width;
+  *wi = sample_cos_hemisphere(N, sp->NU, sp->NV, s1, s2in);
+  float cos_Ng_wi = vdot(sp->Ng, *wi);
+  col3 sc = C(0, 0, 0);
+  if (cos_Ng_wo * cos_Ng_wi > 0) sc = cscale(accum3, C(M->color[0], M->color[1], M->color[2]));
+  *pdf = fabsf(vdot(*wi, N)) * width;
+  *W = fabsf(vdot(*wi, sp->N)) / (*pdf * 0.99f + 0.01f);
+  return sc;
+}
+
+/* shinyDiffuseMat_t::pdf, shinydiffuse.cc:338-377 */
+static float sd_pdf(const yk_material* M, const surfpt* sp, v3 wo, v3 wi, unsigned bsdfs) {
+  if (M->type == YK_MAT_LIGHT) return 0.f;
+  if (!(bsdfs & BSDF_DIFFUSE)) return 0.f;
+  v3 N = (vdot(sp->Ng, wo) < 0) ? vneg(sp->N) : sp->N;
+  if (M->diffuse_reflect <= 0.00001f) return 0.f;
+  float width = M->diffuse_reflect * (((1.f - 0.f * 1.f) * (1.f - 0.f)) * (1.f - 0.f));
+  float sum = 0.f + width;
+  float pdf = 0.f + fabsf(vdot(wi, N)) * width;
+  if (sum < 0.00001f) return 0.f;
+  return pdf / sum;
+}
+
+/* emit: shinyDiffuseMat_t::emit (shinydiffuse.cc:251-257), lightMat_t::emit
+ * (simple.cc:54-61) */
+static col3 mat_emit(const yk_material* M, const surfpt* sp, v3 wo, int includeLights) {
+  if (M->type == YK_MAT_LIGHT) {
+    if (!includeLights) return C(0, 0, 0);
+    col3 lc = C(M->color[0] * M->power, M->color[1] * M->power, M->color[2] * M->power);
+    if (M->double_sided) return lc;
+    float angle = vdot(wo, sp->N);
+    return (angle > 0) ? lc : C(0, 0, 0);
+  }
+  return cscale(M->emit, C(M->color[0], M->color[1], M->color[2]));
+}
+
+/* -------------------------------------------------------------- light -- */
+
+/* triIntersect, arealight.cc:98-115 */
+static int tri_isect_pts(v3 a, v3 b, v3 c, v3 from, v3 dir, float* t) {
+  v3 e1 = vsub(b, a), e2 = vsub(c, a);
+  v3 pvec = vcross(dir, e2);
+  float det = vdot(e1, pvec);
+  if (det == 0.0f) return 0;
+  float inv_det = 1.0f / det;
+  v3 tvec = vsub(from, a);
+  float u = vdot(tvec, pvec) * inv_det;
+  if (u < 0.0f || u > 1.0f) return 0;
+  v3 qvec = vcross(tvec, e1);
+  float v = vdot(dir, qvec) * inv_det;
+  if ((v < 0.0f) || ((u + v) > 1.0f)) return 0;
+  *t = vdot(e2, qvec) * inv_det;
+  return 1;
+}
+
+static void lights_setup(void) {
+  G.al = (struct arealight*)calloc(G.nlights > 0 ? G.nlights : 1, sizeof *G.al);
+  for (int i = 0; i < G.nlights; ++i) {
+    const yk_light* L = &G.lights[i];
+    struct arealight* A = &G.al[i];
+    v3 corner = V(L->corner[0], L->corner[1], L->corner[2]);
+    v3 p1 = V(L->point1[0], L->point1[1], L->point1[2]);
+    v3 p2 = V(L->point2[0], L->point2[1], L->point2[2]);
+    A->corner = corner;
+    A->toX = vsub(p1, corner);
+    A->toY = vsub(p2, corner);
+    A->fnormal = vcross(A->toY, A->toX);
+    col3 ci = C(L->color[0] * L->power, L->color[1] * L->power, L->color[2] * L->power);
+    A->color = cscale((float)M_PI_D, ci);
+    /* fnormal.normLen(), vector3d.h:61-70 */
+    v3 f = A->fnormal;
+    float vl = f.x * f.x + f.y * f.y + f.z * f.z;
+    if (vl != 0.0f) {
+      vl = sqrtf(vl);
+      float d = 1.0f / vl;
+      f.x *= d; f.y *= d; f.z *= d;
+    }
+    A->fnormal = f;
+    A->area = vl;
+    A->inv_area = 1.0f / vl;
+    A->normal = vneg(f);
+    A->c2 = vadd(corner, A->toX);
+    A->c3 = vadd(corner, vadd(A->toX, A->toY));
+    A->c4 = vadd(corner, A->toY);
+    A->samples = L->samples;
+  }
+}
+
+/* areaLight_t::illumSample, arealight.cc:68-96 */
+static int al_illum_sample(const struct arealight* A, v3 P, float s1, float s2, v3* ldir_out, float* tmax,
+                           col3* col, float* pdf) {
+  /* compiled form: x,y as corner + (s1*toX + s2*toY); z in source order
+   * (corner + s1*toX) + s2*toY */
+  v3 p = V(A->corner.x + (s1 * A->toX.x + s2 * A->toY.x), A->corner.y + (s1 * A->toX.y + s2 * A->toY.y),
+           (A->corner.z + s1 * A->toX.z) + s2 * A->toY.z);
+  v3 ldir = vsub(p, P);
+  float dist_sqr = ldir.x * ldir.x + ldir.y * ldir.y + ldir.z * ldir.z;
+  float dist = sqrtf(dist_sqr);
+  if (dist <= 0.0f) return 0;
+  float id = 1.f / dist;
+  ldir = V(ldir.x * id, ldir.y * id, ldir.z * id);
+  float cos_angle = vdot(ldir, A->fnormal);
+  if (cos_angle <= 0) return 0;
+  *tmax = dist;
+  *ldir_out = ldir;
+  *col = A->color;
+  *pdf = (float)((double)dist_sqr * M_PI_D / (double)(A->area * cos_angle));
+  return 1;
+}
+
+/* areaLight_t::intersect, arealight.cc:138-154 */
+static int al_intersect(const struct arealight* A, v3 from, v3 dir, float* t, col3* col, float* ipdf) {
+  float cos_angle = vdot(dir, A->fnormal);
+  if (cos_angle <= 0) return 0;
+  if (!tri_isect_pts(A->corner, A->c2, A->c3, from, dir, t)) {
+    if (!tri_isect_pts(A->corner, A->c3, A->c4, from, dir, t)) return 0;
+  }
+  if (!(*t > 1.0e-10f)) return 0;
+  *col = A->color;
+  *ipdf = (float)((double)((1.f / (*t * *t)) * A->area * cos_angle) * M_1_PI_D);
+  return 1;
+}
+
+/* ------------------------------------------------------ integrators -- */
+
+typedef struct {
+  int pixelSample;
+  unsigned int samplingOffs;
+  int includeLights;
+} rstate;
+
+/* mcIntegrator_t::doLightEstimation (area-light branch), mcintegrator.cc:73-195 */
+static col3 do_light_estimation(rstate* st, int li, const surfpt* sp, v3 wo, unsigned loffs) {
+  col3 col = C(0, 0, 0);
+  const struct arealight* A = &G.al[li];
+  const yk_material* M = mat_of(sp->mat);
+  unsigned l_offs = loffs * 4567u;
+  int n = A->samples;
+  float invNS = 1.f / (float)n;
+  unsigned offs = (unsigned)(n * st->pixelSample) + st->samplingOffs + l_offs;
+  halton h2, h3;
+  hal_init(&h2, 2);
+  hal_init(&h3, 3);
+  col3 ccol = C(0, 0, 0);
+  hal_setstart(&h2, offs - 1);
+  hal_setstart(&h3, offs - 1);
+  for (int i = 0; i < n; ++i) {
+    float s1 = hal_next(&h2), s2 = hal_next(&h3);
+    v3 ldir;
+    float ltmax, lpdf;
+    col3 lcol;
+    if (al_illum_sample(A, sp->P, s1, s2, &ldir, &ltmax, &lcol, &lpdf)) {
+      int shadowed = scene_shadowed(sp->P, ldir, SHADOW_BIAS, ltmax);
+      if (!shadowed && lpdf > 1e-6f) {
+        col3 surf = sd_eval(M, sp, wo, ldir, BSDF_ALL);
+        float mPdf = sd_pdf(M, sp, wo, ldir, BSDF_GLOSSY | BSDF_DIFFUSE | BSDF_DISPERSIVE | BSDF_REFLECT | BSDF_TRANSMIT);
+        /* compiled form: ((surf*lcol) * (|N.l| * (1/pdf))) [* w] */
+        float k = fabsf(vdot(sp->N, ldir)) * (1.0f / lpdf);
+        col3 sl = cmul(surf, lcol);
+        if (mPdf > 1e-6f) {
+          float l2 = lpdf * lpdf, m2 = mPdf * mPdf;
+          float w = l2 / (l2 + m2);
+          ccol = cadd(ccol, C((sl.r * k) * w, (sl.g * k) * w, (sl.b * k) * w));
+        } else {
+          ccol = cadd(ccol, C(sl.r * k, sl.g * k, sl.b * k));
+        }
+      }
+    }
+  }
+  col = cadd(col, cscale(invNS, ccol));
+  /* MIS: sample the BSDF, mcintegrator.cc:156-192 */
+  col3 ccol2 = C(0, 0, 0);
+  hal_setstart(&h2, offs - 1);
+  hal_setstart(&h3, offs - 1);
+  for (int i = 0; i < n; ++i) {
+    float s1 = hal_next(&h2), s2 = hal_next(&h3);
+    float W = 0.f, spdf = 0.f;
+    int ok;
+    v3 bdir = V(0, 0, 0);
+    col3 surf = sd_sample(M, sp, wo, &bdir, s1, s2,
+                          BSDF_GLOSSY | BSDF_DIFFUSE | BSDF_DISPERSIVE | BSDF_REFLECT | BSDF_TRANSMIT, &spdf, &W, &ok);
+    float bt, lightPdf;
+    col3 lcol;
+    if (spdf > 1e-6f && al_intersect(A, sp->P, bdir, &bt, &lcol, &lightPdf)) {
+      int shadowed = scene_shadowed(sp->P, bdir, MIN_RAYDIST, bt);
+      if (!shadowed && lightPdf > 1e-6f) {
+        float lPdf = 1.f / lightPdf;
+        float l2 = lPdf * lPdf, m2 = spdf * spdf;
+        float w = m2 / (l2 + m2);
+        /* compiled form of "surfCol * lcol * w * W": R,G as ((surf*W)*lcol)*w,
+         * B as (surf*W)*(w*lcol) (SLP-vectorised pair + scalar lane) */
+#ifdef VAR_MIS_SRC
+        ccol2 = cadd(ccol2, C(((surf.r * lcol.r) * w) * W, ((surf.g * lcol.g) * w) * W, ((surf.b * lcol.b) * w) * W));
+#else
+        ccol2 = cadd(ccol2, C(((surf.r * W) * lcol.r) * w, ((surf.g * W) * lcol.g) * w, (surf.b * W) * (w * lcol.b)));
+#endif
+      }
+    }
+  }
+  col = cadd(col, cscale(invNS, ccol2));
+  return col;
+}
+
+static col3 estimate_all_direct(rstate* st, const surfpt* sp, v3 wo) {
+  col3 col = C(0, 0, 0);
+  unsigned loffs = 0;
+  for (int l = 0; l < G.nlights; ++l) {
+    col = cadd(col, do_light_estimation(st, l, sp, wo, loffs));
+    loffs++;
+  }
+  return col;
+}
+
+static col3 estimate_one_direct(rstate* st, const surfpt* sp, v3 wo, int n) {
+  int lightNum = G.nlights;
+  if (lightNum == 0) return C(0, 0, 0);
+  halton h2;
+  hal_init(&h2, 2);
+  hal_setstart(&h2, (unsigned)(n - 1));
+  int lnum = (int)(hal_next(&h2) * (float)lightNum);
+  if (lnum > lightNum - 1) lnum = lightNum - 1;
+  col3 c = do_light_estimation(st, lnum, sp, wo, (unsigned)lnum);
+  return cscale((float)lightNum, c);
+}
+
+typedef struct { float r, g, b, a; } rgba;
+
+/* pathIntegrator_t::integrate, pathtracer.cc:134-333 */
+static rgba pt_integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir, float tmin, float tmax) {
+  col3 col = C(0, 0, 0);
+  float alpha = P->transp_background ? 0.0f : 1.0f;
+  surfpt sp;
+  if (scene_intersect(from, dir, tmin, &tmax, &sp)) {
+    st->includeLights = 1;
+    const yk_material* M = mat_of(sp.mat);
+    unsigned bsdfs = mat_flags(sp.mat);
+    v3 wo = vneg(dir);
+    if (bsdfs & BSDF_EMIT) col = cadd(col, mat_emit(M, &sp, wo, st->includeLights));
+    if (bsdfs & BSDF_DIFFUSE) col = cadd(col, estimate_all_direct(st, &sp, wo));
+    if (bsdfs & BSDF_DIFFUSE) {
+      col3 pathCol = C(0, 0, 0);
+      unsigned path_flags = BSDF_DIFFUSE | BSDF_REFLECT | BSDF_TRANSMIT;
+      int nSamples = P->path_samples > 1 ? P->path_samples : 1;
+      float W = 0.f;
+      for (int i = 0; i < nSamples; ++i) {
+        unsigned offs = (unsigned)(P->path_samples * st->pixelSample) + st->samplingOffs + (unsigned)i;
+        col3 throughput, lcol, scol;
+        surfpt hit;
+        v3 pwo = wo, pdir = V(0, 0, 0);
+        float s1 = RI_vdC(offs, 0);
+        float s2 = (float)scrHalton(2, offs);
+        float spdf;
+        int ok;
+        scol = sd_sample(M, &sp, pwo, &pdir, s1, s2, path_flags, &spdf, &W, &ok);
+        scol = cscale(W, scol);
+        throughput = scol;
+        st->includeLights = 0;
+        float ptmax = -1.0f;
+        if (!scene_intersect(sp.P, pdir, MIN_RAYDIST, &ptmax, &hit)) continue;
+        const yk_material* pm = mat_of(hit.mat);
+        unsigned matBSDFs = mat_flags(hit.mat);
+        pwo = vneg(pdir);
+        lcol = estimate_one_direct(st, &hit, pwo, (int)offs);
+        if (matBSDFs & BSDF_EMIT) lcol = cadd(lcol, mat_emit(pm, &hit, pwo, st->includeLights));
+        pathCol = cadd(pathCol, cmul(lcol, throughput));
+        for (int depth = 1; depth < P->bounces; ++depth) {
+          int d4 = 4 * depth;
+          float ss1 = (float)scrHalton(d4 + 3, offs);
+          float ss2 = (float)scrHalton(d4 + 4, offs);
+          scol = sd_sample(pm, &hit, pwo, &pdir, ss1, ss2, BSDF_ALL, &spdf, &W, &ok);
+          scol = cscale(W, scol);
+          if (cblack(scol)) break;
+          throughput = cmul(throughput, scol);
+          st->includeLights = 0; /* caustic = traceCaustics && ... ; NONE/diffuse -> false */
+          surfpt hit2;
+          ptmax = -1.0f;
+          if (!scene_intersect(hit.P, pdir, MIN_RAYDIST, &ptmax, &hit2)) break;
+          hit = hit2;
+          pm = mat_of(hit.mat);
+          matBSDFs = mat_flags(hit.mat);
+          pwo = vneg(pdir);
+          if (matBSDFs & BSDF_DIFFUSE) lcol = estimate_one_direct(st, &hit, pwo, (int)offs);
+          else lcol = C(0, 0, 0);
+          /* "matBSDFs & (BSDF_EMIT && caustic)": caustic is false here */
+          pathCol = cadd(pathCol, cmul(lcol, throughput));
+        }
+      }
+      float ns = (float)nSamples;
+      col = cadd(col, C(pathCol.r / ns, pathCol.g / ns, pathCol.b / ns));
+    }
+    alpha = 1.0f; /* getAlpha of opaque shinydiffuse/light_mat = 1 */
+  }
+  rgba r = {col.r, col.g, col.b, alpha};
+  return r;
+}
+
+/* directLighting_t::integrate, directlight.cc:112-182 */
+static rgba dl_integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir, float tmin, float tmax) {
+  col3 col = C(0, 0, 0);
+  float alpha = P->transp_background ? 0.0f : 1.0f;
+  surfpt sp;
+  if (scene_intersect(from, dir, tmin, &tmax, &sp)) {
+    const yk_material* M = mat_of(sp.mat);
+    unsigned bsdfs = mat_flags(sp.mat);
+    v3 wo = vneg(dir);
+    st->includeLights = 1;
+    if (bsdfs & BSDF_EMIT) col = cadd(col, mat_emit(M, &sp, wo, st->includeLights));
+    if (bsdfs & BSDF_DIFFUSE) col = cadd(col, estimate_all_direct(st, &sp, wo));
+    alpha = 1.0f;
+  }
+  rgba r = {col.r, col.g, col.b, alpha};
+  return r;
+}
+
+/* ------------------------------------------------------------- film -- */
+
+#define FILTER_TABLE_SIZE 16
+#define MAX_FILTER_SIZE 8
+static float f_box(float dx, float dy) { (void)dx; (void)dy; return 1.f; }
+static float f_mitchell(float dx, float dy) {
+  float x = 2.f * sqrtf(dx * dx + dy * dy);
+  if (x >= 2.f) return 0.f;
+  if (x >= 1.f) return (float)(x * (x * (x * -0.38888889f + 2.0f) - 3.33333333f) + 1.77777778f);
+  return (float)(x * x * (1.16666666f * x - 2.0f) + 0.88888889f);
+}
+
+static inline int Round2Int(double v) { return (int)(v + (0.5 - 1.4e-11)); } /* math_utils.h:60-68 (x86-64) */
+static inline int Floor2Int(double v) { return (int)floor(v); }
+
+typedef struct {
+  int w, h, cx0, cy0, cx1, cy1;
+  float filterw;
+  double tableScale;
+  float table[FILTER_TABLE_SIZE * FILTER_TABLE_SIZE];
+  float* acc; /* 5 floats per pixel: R G B A weight */
+} film_t;
+
+static void film_init(film_t* F, const yk_render_params* P) {
+  F->w = P->width; F->h = P->height; F->cx0 = P->xstart; F->cy0 = P->ystart;
+  F->cx1 = P->xstart + P->width; F->cy1 = P->ystart + P->height;
+  F->filterw = (float)((double)P->aa_pixelwidth * 0.5);
+  float (*ff)(float, float) = f_box;
+  if (P->filter == YK_FILTER_MITCHELL) { ff = f_mitchell; F->filterw *= 2.6f; }
+  float fw = F->filterw < 0.501f ? 0.501f : F->filterw;
+  if (fw > 0.5f * MAX_FILTER_SIZE) fw = 0.5f * MAX_FILTER_SIZE;
+  F->filterw = fw;
+  float scale = 1.f / (float)FILTER_TABLE_SIZE;
+  for (int y = 0; y < FILTER_TABLE_SIZE; ++y)
+    for (int x = 0; x < FILTER_TABLE_SIZE; ++x)
+      F->table[y * FILTER_TABLE_SIZE + x] = ff((x + .5f) * scale, (y + .5f) * scale);
+  F->tableScale = 0.9999 * FILTER_TABLE_SIZE / F->filterw;
+  F->acc = (float*)calloc((size_t)F->w * F->h * 5, sizeof(float));
+}
+
+/* imageFilm_t::addSample, imagefilm.cc:453-511 */
+static void film_add(film_t* F, rgba c, int x, int y, float dx, float dy) {
+  int dx0 = Round2Int((double)dx - F->filterw), dx1 = Round2Int((double)dx + F->filterw - 1.0);
+  int dy0 = Round2Int((double)dy - F->filterw), dy1 = Round2Int((double)dy + F->filterw - 1.0);
+  if (F->cx0 - x > dx0) dx0 = F->cx0 - x;
+  if (F->cx1 - x - 1 < dx1) dx1 = F->cx1 - x - 1;
+  if (F->cy0 - y > dy0) dy0 = F->cy0 - y;
+  if (F->cy1 - y - 1 < dy1) dy1 = F->cy1 - y - 1;
+  double x_offs = dx - 0.5, y_offs = dy - 0.5;
+  int xIndex[MAX_FILTER_SIZE + 1], yIndex[MAX_FILTER_SIZE + 1];
+  for (int i = dx0, n = 0; i <= dx1; ++i, ++n) xIndex[n] = Floor2Int(fabs(((double)i - x_offs) * F->tableScale));
+  for (int i = dy0, n = 0; i <= dy1; ++i, ++n) yIndex[n] = Floor2Int(fabs(((double)i - y_offs) * F->tableScale));
+  int x0 = x + dx0, x1 = x + dx1, y0 = y + dy0, y1 = y + dy1;
+  for (int j = y0; j <= y1; ++j)
+    for (int i = x0; i <= x1; ++i) {
+      float wt = F->table[yIndex[j - y0] * FILTER_TABLE_SIZE + xIndex[i - x0]];
+      float* px = F->acc + 5 * ((size_t)(j - F->cy0) * F->w + (i - F->cx0));
+      px[0] += wt * c.r;
+      px[1] += wt * c.g;
+      px[2] += wt * c.b;
+      px[3] += wt * c.a;
+      px[4] += wt;
+    }
+}
+
+/* ---------------------------------------------------------- C entry -- */
+
+int orc_load(const float* tri_verts, const int32_t* tri_mat, int32_t ntris, const uint32_t* nodes,
+             const uint32_t* leaf_prims, const float* bound, const yk_material* mats, int32_t nmats,
+             const yk_light* lights, int32_t nlights, const yk_camera* cam) {
+  qmc_init();
+  free(G.ng);
+  free(G.al);
+  free(G.mats);
+  free(G.lights);
+  memset(&G, 0, sizeof G);
+  G.ntris = ntris;
+  G.tv = tri_verts;
+  G.tmat = tri_mat;
+  G.nodes = nodes;
+  G.leaf = leaf_prims;
+  memcpy(G.bound, bound, sizeof G.bound);
+  G.nmats = nmats;
+  G.mats = (yk_material*)malloc(sizeof(yk_material) * (nmats > 0 ? nmats : 1));
+  memcpy(G.mats, mats, sizeof(yk_material) * nmats);
+  G.nlights = nlights;
+  G.lights = (yk_light*)malloc(sizeof(yk_light) * (nlights > 0 ? nlights : 1));
+  memcpy(G.lights, lights, sizeof(yk_light) * nlights);
+  G.cam = *cam;
+  G.ng = (v3*)malloc(sizeof(v3) * (size_t)ntris);
+  for (int p = 0; p < ntris; ++p) { /* triangle_t::recNormal */
+    v3 a = tri_vert(p, 0), b = tri_vert(p, 1), c = tri_vert(p, 2);
+    G.ng[p] = vnormalize(vcross(vsub(b, a), vsub(c, a)));
+  }
+  camera_setup();
+  lights_setup();
+  return 0;
+}
+
+/* batched closest hit, scene_t::intersect semantics; counters optional */
+int orc_intersect(const yk_ray* rays, int64_t n, yk_hit* hits, uint64_t* counters) {
+  uint64_t n0 = g_nodes_c, t0 = g_tris_c;
+  for (int64_t i = 0; i < n; ++i) {
+    const yk_ray* r = &rays[i];
+    v3 from = V(r->from[0], r->from[1], r->from[2]), dir = V(r->dir[0], r->dir[1], r->dir[2]);
+    float dis = (r->tmax < 0) ? INFINITY : r->tmax, Z = 0, b1 = 0, b2 = 0;
+    int prim = -1;
+    if (kd_traverse(from, dir, r->tmin, dis, 1, &prim, &Z, &b1, &b2, &g_nodes_c, &g_tris_c)) {
+      hits[i].prim = prim; hits[i].t = Z; hits[i].b1 = b1; hits[i].b2 = b2;
+    } else {
+      hits[i].prim = -1; hits[i].t = 0; hits[i].b1 = 0; hits[i].b2 = 0;
+    }
+  }
+  if (counters) { counters[0] = g_nodes_c - n0; counters[1] = g_tris_c - t0; }
+  return 0;
+}
+
+/* batched any hit, scene_t::isShadowed semantics */
+int orc_shadow(const yk_ray* rays, int64_t n, uint8_t* occ, uint64_t* counters) {
+  uint64_t n0 = g_nodes_s, t0 = g_tris_s, c0 = g_nshadow;
+  for (int64_t i = 0; i < n; ++i) {
+    const yk_ray* r = &rays[i];
+    occ[i] = (uint8_t)scene_shadowed(V(r->from[0], r->from[1], r->from[2]), V(r->dir[0], r->dir[1], r->dir[2]),
+                                     r->tmin, r->tmax);
+  }
+  g_nshadow = c0;
+  if (counters) { counters[0] = g_nodes_s - n0; counters[1] = g_tris_s - t0; }
+  return 0;
+}
+
+/* camera rays of pixel (x,y) sample s, as renderTile generates them */
+int orc_camera_rays(int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t spp, yk_ray* out) {
+  float d1 = (float)(1.0 / (double)(float)spp);
+  size_t k = 0;
+  for (int i = y0; i < y0 + h; ++i)
+    for (int j = x0; j < x0 + w; ++j) {
+      unsigned so = fnv_32a_buf((unsigned)i * fnv_32a_buf((unsigned)j));
+      for (int s = 0; s < spp; ++s) {
+        float dx = 0.5f, dy = 0.5f;
+        if (spp > 1) { dx = (0.5f + (float)s) * d1; dy = RI_LP((unsigned)s + so, 0); }
+        v3 f, d;
+        float tmin, tmax;
+        camera_ray((float)j + dx, (float)i + dy, &f, &d, &tmin, &tmax);
+        yk_ray* r = &out[k++];
+        r->from[0] = f.x; r->from[1] = f.y; r->from[2] = f.z;
+        r->dir[0] = d.x; r->dir[1] = d.y; r->dir[2] = d.z;
+        r->tmin = tmin; r->tmax = tmax;
+      }
+    }
+  return 0;
+}
+
+/* tiledIntegrator_t::render single pass, single thread (integrator.cc:132-339):
+ * tiles row-major, pixels row-major inside a tile, samples in order. Output:
+ * rgba (w*h*4, imageFilm_t::flush + clampRGB0); optional film sums (w*h*5);
+ * counts[0..5] = closest, shadow, closest nodes, closest tris, shadow nodes,
+ * shadow tris. */
+int orc_render(const yk_render_params* P, float* rgba_out, float* film_sums, uint64_t* counts) {
+  if (P->aa_passes != 1) return 4;
+  film_t F;
+  film_init(&F, P);
+  g_nclosest = g_nshadow = g_nodes_c = g_tris_c = g_nodes_s = g_tris_s = 0;
+  int ts = P->tile_size > 0 ? P->tile_size : 32;
+  int n = P->aa_samples > 0 ? P->aa_samples : 1;
+  float d1 = (float)(1.0 / (double)(float)n);
+  int nx = (F.w + ts - 1) / ts, ny = (F.h + ts - 1) / ts;
+  for (int ty = 0; ty < ny; ++ty)
+    for (int tx = 0; tx < nx; ++tx) {
+      int X = F.cx0 + tx * ts, Y = F.cy0 + ty * ts;
+      int W = (F.cx0 + F.w - X) < ts ? (F.cx0 + F.w - X) : ts;
+      int H = (F.cy0 + F.h - Y) < ts ? (F.cy0 + F.h - Y) : ts;
+      for (int i = Y; i < Y + H; ++i)
+        for (int j = X; j < X + W; ++j) {
+          rstate st;
+          st.samplingOffs = fnv_32a_buf((unsigned)i * fnv_32a_buf((unsigned)j));
+          st.includeLights = 0;
+          for (int s = 0; s < n; ++s) {
+            st.pixelSample = s;
+            float dx = 0.5f, dy = 0.5f;
+            if (n > 1) { dx = (0.5f + (float)s) * d1; dy = RI_LP((unsigned)s + st.samplingOffs, 0); }
+            v3 from, dir;
+            float tmin, tmax;
+            camera_ray((float)j + dx, (float)i + dy, &from, &dir, &tmin, &tmax);
+            rgba c = (P->integrator == YK_INTEGRATOR_DIRECT) ? dl_integrate(&st, P, from, dir, tmin, tmax)
+                                                            : pt_integrate(&st, P, from, dir, tmin, tmax);
+            c.r = 1.f * c.r; c.g = 1.f * c.g; c.b = 1.f * c.b; c.a = 1.f * c.a; /* wt * col */
+            film_add(&F, c, j, i, dx, dy);
+          }
+        }
+    }
+  size_t npx = (size_t)F.w * F.h;
+  for (size_t p = 0; p < npx; ++p) {
+    float* a = F.acc + 5 * p;
+    float r = 0, g = 0, b = 0, al = 0;
+    if (a[4] > 0.f) { /* pixel_t::normalized + colorA_t / f (color.h:329-333) */
+      float f = (float)(1.0 / (double)a[4]);
+      r = a[0] * f; g = a[1] * f; b = a[2] * f; al = a[3] * f;
+    }
+    if (r < 0.f) r = 0.f;
+    if (g < 0.f) g = 0.f;
+    if (b < 0.f) b = 0.f;
+    if (rgba_out) { rgba_out[4 * p] = r; rgba_out[4 * p + 1] = g; rgba_out[4 * p + 2] = b; rgba_out[4 * p + 3] = al; }
+  }
+  if (film_sums) memcpy(film_sums, F.acc, npx * 5 * sizeof(float));
+  if (counts) {
+    counts[0] = g_nclosest; counts[1] = g_nshadow; counts[2] = g_nodes_c; counts[3] = g_tris_c;
+    counts[4] = g_nodes_s; counts[5] = g_tris_s;
+  }
+  free(F.acc);
+  return 0;
+}
+
+/* QMC probes for the unit tests */
+double orc_scrhalton(int dim, unsigned n) { qmc_init(); return scrHalton(dim, n); }
+float orc_ri_vdc(unsigned b, unsigned r) { return RI_vdC(b, r); }
+float orc_ri_s(unsigned i, unsigned r) { return RI_S(i, r); }
+float orc_ri_lp(unsigned i, unsigned r) { return RI_LP(i, r); }
+unsigned orc_fnv(unsigned v) { return fnv_32a_buf(v); }
+float orc_fsin(float x) { return fSin(x); }
+void orc_halton_seq(int base, unsigned start, int n, float* out) {
+  halton h;
+  hal_init(&h, base);
+  hal_setstart(&h, start);
+  for (int i = 0; i < n; ++i) out[i] = hal_next(&h);
+}
+void orc_faure(int dim, int* out) { qmc_init(); for (int i = 0; i < g_prims[dim]; ++i) out[i] = g_faure[dim][i]; }
