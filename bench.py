@@ -1,0 +1,207 @@
+"""Headline benchmark: Mrays/s (closest + shadow) of the path-tracing hot path
+on the procedural 1M-triangle scene, 1920x1080, 256 spp (BASELINE.json
+configs[2]; configs[3] when launched on N GPUs).
+
+One step = one whole frame: every rank renders the tiles t with
+t % world == rank (yk_render_shard), the film sums are reduced to rank 0 over
+RCCL (torch.distributed "nccl") and rank 0 normalises the frame
+(yk_film_resolve). Total work is fixed as N grows ("scaling": "strong").
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from core_amd import _abi as A  # noqa: E402
+from core_amd.device import Device  # noqa: E402
+from core_amd.scene import probe_scene  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def algorithmic_bytes(rays, nodes, tris, out_bytes):
+    """Bytes one traversal launch must move if nothing were cached: the ray
+    (32 B) and its result, one 8-B node per visit, and per triangle test the
+    9 vertex floats (36 B) plus its 4-B leaf-list entry."""
+    return rays * (32 + out_bytes) + 8 * nodes + 40 * tris
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--nu", type=int, default=1000, help="sphere segments (1000x501 -> 1,000,002 tris)")
+    ap.add_argument("--nv", type=int, default=501)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target length of the CPU baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC HBM-traffic summary (tools/pmc_traffic.py output) to attach, if present")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    t_build = time.perf_counter()
+    scene, p = probe_scene("bumpy", args.width, args.height, args.nu, args.nv)
+    t_build = time.perf_counter() - t_build
+    info = scene.info()
+    p.aa_samples = args.spp
+    dev = Device(local)
+    dev.upload(scene)
+    film = dev.new_film(p)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def step(st):
+        film.zero_()
+        dev.render_shard(p, film, rank, world, st)
+        if dist is not None:
+            dist.reduce(film, dst=0)
+        if rank == 0:
+            rgba = dev.film_resolve(p, film)
+            return rgba
+        return None
+
+    for _ in range(args.warmup):
+        step(A.yk_stats())
+    st = A.yk_stats()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(st)
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    # whole-job numbers: sum the work, take the slowest rank's time
+    work = torch.tensor([st.closest_rays, st.shadow_rays, st.closest_nodes, st.closest_tris, st.shadow_nodes,
+                         st.shadow_tris, st.closest_launches, st.shadow_launches, st.camera_samples],
+                        dtype=torch.float64, device="cuda")
+    kern = torch.tensor([st.ms_closest, st.ms_shadow], dtype=torch.float64, device="cuda")
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if dist is not None:
+        dist.all_reduce(work)
+        dist.all_reduce(kern)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    w = work.cpu().numpy()
+    ms_c, ms_s = kern.cpu().numpy()
+    elapsed = float(tmax.item())
+    rays = w[0] + w[1]
+    value = rays / elapsed / 1e6
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    # roofline of the dominant kernel, from HIP events on the kernel's stream
+    kc = dict(name="k_trace<closest>", launches=w[6], ms=ms_c,
+              bytes=algorithmic_bytes(w[0], w[2], w[3], 16))
+    ks = dict(name="k_trace<shadow>", launches=w[7], ms=ms_s,
+              bytes=algorithmic_bytes(w[1], w[4], w[5], 1))
+    for k in (kc, ks):
+        k["gbs"] = k["bytes"] / (k["ms"] * 1e-3) / 1e9 if k["ms"] > 0 else 0.0
+        k["avg_ms"] = k["ms"] / max(k["launches"], 1)
+    dom = kc if kc["ms"] >= ks["ms"] else ks
+    traffic = None
+    traffic_note = None
+    if os.path.exists(args.traffic):
+        with open(args.traffic) as f:
+            tj = json.load(f)
+        key = "closest" if dom is kc else "shadow"
+        if key in tj:
+            traffic = tj[key].get("hbm_bytes_per_launch")
+            traffic_note = tj.get("source")
+    roofline = {"bound": "hbm", "achieved": round(dom["gbs"], 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": dom["name"], "avg_launch_ms": round(dom["avg_ms"], 4),
+                "algorithmic_bytes_per_launch": round(dom["bytes"] / max(dom["launches"], 1)),
+                "other_kernel": {"name": (ks if dom is kc else kc)["name"],
+                                 "achieved": round((ks if dom is kc else kc)["gbs"], 2)}}
+    if traffic_note:
+        roofline["traffic_source"] = traffic_note
+
+    cpu = None
+    if not args.no_cpu:
+        cpu = cpu_baseline(scene, p, args.cpu_seconds)
+
+    out = {
+        "metric": "Mrays/s (primary+shadow), 1M-tri scene",
+        "value": round(value, 3),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic: procedural displaced sphere + floor, {info.ntris} tris, kd-tree built on host "
+                f"({t_build:.1f} s, not timed)",
+        "config": {"workload": f"bumpy {info.ntris} tris, pathtracing bounces {p.bounces}, "
+                               f"{p.width}x{p.height}, {p.aa_samples} spp, area light 1 sample",
+                   "tris": int(info.ntris), "width": p.width, "height": p.height, "spp": p.aa_samples,
+                   "parallelism": f"tiles%{world}" if world > 1 else "single",
+                   "closest_rays": int(w[0]), "shadow_rays": int(w[1]),
+                   "camera_samples": int(w[8])},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(scene, p, seconds):
+    """The oracle (scalar C restatement, 1 thread) on a bounded crop of the
+    same frame: rays/s scaled from a short probe to about `seconds` of work."""
+    sys.path.insert(0, ROOT)
+    from oracle.oracle import Oracle
+    orc = Oracle(scene)
+    q = A.yk_render_params.from_buffer_copy(p)
+    q.width, q.height = 16, 16
+    q.xstart, q.ystart = p.width // 2, p.height // 2
+    t0 = time.perf_counter()
+    _, _, c = orc.render(q)
+    probe = time.perf_counter() - t0
+    # grow the crop to ~`seconds` of work (square, centred)
+    px = max(256, int(16 * 16 * seconds / max(probe, 1e-3)))
+    side = int(np.sqrt(px))
+    q.width, q.height = min(side, p.width), min(side, p.height)
+    q.xstart, q.ystart = (p.width - q.width) // 2, (p.height - q.height) // 2
+    t0 = time.perf_counter()
+    _, _, c = orc.render(q)
+    dt = time.perf_counter() - t0
+    r = c["closest"] + c["shadow"]
+    return {"value": round(r / dt / 1e6, 4), "unit": "Mrays/s", "cores": 1, "kind": "port",
+            "sample": f"oracle, 1 thread: {q.width}x{q.height} crop at ({q.xstart},{q.ystart}) of the same "
+                      f"frame, {p.aa_samples} spp, {r} rays in {dt:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,1705 @@
+// MI355X (gfx950) device half of libyk: scene upload, persistent kd-tree
+// traversal kernels, the wavefront path-integrator pipeline and the
+// deterministic image-film gather. Host entry points are the C-ABI of
+// include/yk_api.h.
+//
+// Reference behaviour restated here:
+//   triKdTree_t::Intersect / IntersectS      src/yafraycore/kdtree.cc:675-947
+//   bound_t::cross                           include/core_api/bound.h:148-204
+//   scene_t::intersect / isShadowed          src/yafraycore/scene.cc:852-902
+//   pathIntegrator_t::integrate              src/integrators/pathtracer.cc:134-333
+//   directLighting_t::integrate              src/integrators/directlight.cc:112-182
+//   mcIntegrator_t::doLightEstimation        src/yafraycore/mcintegrator.cc:45-195
+//   tiledIntegrator_t::renderTile            src/yafraycore/integrator.cc:229-339
+//   imageFilm_t::addSample / flush           src/yafraycore/imagefilm.cc:383-511
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/yk_api.h"
+#include "scene.h"
+#include "yk_internal.h"
+#include "yk_math.h"
+
+struct yk_scene {
+  yk::Scene s;
+};
+
+namespace yk {
+
+__constant__ QmcTables c_qmc;
+__constant__ int c_faure[5600];
+
+// ------------------------------------------------------------ device data
+
+struct DMat {
+  int type;
+  unsigned flags;
+  float col[3];       // diffuse colour (shinydiffuse) / lightCol = col*power (light_mat)
+  float diffuse;      // component[3] = diffuse strength (shinydiffuse.cc:98-101)
+  float emit_col[3];  // mEmitColor = emit * color (shinydiffuse.cc:12)
+  int double_sided;
+};
+
+struct DLight {  // areaLight_t members after its constructor (arealight.cc:30-49)
+  float corner[3], toX[3], toY[3], fnormal[3], c2[3], c3[3], c4[3], color[3];
+  float area;
+  int samples;
+};
+
+struct DCam {  // perspectiveCam_t after camera_t ctor + setAxis
+  float pos[3], vright[3], vup[3], vto[3], camZ[3], near_p[3], far_p[3];
+};
+
+constexpr int kMaxMats = 64;
+constexpr int kMaxLights = 8;
+__constant__ DMat c_mats[kMaxMats];
+__constant__ DLight c_lights[kMaxLights];
+__constant__ DCam c_cam;
+
+struct DScene {
+  const float4* tris;    // 3 float4 per prim: a, e1=b-a, e2=c-a
+  const uint2* nodes;    // kd nodes (kdtree_build.h encoding)
+  const uint32_t* leaf;  // leaf primitive lists
+  const float4* ng;      // geometric normal xyz, material id in w (int bits)
+  float bound[6];
+  int nlights;
+  unsigned nnodes;  // node count, for the pop-time bounds guard
+};
+
+__device__ __forceinline__ v3 ld3(const float* p) { return V3(p[0], p[1], p[2]); }
+
+// ============================================================ traversal
+
+// bound_t::cross (Smits), compiled form: ((a1-a0)-p)*inv evaluates as (a1-from)*inv
+__device__ __forceinline__ bool bound_cross(const float* bb, v3 from, v3 dir, float& enter, float& leave,
+                                            float dist) {
+  float lmin = -1e38f, lmax = 1e38f;
+  const float o[3] = {from.x, from.y, from.z}, d[3] = {dir.x, dir.y, dir.z};
+#pragma unroll
+  for (int ax = 0; ax < 3; ++ax) {
+    if (d[ax] != 0.f) {
+      const float invr = 1.0f / d[ax];
+      const float t0 = (bb[ax] - o[ax]) * invr, t1 = (bb[3 + ax] - o[ax]) * invr;
+      const float ltmin = invr > 0.f ? t0 : t1, ltmax = invr > 0.f ? t1 : t0;
+      if (ax == 0) {
+        lmin = ltmin;
+        lmax = ltmax;
+      } else {
+        lmin = (ltmin < lmin) ? lmin : ltmin;
+        lmax = (lmax < ltmax) ? lmax : ltmax;
+      }
+      if ((lmax < 0.f) || (lmin > dist)) return false;
+    }
+  }
+  if ((lmin <= lmax) && (lmax >= 0.f) && (lmin <= dist)) {
+    enter = lmin;
+    leave = lmax;
+    return true;
+  }
+  return false;
+}
+
+// Exit-point stack. The reference keeps {node*, t, pb[3], prev} per entry
+// (kdtree.h:103-109); exits form a LIFO (prev links). Here the current entry
+// and exit live in registers and older exits in LDS as {t, split, node|code}:
+// on pop, pb is regenerated bit-exactly as pb[code] = split and the other
+// axes from + t*dir (code 3 = the initial exit, all three axes from t).
+struct Trav {
+  v3 o, d, inv;
+  float tmin, dist;
+  float en_t, ex_t, ex_split;
+  v3 en_pb, ex_pb;
+  int ex_code, ex_node;
+  int node, sp;
+  float Z, b1, b2;
+  int prim;
+};
+
+__device__ __forceinline__ void exit_pb(Trav& st) {
+  const float x = st.o.x + st.ex_t * st.d.x, y = st.o.y + st.ex_t * st.d.y, z = st.o.z + st.ex_t * st.d.z;
+  st.ex_pb = V3(st.ex_code == 0 ? st.ex_split : x, st.ex_code == 1 ? st.ex_split : y,
+                st.ex_code == 2 ? st.ex_split : z);
+}
+
+// scene_t::intersect (scene.cc:852-879) / isShadowed (scene.cc:881-902)
+// setup + tree bound test; false = miss.
+template <bool CLOSEST>
+__device__ __forceinline__ bool trav_begin(const DScene& S, Trav& st, const yk_ray& r) {
+  st.d = V3(r.dir[0], r.dir[1], r.dir[2]);
+  if (CLOSEST) {
+    st.o = V3(r.from[0], r.from[1], r.from[2]);
+    st.tmin = r.tmin;
+    st.dist = (r.tmax < 0.f) ? INFINITY : r.tmax;
+  } else {
+    st.o = V3(r.from[0] + r.tmin * st.d.x, r.from[1] + r.tmin * st.d.y, r.from[2] + r.tmin * st.d.z);
+    st.tmin = 0.f;
+    st.dist = (r.tmax < 0.f) ? INFINITY : r.tmax - 2.0f * r.tmin;
+  }
+  st.Z = st.dist;
+  st.prim = -1;
+  st.b1 = st.b2 = 0.f;
+  float a, b;
+  if (!bound_cross(S.bound, st.o, st.d, a, b, st.dist)) return false;
+  st.inv = V3(1.0f / st.d.x, 1.0f / st.d.y, 1.0f / st.d.z);
+  st.en_t = a;
+  st.en_pb = (a >= 0.0f) ? vadd(st.o, vmul(a, st.d)) : st.o;
+  st.ex_t = b;
+  st.ex_code = 3;
+  st.ex_split = 0.f;
+  st.ex_node = -1;
+  exit_pb(st);
+  st.node = 0;
+  st.sp = 0;
+  return true;
+}
+
+// One iteration of the reference's outer traversal loop (kdtree.cc:707-812):
+// descend to a leaf, test its primitives, then stop or pop. Returns true when
+// the ray is finished.
+template <bool CLOSEST>
+__device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, float* __restrict__ st_t,
+                                          float* __restrict__ st_s, uint32_t* __restrict__ st_n, int lane,
+                                          unsigned& nnodes, unsigned& ntris, bool& occluded) {
+  if (st.dist < st.en_t) return true;
+  int node = st.node;
+  uint2 nd = S.nodes[node];
+  nnodes++;
+  while ((nd.y & 3u) != 3u) {
+    const int axis = (int)(nd.y & 3u);
+    const float split = __uint_as_float(nd.x);
+    const int right = (int)(nd.y >> 2);
+    const float enp = vget(st.en_pb, axis), exq = vget(st.ex_pb, axis);
+    int far_;
+    if (enp <= split) {
+      if (exq <= split) {
+        node = node + 1;
+        nd = S.nodes[node];
+        nnodes++;
+        continue;
+      }
+      if (exq == split) {
+        node = right;
+        nd = S.nodes[node];
+        nnodes++;
+        continue;
+      }
+      far_ = right;
+      node = node + 1;
+    } else {
+      if (split < exq) {
+        node = right;
+        nd = S.nodes[node];
+        nnodes++;
+        continue;
+      }
+      far_ = node + 1;
+      node = right;
+    }
+    const float t = (split - vget(st.o, axis)) * vget(st.inv, axis);
+    const int slot = st.sp * 64 + lane;
+    st_t[slot] = st.ex_t;
+    st_s[slot] = st.ex_split;
+    st_n[slot] = ((uint32_t)(st.ex_node + 1)) | ((uint32_t)st.ex_code << 30);
+    st.sp++;
+    st.ex_t = t;
+    st.ex_split = split;
+    st.ex_code = axis;
+    st.ex_node = far_;
+    exit_pb(st);
+    nd = S.nodes[node];
+    nnodes++;
+  }
+  const uint32_t n = nd.y >> 2, w0 = nd.x;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t p = (n == 1) ? w0 : S.leaf[w0 + i];
+    ntris++;
+    const float4 A = S.tris[3 * p], E1 = S.tris[3 * p + 1], E2 = S.tris[3 * p + 2];
+    float th, u, v;
+    if (mt_intersect(V3(A.x, A.y, A.z), V3(E1.x, E1.y, E1.z), V3(E2.x, E2.y, E2.z), st.o, st.d, th, u, v)) {
+      if (CLOSEST) {
+        if (th < st.Z && th >= st.tmin) {
+          st.Z = th;
+          st.prim = (int)p;
+          st.b1 = u;
+          st.b2 = v;
+        }
+      } else if (th < st.dist && th >= 0.f) {
+        occluded = true;
+        return true;
+      }
+    }
+  }
+  if (CLOSEST && st.prim >= 0 && st.Z <= st.ex_t) return true;
+  // pop: entry := exit, exit := previous exit
+  st.en_t = st.ex_t;
+  st.en_pb = st.ex_pb;
+  st.node = st.ex_node;
+  if (st.node < 0) return true;
+  if ((unsigned)st.node >= S.nnodes || st.sp <= 0) {  // corrupt state: never index out of the tree
+    st.prim = -2;
+    return true;
+  }
+  st.sp--;
+  const int slot = st.sp * 64 + lane;
+  st.ex_t = st_t[slot];
+  st.ex_split = st_s[slot];
+  const uint32_t w = st_n[slot];
+  st.ex_node = (int)(w & 0x3FFFFFFFu) - 1;
+  st.ex_code = (int)(w >> 30);
+  exit_pb(st);
+  return false;
+}
+
+__device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int src) {
+  unsigned lo = __shfl((unsigned)v, src), hi = __shfl((unsigned)(v >> 32), src);
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+// Persistent ray-query kernel. One 64-lane wave per workgroup; each lane owns
+// one ray at a time and advances it one leaf visit per loop iteration. Lanes
+// whose ray finished are refilled from a global work counter in bulk
+// (__ballot + one atomicAdd per wave + mbcnt-style ranks), so the wave stays
+// packed with live rays until the queue drains. Stack: LDS, [depth][lane].
+// idx (optional): queue entry r is ray idx[r]; the result goes to the same
+// slot (used by the shadow queue, whose rays sit in per-sample slots).
+template <bool CLOSEST>
+__global__ void __launch_bounds__(64) k_trace(DScene S, const yk_ray* __restrict__ rays,
+                                              const unsigned* __restrict__ idx, long long n,
+                                              yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
+                                              unsigned long long* __restrict__ work,
+                                              unsigned long long* __restrict__ ctr, int D) {
+  extern __shared__ uint32_t lds[];
+  float* st_t = reinterpret_cast<float*>(lds);
+  float* st_s = reinterpret_cast<float*>(lds + D * 64);
+  uint32_t* st_n = lds + 2 * D * 64;
+  const int lane = threadIdx.x;
+  long long rid = -1;
+  bool exhausted = false;
+  Trav st;
+  unsigned nnodes = 0, ntris = 0, steps = 0, nerr = 0;
+  for (;;) {
+    const unsigned long long want = __ballot(rid < 0 && !exhausted);
+    const unsigned long long act = __ballot(rid >= 0);
+    if (want != 0ull && (act == 0ull || __popcll(want) >= 24)) {
+      const int cnt = __popcll(want);
+      const int leader = __ffsll((long long)want) - 1;
+      unsigned long long base = 0;
+      if (lane == leader) base = atomicAdd(work, (unsigned long long)cnt);
+      base = shfl_u64(base, leader);
+      if (rid < 0 && !exhausted) {
+        const int rank = __popcll(want & ((1ull << lane) - 1ull));
+        const long long q = (long long)base + rank;
+        if (q < n) {
+          const long long r = idx ? (long long)idx[q] : q;
+          const yk_ray ray = rays[r];
+          if (trav_begin<CLOSEST>(S, st, ray)) {
+            rid = r;
+          } else if (CLOSEST) {
+            hits[r] = yk_hit{-1, 0.f, 0.f, 0.f};
+          } else {
+            occl[r] = 0;
+          }
+        } else {
+          exhausted = true;
+        }
+      }
+    }
+    if (__ballot(rid >= 0) == 0ull) {
+      if (__ballot(!exhausted) == 0ull) break;
+      continue;
+    }
+    if (rid >= 0) {
+      bool occ = false;
+      bool done = trav_step<CLOSEST>(S, st, st_t, st_s, st_n, lane, nnodes, ntris, occ);
+      if (++steps > (1u << 22)) {  // watchdog: no ray of a valid tree gets near this
+        st.prim = -2;
+        done = true;
+      }
+      if (st.prim == -2) {
+        nerr++;
+        st.prim = -1;
+      }
+      if (done) {
+        steps = 0;
+        if (CLOSEST) {
+          hits[rid] = (st.prim >= 0) ? yk_hit{st.prim, st.Z, st.b1, st.b2} : yk_hit{-1, 0.f, 0.f, 0.f};
+        } else {
+          occl[rid] = occ ? 1 : 0;
+        }
+        rid = -1;
+      }
+    }
+  }
+  // wave-reduced work counters (nodes visited, triangle tests)
+  unsigned long long a = nnodes, b = ntris;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    a += shfl_u64(a, lane ^ off);
+    b += shfl_u64(b, lane ^ off);
+  }
+  if (lane == 0) {
+    atomicAdd(&ctr[0], a);
+    atomicAdd(&ctr[1], b);
+  }
+  if (nerr) atomicAdd(&ctr[2], (unsigned long long)nerr);
+}
+
+// ============================================================ shading
+
+struct SurfPt {
+  v3 P, N, Ng, NU, NV;
+  int mat;
+};
+
+// scene_t::intersect tail + triangle_t::getSurface (flat shading subset)
+__device__ __forceinline__ SurfPt make_surface(const DScene& S, v3 from, v3 dir, const yk_hit& h) {
+  SurfPt sp;
+  sp.P = vadd(from, vmul(h.t, dir));
+  const float4 g = S.ng[h.prim];
+  sp.Ng = V3(g.x, g.y, g.z);
+  sp.N = sp.Ng;
+  sp.mat = __float_as_int(g.w);
+  create_cs(sp.N, sp.NU, sp.NV);
+  return sp;
+}
+
+// shinyDiffuseMat_t::eval (diffuse subset), shinydiffuse.cc:223-249 (compiled
+// order of mD: ((1-c2)*c3)*mT)
+__device__ __forceinline__ c3 mat_eval(const DMat& M, const SurfPt& sp, v3 wo, v3 wl) {
+  if (M.type == YK_MAT_LIGHT) return C3(0.f, 0.f, 0.f);
+  v3 N = (vdot(sp.Ng, wo) < 0.f) ? vneg(sp.N) : sp.N;
+  if (!(M.flags & BSDF_DIFFUSE)) return C3(0.f, 0.f, 0.f);
+  const float mT = (1.f - 0.f) * (1.f - 0.f);
+  if (vdot(N, wl) < 0.0f) return C3(0.f, 0.f, 0.f);
+  const float mD = ((1.f - 0.f) * M.diffuse) * mT;
+  return cscale(mD, C3(M.col[0], M.col[1], M.col[2]));
+}
+
+// shinyDiffuseMat_t::sample, diffuse-reflect component (shinydiffuse.cc:259-336);
+// lightMat_t::sample (simple.cc:47-52). ok=false: early return, W untouched.
+__device__ __forceinline__ c3 mat_sample(const DMat& M, const SurfPt& sp, v3 wo, v3& wi, float s1in, float s2in,
+                                         unsigned flags, float& pdf, float& W, bool& ok) {
+  ok = true;
+  if (M.type == YK_MAT_LIGHT) {
+    pdf = 0.f;
+    W = 0.f;
+    return C3(0.f, 0.f, 0.f);
+  }
+  const float cos_Ng_wo = vdot(sp.Ng, wo);
+  const v3 N = (cos_Ng_wo < 0.f) ? vneg(sp.N) : sp.N;
+  const float accum3 = M.diffuse * (((1.f - 0.f * 1.f) * (1.f - 0.f)) * (1.f - 0.f));
+  const unsigned cf = BSDF_DIFFUSE | BSDF_REFLECT;
+  if (!(M.flags & BSDF_DIFFUSE) || (flags & cf) != cf) {
+    pdf = 0.f;
+    ok = false;
+    return C3(1.f, 1.f, 1.f);
+  }
+  float width = accum3;
+  const float sum = 0.f + width;
+  if (sum < 0.00001f) {
+    pdf = 0.f;
+    ok = false;
+    return C3(1.f, 1.f, 1.f);
+  }
+  const float inv_sum = 1.f / sum;
+  width *= inv_sum;
+  const float s1 = s1in / width;
+  wi = sample_cos_hemisphere(N, sp.NU, sp.NV, s1, s2in);
+  const float cos_Ng_wi = vdot(sp.Ng, wi);
+  c3 sc = C3(0.f, 0.f, 0.f);
+  if (cos_Ng_wo * cos_Ng_wi > 0.f) sc = cscale(accum3, C3(M.col[0], M.col[1], M.col[2]));
+  pdf = fabsf(vdot(wi, N)) * width;
+  W = fabsf(vdot(wi, sp.N)) / (pdf * 0.99f + 0.01f);
+  return sc;
+}
+
+// shinyDiffuseMat_t::pdf, shinydiffuse.cc:338-377
+__device__ __forceinline__ float mat_pdf(const DMat& M, const SurfPt& sp, v3 wo, v3 wi) {
+  if (M.type == YK_MAT_LIGHT || !(M.flags & BSDF_DIFFUSE)) return 0.f;
+  const v3 N = (vdot(sp.Ng, wo) < 0.f) ? vneg(sp.N) : sp.N;
+  const float width = M.diffuse * (((1.f - 0.f * 1.f) * (1.f - 0.f)) * (1.f - 0.f));
+  const float sum = 0.f + width;
+  const float pdf = 0.f + fabsf(vdot(wi, N)) * width;
+  if (sum < 0.00001f) return 0.f;
+  return pdf / sum;
+}
+
+// emit: shinyDiffuseMat_t::emit (shinydiffuse.cc:251-257), lightMat_t::emit (simple.cc:54-61)
+__device__ __forceinline__ c3 mat_emit(const DMat& M, const SurfPt& sp, v3 wo, bool includeLights) {
+  if (M.type == YK_MAT_LIGHT) {
+    if (!includeLights) return C3(0.f, 0.f, 0.f);
+    const c3 lc = C3(M.col[0], M.col[1], M.col[2]);
+    if (M.double_sided) return lc;
+    return (vdot(wo, sp.N) > 0.f) ? lc : C3(0.f, 0.f, 0.f);
+  }
+  return C3(M.emit_col[0], M.emit_col[1], M.emit_col[2]);
+}
+
+// triIntersect, arealight.cc:98-115
+__device__ __forceinline__ bool tri_isect_pts(v3 a, v3 b, v3 c, v3 from, v3 dir, float& t) {
+  float u, v;
+  return mt_intersect(a, vsub(b, a), vsub(c, a), from, dir, t, u, v);
+}
+
+// areaLight_t::illumSample, arealight.cc:68-96 (compiled sample point form)
+__device__ __forceinline__ bool light_illum(const DLight& L, v3 P, float s1, float s2, v3& ldir, float& tmax,
+                                            float& pdf) {
+  const v3 p = V3(L.corner[0] + (s1 * L.toX[0] + s2 * L.toY[0]), L.corner[1] + (s1 * L.toX[1] + s2 * L.toY[1]),
+                  (L.corner[2] + s1 * L.toX[2]) + s2 * L.toY[2]);
+  v3 l = vsub(p, P);
+  const float dist_sqr = l.x * l.x + l.y * l.y + l.z * l.z;
+  const float dist = sqrtf(dist_sqr);
+  if (dist <= 0.0f) return false;
+  const float id = 1.f / dist;
+  l = V3(l.x * id, l.y * id, l.z * id);
+  const float cos_angle = vdot(l, ld3(L.fnormal));
+  if (cos_angle <= 0.f) return false;
+  tmax = dist;
+  ldir = l;
+  pdf = (float)((double)dist_sqr * YK_PI_D / (double)(L.area * cos_angle));
+  return true;
+}
+
+// areaLight_t::intersect, arealight.cc:138-154
+__device__ __forceinline__ bool light_hit(const DLight& L, v3 from, v3 dir, float& t, float& ipdf) {
+  const float cos_angle = vdot(dir, ld3(L.fnormal));
+  if (cos_angle <= 0.f) return false;
+  if (!tri_isect_pts(ld3(L.corner), ld3(L.c2), ld3(L.c3), from, dir, t)) {
+    if (!tri_isect_pts(ld3(L.corner), ld3(L.c3), ld3(L.c4), from, dir, t)) return false;
+  }
+  if (!(t > 1.0e-10f)) return false;
+  ipdf = (float)((double)((1.f / (t * t)) * L.area * cos_angle) * YK_1_PI_D);
+  return true;
+}
+
+// ------------------------------------------------------------ queues
+
+// Wave-aggregated append of m items: one atomicAdd per wave, each lane gets
+// a contiguous range. Must be called by the whole wave (m may be 0).
+__device__ __forceinline__ unsigned wave_append(unsigned* counter, unsigned m) {
+  const int lane = threadIdx.x & 63;
+  unsigned incl = m;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned v = __shfl_up(incl, off);
+    if (lane >= off) incl += v;
+  }
+  const unsigned total = __shfl(incl, 63);
+  unsigned base = 0;
+  if (lane == 63 && total) base = atomicAdd(counter, total);
+  base = __shfl(base, 63);
+  return base + incl - m;
+}
+
+// Shadow-ray slot flags
+enum : uint8_t { SL_TRACED = 1, SL_ADDS = 2 };
+// prim_hit flags
+enum : int { PH_HIT = 1, PH_DIFFUSE = 2 };
+// path state bits
+enum : int { PS_ALIVE = 1, PS_RESOLVE = 2, PS_CONT = 4, PS_EST = 8 };
+
+// Per-batch device state. Camera sample c owns K shadow slots c*K + k:
+// doLightEstimation's i-th light sample is slot k0+i, its i-th BSDF (MIS)
+// sample slot k0+n+i. Shadow rays are written straight into their slot and
+// only the slot index goes through the compacted queue, so the resolve step
+// reads results in the reference's summation order without any sorting.
+struct Batch {
+  int* prim_hit;        // PH_* flags of the camera ray
+  unsigned* soffs;      // samplingOffs (fnv of pixel)
+  float* col;           // 3 floats: primary emission + direct light
+  float* alpha;
+  yk_ray* p_rays;       // camera rays (kept for all sub-paths)
+  yk_hit* p_hits;
+  float* thr;           // 3 floats: path throughput
+  float* pathcol;       // 3 floats, accumulated over sub-paths
+  float* scol_next;     // 3 floats, BSDF weight of the next segment
+  float* wlast;         // last W written by material sample (kept when sample() returns early)
+  float* emit_b;        // 3 floats: emission added at the current bounce
+  int* pstate;          // PS_* bits
+  int* lsel;            // light chosen by estimateOneDirectLight
+  int* qidx;            // index of the sample's current bounce ray in its queue
+  yk_ray* q_rays[2];    // bounce queues (ping-pong)
+  yk_hit* q_hits[2];
+  unsigned* q_count;    // [0],[1] bounce queues, [2] shadow queue
+  yk_ray* s_rays;       // K per camera sample
+  uint8_t* s_occl;      // K per camera sample
+  unsigned* s_idx;      // compacted shadow queue of slot indices
+  float* sl_contrib;    // 3 floats per slot
+  uint8_t* sl_flags;    // 1 per slot
+  float4* samples;      // final RGBA per camera sample
+  int K;
+};
+
+struct RenderConst {
+  int spp;
+  int nsub;       // path_samples
+  int bounces;    // maxBounces
+  int integrator;
+  int transp_bg;
+  int nlights;
+  float d1;       // 1/spp as renderTile computes it
+};
+
+// ------------------------------------------------------------ kernels
+
+// Camera rays for the camera samples of the batch tiles (renderTile,
+// integrator.cc:251-306): sample index s is the fastest-running index.
+struct TileList {
+  const int4* tiles;  // X, Y, W, H per tile of the batch
+  const int* base;    // first camera-sample index of each tile
+  int ntiles;
+};
+
+__global__ void __launch_bounds__(256) k_camera(TileList TL, Batch B, RenderConst R, long long nc) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  int lo = 0, hi = TL.ntiles - 1;
+  while (lo < hi) {  // tile owning c
+    const int mid = (lo + hi + 1) >> 1;
+    if (TL.base[mid] <= c) lo = mid;
+    else hi = mid - 1;
+  }
+  const int4 T = TL.tiles[lo];
+  const long long local = c - TL.base[lo];
+  const int s = (int)(local % R.spp);
+  const int pl = (int)(local / R.spp);
+  const int j = T.x + pl % T.z, i = T.y + pl / T.z;
+  const unsigned so = fnv32a((unsigned)i * fnv32a((unsigned)j));
+  B.soffs[c] = so;
+  float dx = 0.5f, dy = 0.5f;
+  if (R.spp > 1) {
+    dx = (0.5f + (float)s) * R.d1;
+    dy = ri_lp((unsigned)s + so, 0u);
+  }
+  const float px = (float)j + dx, py = (float)i + dy;
+  const v3 vr = ld3(c_cam.vright), vu = ld3(c_cam.vup), vt = ld3(c_cam.vto), cz = ld3(c_cam.camZ);
+  v3 d = vadd(vadd(vmul(px, vr), vmul(py, vu)), vt);
+  d = vnormalize(d);
+  const v3 from = ld3(c_cam.pos);
+  yk_ray r;
+  r.from[0] = from.x;
+  r.from[1] = from.y;
+  r.from[2] = from.z;
+  r.dir[0] = d.x;
+  r.dir[1] = d.y;
+  r.dir[2] = d.z;
+  const float den = vdot(d, cz);
+  r.tmin = vdot(cz, vsub(ld3(c_cam.near_p), from)) / den;
+  r.tmax = vdot(cz, vsub(ld3(c_cam.far_p), from)) / den;
+  B.p_rays[c] = r;
+}
+
+__device__ __forceinline__ void put_ray(yk_ray& r, v3 f, v3 d, float tmin, float tmax) {
+  r.from[0] = f.x;
+  r.from[1] = f.y;
+  r.from[2] = f.z;
+  r.dir[0] = d.x;
+  r.dir[1] = d.y;
+  r.dir[2] = d.z;
+  r.tmin = tmin;
+  r.tmax = tmax;
+}
+
+__device__ __forceinline__ void put_slot(const Batch& B, long long slot, uint8_t fl, c3 v) {
+  B.sl_flags[slot] = fl;
+  B.sl_contrib[3 * slot] = v.r;
+  B.sl_contrib[3 * slot + 1] = v.g;
+  B.sl_contrib[3 * slot + 2] = v.b;
+}
+
+// mcIntegrator_t::doLightEstimation (area light), mcintegrator.cc:73-195, split
+// at its isShadowed calls: every shadow ray it would trace is written to its
+// slot with the contribution it adds when unoccluded. Returns #rays.
+__device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, int li, const SurfPt& sp, v3 wo,
+                                         unsigned pixelSample, unsigned soffs, unsigned loffs) {
+  const DLight& L = c_lights[li];
+  const DMat& M = c_mats[sp.mat];
+  const int n = L.samples;
+  const unsigned offs = (unsigned)(n * (int)pixelSample) + soffs + loffs * 4567u;
+  const c3 lcol = C3(L.color[0], L.color[1], L.color[2]);
+  const c3 black = C3(0.f, 0.f, 0.f);
+  int nr = 0;
+  Halton h2, h3;
+  hal_start(h2, 2u, offs - 1u);
+  hal_start(h3, 3u, offs - 1u);
+  for (int i = 0; i < n; ++i) {
+    const float s1 = hal_next(h2), s2 = hal_next(h3);
+    const long long slot = c * B.K + k0 + i;
+    v3 ldir;
+    float ltmax, lpdf;
+    if (!light_illum(L, sp.P, s1, s2, ldir, ltmax, lpdf)) {
+      put_slot(B, slot, 0, black);
+      continue;
+    }
+    put_ray(B.s_rays[slot], sp.P, ldir, YK_SHADOW_BIAS, ltmax);
+    ++nr;
+    if (!(lpdf > 1e-6f)) {
+      put_slot(B, slot, SL_TRACED, black);
+      continue;
+    }
+    const c3 surf = mat_eval(M, sp, wo, ldir);
+    const float mPdf = mat_pdf(M, sp, wo, ldir);
+    // compiled form: ((surf*lcol) * (|N.l| * (1/pdf))) [* w]
+    const float k = fabsf(vdot(sp.N, ldir)) * (1.0f / lpdf);
+    const c3 sl = cmul(surf, lcol);
+    c3 v;
+    if (mPdf > 1e-6f) {
+      const float l2 = lpdf * lpdf, m2 = mPdf * mPdf;
+      const float w = l2 / (l2 + m2);
+      v = C3((sl.r * k) * w, (sl.g * k) * w, (sl.b * k) * w);
+    } else {
+      v = C3(sl.r * k, sl.g * k, sl.b * k);
+    }
+    put_slot(B, slot, SL_TRACED | SL_ADDS, v);
+  }
+  hal_start(h2, 2u, offs - 1u);
+  hal_start(h3, 3u, offs - 1u);
+  for (int i = 0; i < n; ++i) {
+    const float s1 = hal_next(h2), s2 = hal_next(h3);
+    const long long slot = c * B.K + k0 + n + i;
+    float W = 0.f, spdf = 0.f;
+    bool ok;
+    v3 bdir = V3(0.f, 0.f, 0.f);
+    const c3 surf = mat_sample(M, sp, wo, bdir, s1, s2,
+                               BSDF_GLOSSY | BSDF_DIFFUSE | BSDF_DISPERSIVE | BSDF_REFLECT | BSDF_TRANSMIT, spdf, W,
+                               ok);
+    float bt, lightPdf;
+    if (!(spdf > 1e-6f && light_hit(L, sp.P, bdir, bt, lightPdf))) {
+      put_slot(B, slot, 0, black);
+      continue;
+    }
+    put_ray(B.s_rays[slot], sp.P, bdir, YK_MIN_RAYDIST, bt);
+    ++nr;
+    if (!(lightPdf > 1e-6f)) {
+      put_slot(B, slot, SL_TRACED, black);
+      continue;
+    }
+    const float lPdf = 1.f / lightPdf;
+    const float l2 = lPdf * lPdf, m2 = spdf * spdf;
+    const float w = m2 / (l2 + m2);
+    // compiled form of "surfCol * lcol * w * W": R,G ((surf*W)*lcol)*w, B (surf*W)*(w*lcol)
+    put_slot(B, slot, SL_TRACED | SL_ADDS,
+             C3(((surf.r * W) * lcol.r) * w, ((surf.g * W) * lcol.g) * w, (surf.b * W) * (w * lcol.b)));
+  }
+  return nr;
+}
+
+// Appends the traced slots [kbeg,kend) of sample c to the shadow queue, in
+// slot order. Whole-wave call.
+__device__ __forceinline__ void flush_shadow(const Batch& B, long long c, int kbeg, int kend, int nr, bool valid) {
+  const unsigned base = wave_append(&B.q_count[2], valid ? (unsigned)nr : 0u);
+  if (!valid || nr == 0) return;
+  unsigned r = base;
+  for (int k = kbeg; k < kend; ++k) {
+    const long long slot = c * B.K + k;
+    if (B.sl_flags[slot] & SL_TRACED) B.s_idx[r++] = (unsigned)slot;
+  }
+}
+
+// Camera-ray hit (pathtracer.cc:146-160, directlight.cc:124-135): emission
+// and the estimateAllDirectLight shadow rays.
+__global__ void __launch_bounds__(256) k_shade_primary(DScene S, Batch B, RenderConst R, long long nc) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = c < nc;
+  int nr = 0, kend = 0;
+  if (valid) {
+    const yk_hit h = B.p_hits[c];
+    c3 col = C3(0.f, 0.f, 0.f);
+    float alpha = R.transp_bg ? 0.f : 1.f;
+    int ph = 0;
+    if (h.prim >= 0) {
+      const yk_ray r = B.p_rays[c];
+      const v3 from = V3(r.from[0], r.from[1], r.from[2]), dir = V3(r.dir[0], r.dir[1], r.dir[2]);
+      const SurfPt sp = make_surface(S, from, dir, h);
+      const DMat& M = c_mats[sp.mat];
+      const v3 wo = vneg(dir);
+      ph = PH_HIT;
+      if (M.flags & BSDF_EMIT) col = cadd(col, mat_emit(M, sp, wo, true));
+      if (M.flags & BSDF_DIFFUSE) {
+        ph |= PH_DIFFUSE;
+        const unsigned s = (unsigned)(c % R.spp);
+        int k0 = 0;
+        for (int l = 0; l < R.nlights; ++l) {
+          nr += gen_light(B, c, k0, l, sp, wo, s, B.soffs[c], (unsigned)l);
+          k0 += 2 * c_lights[l].samples;
+        }
+        kend = k0;
+      }
+      alpha = 1.0f;
+    }
+    B.prim_hit[c] = ph;
+    B.col[3 * c] = col.r;
+    B.col[3 * c + 1] = col.g;
+    B.col[3 * c + 2] = col.b;
+    B.alpha[c] = alpha;
+    B.pathcol[3 * c] = 0.f;
+    B.pathcol[3 * c + 1] = 0.f;
+    B.pathcol[3 * c + 2] = 0.f;
+    B.wlast[c] = 0.f;
+  }
+  flush_shadow(B, c, 0, kend, nr, valid);
+}
+
+// Sums light li's unoccluded slot contributions in reference order:
+// (0 + invNS*ccol) + invNS*ccol2 (mcintegrator.cc:116-191).
+__device__ __forceinline__ c3 resolve_light(const Batch& B, long long c, int k0, int n) {
+  const float invNS = 1.f / (float)n;
+  c3 ccol = C3(0.f, 0.f, 0.f), ccol2 = C3(0.f, 0.f, 0.f);
+  for (int i = 0; i < 2 * n; ++i) {
+    const long long slot = c * B.K + k0 + i;
+    if ((B.sl_flags[slot] & SL_ADDS) && !B.s_occl[slot]) {
+      const c3 v = C3(B.sl_contrib[3 * slot], B.sl_contrib[3 * slot + 1], B.sl_contrib[3 * slot + 2]);
+      if (i < n) ccol = cadd(ccol, v);
+      else ccol2 = cadd(ccol2, v);
+    }
+  }
+  c3 col = C3(0.f, 0.f, 0.f);
+  col = cadd(col, cscale(invNS, ccol));
+  col = cadd(col, cscale(invNS, ccol2));
+  return col;
+}
+
+// col += estimateAllDirectLight (sum over lights, starting from 0)
+__global__ void __launch_bounds__(256) k_resolve_primary(Batch B, RenderConst R, long long nc) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc || !(B.prim_hit[c] & PH_DIFFUSE)) return;
+  c3 dl = C3(0.f, 0.f, 0.f);
+  int k0 = 0;
+  for (int l = 0; l < R.nlights; ++l) {
+    const int n = c_lights[l].samples;
+    dl = cadd(dl, resolve_light(B, c, k0, n));
+    k0 += 2 * n;
+  }
+  B.col[3 * c] = B.col[3 * c] + dl.r;
+  B.col[3 * c + 1] = B.col[3 * c + 1] + dl.g;
+  B.col[3 * c + 2] = B.col[3 * c + 2] + dl.b;
+}
+
+// First segment of sub-path isub: sample the primary BSDF (pathtracer.cc:169-187).
+__global__ void __launch_bounds__(256) k_path_start(DScene S, Batch B, RenderConst R, long long nc, int isub) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = c < nc;
+  bool emit = false;
+  yk_ray r;
+  if (valid) {
+    B.pstate[c] = 0;
+    if (B.prim_hit[c] & PH_DIFFUSE) {
+      const yk_hit h = B.p_hits[c];
+      const yk_ray pr = B.p_rays[c];
+      const v3 from = V3(pr.from[0], pr.from[1], pr.from[2]), dir = V3(pr.dir[0], pr.dir[1], pr.dir[2]);
+      const SurfPt sp = make_surface(S, from, dir, h);
+      const DMat& M = c_mats[sp.mat];
+      const unsigned s = (unsigned)(c % R.spp);
+      const unsigned offs = (unsigned)(R.nsub * (int)s) + B.soffs[c] + (unsigned)isub;
+      const float s1 = ri_vdc(offs, 0u);
+      const float s2 = (float)scr_halton(2, offs);
+      float pdf, W = B.wlast[c];
+      bool ok;
+      v3 pdir = V3(0.f, 0.f, 0.f);
+      c3 scol =
+          mat_sample(M, sp, vneg(dir), pdir, s1, s2, BSDF_DIFFUSE | BSDF_REFLECT | BSDF_TRANSMIT, pdf, W, ok);
+      B.wlast[c] = W;
+      scol = cscale(W, scol);
+      B.thr[3 * c] = scol.r;
+      B.thr[3 * c + 1] = scol.g;
+      B.thr[3 * c + 2] = scol.b;
+      put_ray(r, sp.P, pdir, YK_MIN_RAYDIST, -1.0f);
+      emit = true;
+      B.pstate[c] = PS_ALIVE;
+    }
+  }
+  const unsigned q = wave_append(&B.q_count[1], emit ? 1u : 0u);
+  if (emit) {
+    B.q_rays[1][q] = r;
+    B.qidx[c] = (int)q;
+  }
+}
+
+// Hit at bounce `depth` (1-based) of the current sub-path
+// (pathtracer.cc:189-298): estimateOneDirectLight shadow rays, emission,
+// and the BSDF sample of the next segment.
+__global__ void __launch_bounds__(256) k_shade_bounce(DScene S, Batch B, RenderConst R, long long nc, int depth,
+                                                      int isub, int qin) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = c < nc && (B.pstate[c] & PS_ALIVE);
+  int nr = 0, kend = 0;
+  bool emit_next = false;
+  yk_ray nxt;
+  if (valid) {
+    const int q = B.qidx[c];
+    const yk_hit h = B.q_hits[qin][q];
+    if (h.prim < 0) {
+      B.pstate[c] = 0;  // background: "continue" at depth 1, "break" later
+    } else {
+      const yk_ray pr = B.q_rays[qin][q];
+      const v3 from = V3(pr.from[0], pr.from[1], pr.from[2]), dir = V3(pr.dir[0], pr.dir[1], pr.dir[2]);
+      const SurfPt sp = make_surface(S, from, dir, h);
+      const DMat& M = c_mats[sp.mat];
+      const v3 pwo = vneg(dir);
+      const unsigned s = (unsigned)(c % R.spp);
+      const unsigned offs = (unsigned)(R.nsub * (int)s) + B.soffs[c] + (unsigned)isub;
+      int ps = PS_RESOLVE;
+      // estimateOneDirectLight(state, hit, pwo, offs): always at the first
+      // bounce, for diffuse materials afterwards (mcintegrator.cc:198-215)
+      if ((depth == 1 || (M.flags & BSDF_DIFFUSE)) && R.nlights > 0) {
+        Halton h2;
+        hal_start(h2, 2u, (unsigned)((int)offs - 1));
+        int lnum = (int)(hal_next(h2) * (float)R.nlights);
+        if (lnum > R.nlights - 1) lnum = R.nlights - 1;
+        nr = gen_light(B, c, 0, lnum, sp, pwo, s, B.soffs[c], (unsigned)lnum);
+        kend = 2 * c_lights[lnum].samples;
+        B.lsel[c] = lnum;
+        ps |= PS_EST;
+      }
+      c3 em = C3(0.f, 0.f, 0.f);
+      if (depth == 1 && (M.flags & BSDF_EMIT)) em = mat_emit(M, sp, pwo, false);
+      B.emit_b[3 * c] = em.r;
+      B.emit_b[3 * c + 1] = em.g;
+      B.emit_b[3 * c + 2] = em.b;
+      if (depth < R.bounces) {
+        const float s1 = (float)scr_halton(4 * depth + 3, offs);
+        const float s2 = (float)scr_halton(4 * depth + 4, offs);
+        float pdf, W = B.wlast[c];
+        bool ok;
+        v3 ndir = V3(0.f, 0.f, 0.f);
+        c3 sc = mat_sample(M, sp, pwo, ndir, s1, s2, BSDF_ALL, pdf, W, ok);
+        B.wlast[c] = W;
+        sc = cscale(W, sc);
+        if (!cblack(sc)) {
+          put_ray(nxt, sp.P, ndir, YK_MIN_RAYDIST, -1.0f);
+          emit_next = true;
+          B.scol_next[3 * c] = sc.r;
+          B.scol_next[3 * c + 1] = sc.g;
+          B.scol_next[3 * c + 2] = sc.b;
+          ps |= PS_CONT;
+        }
+      }
+      B.pstate[c] = ps;
+    }
+  }
+  flush_shadow(B, c, 0, kend, nr, valid);
+  const unsigned qn = wave_append(&B.q_count[qin ^ 1], emit_next ? 1u : 0u);
+  if (emit_next) {
+    B.q_rays[qin ^ 1][qn] = nxt;
+    B.qidx[c] = (int)qn;
+  }
+}
+
+// pathCol += lcol*throughput; throughput *= scol of the next segment.
+__global__ void __launch_bounds__(256) k_resolve_bounce(Batch B, RenderConst R, long long nc, int depth) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  const int ps = B.pstate[c];
+  if (!(ps & PS_RESOLVE)) return;
+  c3 lcol = C3(0.f, 0.f, 0.f);
+  if (ps & PS_EST) {
+    const int lnum = B.lsel[c];
+    lcol = cscale((float)R.nlights, resolve_light(B, c, 0, c_lights[lnum].samples));
+  }
+  if (depth == 1) lcol = cadd(lcol, C3(B.emit_b[3 * c], B.emit_b[3 * c + 1], B.emit_b[3 * c + 2]));
+  const c3 thr = C3(B.thr[3 * c], B.thr[3 * c + 1], B.thr[3 * c + 2]);
+  B.pathcol[3 * c] = B.pathcol[3 * c] + lcol.r * thr.r;
+  B.pathcol[3 * c + 1] = B.pathcol[3 * c + 1] + lcol.g * thr.g;
+  B.pathcol[3 * c + 2] = B.pathcol[3 * c + 2] + lcol.b * thr.b;
+  if (ps & PS_CONT) {
+    B.thr[3 * c] = thr.r * B.scol_next[3 * c];
+    B.thr[3 * c + 1] = thr.g * B.scol_next[3 * c + 1];
+    B.thr[3 * c + 2] = thr.b * B.scol_next[3 * c + 2];
+    B.pstate[c] = PS_ALIVE;
+  } else {
+    B.pstate[c] = 0;
+  }
+}
+
+// col += pathCol / nSamples (pathtracer.cc:300-302); final sample (wt = 1)
+__global__ void __launch_bounds__(256) k_finish(Batch B, RenderConst R, long long nc) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  c3 col = C3(B.col[3 * c], B.col[3 * c + 1], B.col[3 * c + 2]);
+  if (R.integrator == YK_INTEGRATOR_PATH && (B.prim_hit[c] & PH_DIFFUSE)) {
+    const float ns = (float)R.nsub;
+    col = cadd(col, C3(B.pathcol[3 * c] / ns, B.pathcol[3 * c + 1] / ns, B.pathcol[3 * c + 2] / ns));
+  }
+  B.samples[c] = make_float4(col.r, col.g, col.b, B.alpha[c]);
+}
+
+// ------------------------------------------------------------ film
+
+struct FilmConst {
+  int cx0, cy0, cx1, cy1, w, h;  // film area (imagefilm.cc:119-127)
+  int tile, ntx;                 // tile size, tiles per row (imagesplitter.cc:29-53)
+  float filterw;
+  double tableScale;
+  int olo_x, ohi_x, olo_y, ohi_y;  // target-source offset window
+  int shard, nshards;
+  int tb0, tb1;                  // batch = owned tile ranks [tb0, tb1)
+  int spp;
+  float d1;
+  float table[256];
+};
+
+__device__ __forceinline__ int round2int(double v) { return (int)(v + (0.5 - 1.4e-11)); }
+__device__ __forceinline__ int floor2int(double v) { return (int)floor(v); }
+
+// imageFilm_t::addSample as a gather (imagefilm.cc:453-511): each thread owns
+// one target pixel and adds every covering sample of the batch's source pixels
+// in the reference's single-thread order (tile, row, column, sample), so the
+// float sums match the sequential CPU splat bit for bit.
+__global__ void __launch_bounds__(256) k_film_gather(FilmConst F, const float4* __restrict__ samples,
+                                                     const int* __restrict__ tile_base, float* __restrict__ film,
+                                                     int rx0, int ry0, int rw, int rh) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= rw * rh) return;
+  const int tx = rx0 + tid % rw, ty = ry0 + tid / rw;
+  if (tx < F.cx0 || tx >= F.cx1 || ty < F.cy0 || ty >= F.cy1) return;
+  // candidate sources, ordered by reference processing order
+  int keys[64];
+  int nk = 0;
+  for (int oy = F.olo_y; oy <= F.ohi_y; ++oy)
+    for (int ox = F.olo_x; ox <= F.ohi_x; ++ox) {
+      const int sx = tx - ox, sy = ty - oy;
+      if (sx < F.cx0 || sx >= F.cx1 || sy < F.cy0 || sy >= F.cy1) continue;
+      const int ti = ((sy - F.cy0) / F.tile) * F.ntx + (sx - F.cx0) / F.tile;
+      if (ti % F.nshards != F.shard) continue;
+      const int rank = ti / F.nshards;
+      if (rank < F.tb0 || rank >= F.tb1) continue;
+      const int key = (ti << 12) | (((sy - F.cy0) % F.tile) << 6) | ((sx - F.cx0) % F.tile);
+      int k = nk++;
+      while (k > 0 && keys[k - 1] > key) {
+        keys[k] = keys[k - 1];
+        --k;
+      }
+      keys[k] = key;
+    }
+  if (nk == 0) return;
+  float* px = film + 5 * ((size_t)(ty - F.cy0) * F.w + (tx - F.cx0));
+  float aR = px[0], aG = px[1], aB = px[2], aA = px[3], aW = px[4];
+  for (int q = 0; q < nk; ++q) {
+    const int ti = keys[q] >> 12, ly = (keys[q] >> 6) & 63, lx = keys[q] & 63;
+    const int tcol = ti % F.ntx, trow = ti / F.ntx;
+    const int X = F.cx0 + tcol * F.tile, Y = F.cy0 + trow * F.tile;
+    const int W = min(F.tile, F.cx1 - X);
+    const int sx = X + lx, sy = Y + ly;
+    const unsigned so = fnv32a((unsigned)sy * fnv32a((unsigned)sx));
+    const long long cbase = tile_base[ti / F.nshards - F.tb0] + (long long)(ly * W + lx) * F.spp;
+    for (int s = 0; s < F.spp; ++s) {
+      float dx = 0.5f, dy = 0.5f;
+      if (F.spp > 1) {
+        dx = (0.5f + (float)s) * F.d1;
+        dy = ri_lp((unsigned)s + so, 0u);
+      }
+      int dx0 = round2int((double)dx - F.filterw), dx1 = round2int((double)dx + F.filterw - 1.0);
+      int dy0 = round2int((double)dy - F.filterw), dy1 = round2int((double)dy + F.filterw - 1.0);
+      dx0 = max(F.cx0 - sx, dx0);
+      dx1 = min(F.cx1 - sx - 1, dx1);
+      dy0 = max(F.cy0 - sy, dy0);
+      dy1 = min(F.cy1 - sy - 1, dy1);
+      const int ox = tx - sx, oy = ty - sy;
+      if (ox < dx0 || ox > dx1 || oy < dy0 || oy > dy1) continue;
+      const int xi = floor2int(fabs(((double)ox - ((double)dx - 0.5)) * F.tableScale));
+      const int yi = floor2int(fabs(((double)oy - ((double)dy - 0.5)) * F.tableScale));
+      const float wt = F.table[yi * 16 + xi];
+      const float4 col = samples[cbase + s];
+      aR = aR + wt * col.x;
+      aG = aG + wt * col.y;
+      aB = aB + wt * col.z;
+      aA = aA + wt * col.w;
+      aW = aW + wt;
+    }
+  }
+  px[0] = aR;
+  px[1] = aG;
+  px[2] = aB;
+  px[3] = aA;
+  px[4] = aW;
+}
+
+// imageFilm_t::flush: pixel_t::normalized (colorA_t / f multiplies by 1.0/f,
+// color.h:329-333) + clampRGB0 (imagefilm.cc:400-424)
+__global__ void k_film_resolve(const float* __restrict__ film, float* __restrict__ rgba, long long npx) {
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npx) return;
+  const float* a = film + 5 * p;
+  float r = 0.f, g = 0.f, b = 0.f, al = 0.f;
+  if (a[4] > 0.f) {
+    const float f = (float)(1.0 / (double)a[4]);
+    r = a[0] * f;
+    g = a[1] * f;
+    b = a[2] * f;
+    al = a[3] * f;
+  }
+  rgba[4 * p] = r < 0.f ? 0.f : r;
+  rgba[4 * p + 1] = g < 0.f ? 0.f : g;
+  rgba[4 * p + 2] = b < 0.f ? 0.f : b;
+  rgba[4 * p + 3] = al;
+}
+
+}  // namespace yk
+
+// ============================================================ host side
+
+using namespace yk;
+
+#define HIPCHK(x)                                                                                \
+  do {                                                                                           \
+    hipError_t e_ = (x);                                                                         \
+    if (e_ != hipSuccess)                                                                        \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e_) + " at " #x); \
+  } while (0)
+
+namespace {
+
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  void ensure(size_t cnt) {
+    if (cnt <= n && p) return;
+    if (p) HIPCHK(hipFree(p));
+    p = nullptr;
+    n = 0;
+    if (cnt == 0) return;
+    HIPCHK(hipMalloc(&p, cnt * sizeof(T)));
+    n = cnt;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  DBuf() = default;
+  DBuf(const DBuf&) = delete;
+  DBuf& operator=(const DBuf&) = delete;
+  ~DBuf() { release(); }
+};
+
+}  // namespace
+
+struct yk_device {
+  int ordinal = 0;
+  int cus = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool uploaded = false;
+  // scene
+  DBuf<float4> tris, ng;
+  DBuf<uint2> nodes;
+  DBuf<uint32_t> leaf;
+  DScene S{};
+  int ntris = 0, max_depth = 0, nlights = 0, sum_light_samples = 0;
+  // traversal work counter + node/tri counters
+  DBuf<unsigned long long> counters;
+  // batch buffers (grown on demand, kept across renders)
+  DBuf<unsigned> soffs, qcount, s_idx;
+  DBuf<float> col, alpha, thr, pathcol, scol_next, wlast, emit_b, sl_contrib;
+  DBuf<int> prim_hit, pstate, lsel, qidx, tile_base;
+  DBuf<int4> tiles;
+  DBuf<yk_ray> p_rays, qr0, qr1, s_rays;
+  DBuf<yk_hit> p_hits, qh0, qh1;
+  DBuf<uint8_t> sl_flags, s_occl;
+  DBuf<float4> samples;
+  ~yk_device() {
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+namespace {
+
+#define YK_GUARD_BEGIN try {
+#define YK_GUARD_END                                                                              \
+  }                                                                                               \
+  catch (const std::bad_alloc&) { return set_error(YK_ERR_ALLOC, "out of host memory"); }        \
+  catch (const std::invalid_argument& e) { return set_error(YK_ERR_ARG, e.what()); }             \
+  catch (const std::runtime_error& e) { return set_error(YK_ERR_HIP, e.what()); }                \
+  catch (const std::exception& e) { return set_error(YK_ERR_INTERNAL, e.what()); }               \
+  catch (...) { return set_error(YK_ERR_INTERNAL, "unknown C++ exception"); }
+
+// host float helpers with the reference's operation order (compiled with
+// -ffp-contract=off, IEEE)
+struct hv3 {
+  float x, y, z;
+};
+hv3 hsub(hv3 a, hv3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+hv3 hadd(hv3 a, hv3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+hv3 hmul(float f, hv3 b) { return {f * b.x, f * b.y, f * b.z}; }
+hv3 hcross(hv3 a, hv3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+hv3 hnorm(hv3 a) {
+  float len = a.x * a.x + a.y * a.y + a.z * a.z;
+  if (len != 0.f) {
+    len = 1.0f / std::sqrt(len);
+    a.x *= len;
+    a.y *= len;
+    a.z *= len;
+  }
+  return a;
+}
+void put3(float* d, hv3 v) {
+  d[0] = v.x;
+  d[1] = v.y;
+  d[2] = v.z;
+}
+
+DCam make_cam(const yk_camera& c) {
+  DCam C{};
+  hv3 pos{c.from[0], c.from[1], c.from[2]}, look{c.to[0], c.to[1], c.to[2]}, up{c.up[0], c.up[1], c.up[2]};
+  const float aspect = c.aspect_ratio * (float)c.resy / (float)c.resx;  // camera.h:44
+  hv3 camY = hsub(up, pos), camZ = hsub(look, pos);
+  hv3 camX = hcross(camZ, camY);
+  camY = hcross(camZ, camX);
+  camX = hnorm(camX);
+  camY = hnorm(camY);
+  camZ = hnorm(camZ);
+  put3(C.pos, pos);
+  put3(C.camZ, camZ);
+  put3(C.near_p, hadd(pos, hmul(c.near_clip, camZ)));
+  put3(C.far_p, hadd(pos, hmul(c.far_clip, camZ)));
+  hv3 vright = camX, vup = hmul(aspect, camY);
+  hv3 vto = hsub(hmul(c.focal, camZ), hmul(0.5f, hadd(vup, vright)));
+  const float ry = 1.0f / (float)c.resy, rx = 1.0f / (float)c.resx;  // compiled form of "/= res"
+  put3(C.vup, {vup.x * ry, vup.y * ry, vup.z * ry});
+  put3(C.vright, {vright.x * rx, vright.y * rx, vright.z * rx});
+  put3(C.vto, vto);
+  return C;
+}
+
+DLight make_light(const yk_light& L) {
+  DLight D{};
+  hv3 corner{L.corner[0], L.corner[1], L.corner[2]}, p1{L.point1[0], L.point1[1], L.point1[2]},
+      p2{L.point2[0], L.point2[1], L.point2[2]};
+  hv3 toX = hsub(p1, corner), toY = hsub(p2, corner);
+  hv3 f = hcross(toY, toX);
+  float vl = f.x * f.x + f.y * f.y + f.z * f.z;  // normLen, vector3d.h:61-70
+  if (vl != 0.f) {
+    vl = std::sqrt(vl);
+    const float d = 1.0f / vl;
+    f.x *= d;
+    f.y *= d;
+    f.z *= d;
+  }
+  put3(D.corner, corner);
+  put3(D.toX, toX);
+  put3(D.toY, toY);
+  put3(D.fnormal, f);
+  put3(D.c2, hadd(corner, toX));
+  put3(D.c3, hadd(corner, hadd(toX, toY)));
+  put3(D.c4, hadd(corner, toY));
+  const float pi = (float)3.14159265358979323846;
+  for (int k = 0; k < 3; ++k) D.color[k] = pi * (L.color[k] * L.power);
+  D.area = vl;
+  D.samples = L.samples;
+  return D;
+}
+
+DMat make_mat(const yk_material& m) {
+  DMat M{};
+  M.type = m.type;
+  if (m.type == YK_MAT_LIGHT) {
+    M.flags = BSDF_EMIT;
+    for (int k = 0; k < 3; ++k) M.col[k] = m.color[k] * m.power;
+    M.double_sided = m.double_sided;
+  } else {
+    M.flags = 0;
+    if (m.emit > 0.f) M.flags |= BSDF_EMIT;
+    if (m.diffuse_reflect > 0.00001f) M.flags |= BSDF_DIFFUSE | BSDF_REFLECT;
+    for (int k = 0; k < 3; ++k) {
+      M.col[k] = m.color[k];
+      M.emit_col[k] = m.emit * m.color[k];
+    }
+    M.diffuse = m.diffuse_reflect;
+  }
+  return M;
+}
+
+void upload_qmc() {
+  QmcTables T{};
+  std::vector<int> fa;
+  int prims[50];
+  prims[0] = 1;
+  int n = 1;
+  for (int c = 2; n < 50; ++c) {
+    bool isp = true;
+    for (int d = 2; d * d <= c; ++d)
+      if (c % d == 0) {
+        isp = false;
+        break;
+      }
+    if (isp) prims[n++] = c;
+  }
+  // Faure permutations by the standard construction (faure_tables.cc)
+  std::vector<std::vector<int>> perm(232);
+  perm[2] = {0, 1};
+  for (int b = 3; b <= 231; ++b) {
+    perm[b].resize(b);
+    if (b % 2 == 0) {
+      const int h = b / 2;
+      for (int i = 0; i < h; ++i) {
+        perm[b][i] = 2 * perm[h][i];
+        perm[b][i + h] = 2 * perm[h][i] + 1;
+      }
+    } else {
+      const int c = (b - 1) / 2;
+      int k = 0;
+      for (int i = 0; i < b - 1; ++i) {
+        if (i == c) perm[b][k++] = c;
+        const int v = perm[b - 1][i];
+        perm[b][k++] = v >= c ? v + 1 : v;
+      }
+    }
+  }
+  for (int d = 0; d < 50; ++d) {
+    T.prims[d] = prims[d];
+    char buf[64];
+    std::snprintf(buf, sizeof buf, "%.9f", 1.0 / prims[d]);
+    T.invprims[d] = std::strtod(buf, nullptr);
+    T.off[d] = (int)fa.size();
+    const std::vector<int>& p = perm[d < 2 ? 3 : prims[d]];
+    for (int i = 0; i < prims[d]; ++i) fa.push_back(p[i]);
+  }
+  if (fa.size() > 5600) throw std::runtime_error("faure table overflow");
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_qmc), &T, sizeof T));
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_faure), fa.data(), fa.size() * sizeof(int)));
+}
+
+int stack_depth(const yk_device* d) { return d->max_depth + 2; }
+
+template <bool CLOSEST>
+void launch_trace(yk_device* d, const yk_ray* rays, const unsigned* idx, long long n, yk_hit* hits, uint8_t* occ,
+                  yk_stats* st) {
+  if (n <= 0) return;
+  unsigned long long* ctr = d->counters.p;
+  HIPCHK(hipMemsetAsync(ctr, 0, 4 * sizeof(unsigned long long), d->stream));
+  const int D = stack_depth(d);
+  const size_t lds = (size_t)3 * D * 64 * sizeof(uint32_t);
+  // persistent grid: enough waves to fill every CU at the LDS-limited occupancy
+  int per_cu = (int)std::min<size_t>(32, (160 * 1024) / std::max<size_t>(lds, 1));
+  if (per_cu < 1) per_cu = 1;
+  long long grid = (long long)d->cus * per_cu;
+  grid = std::min<long long>(grid, (n + 63) / 64);
+  if (grid < 1) grid = 1;
+  HIPCHK(hipEventRecord(d->ev0, d->stream));
+  hipLaunchKernelGGL(k_trace<CLOSEST>, dim3((unsigned)grid), dim3(64), lds, d->stream, d->S, rays, idx, n, hits, occ,
+                     ctr, ctr + 1, D);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(d->ev1, d->stream));
+  unsigned long long h[4];
+  HIPCHK(hipMemcpyAsync(h, ctr, sizeof h, hipMemcpyDeviceToHost, d->stream));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  if (h[3]) throw std::runtime_error("kd-tree traversal watchdog fired on " + std::to_string(h[3]) + " rays");
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, d->ev0, d->ev1));
+  if (!st) return;
+  if (CLOSEST) {
+    st->closest_rays += (uint64_t)n;
+    st->closest_nodes += h[1];
+    st->closest_tris += h[2];
+    st->ms_closest += ms;
+    st->closest_launches++;
+  } else {
+    st->shadow_rays += (uint64_t)n;
+    st->shadow_nodes += h[1];
+    st->shadow_tris += h[2];
+    st->ms_shadow += ms;
+    st->shadow_launches++;
+  }
+}
+
+inline unsigned grid_for(long long n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+
+}  // namespace
+
+extern "C" {
+
+int yk_device_open(int32_t ordinal, yk_device** out) {
+  if (!out) return set_error(YK_ERR_ARG, "yk_device_open: out is NULL");
+  YK_GUARD_BEGIN
+  int n = 0;
+  HIPCHK(hipGetDeviceCount(&n));
+  if (ordinal < 0 || ordinal >= n) return set_error(YK_ERR_ARG, "yk_device_open: no such device");
+  HIPCHK(hipSetDevice(ordinal));
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, ordinal));
+  if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+    return set_error(YK_ERR_UNSUPPORTED, std::string("libyk is built for gfx950, device is ") + prop.gcnArchName);
+  yk_device* d = new yk_device();
+  d->ordinal = ordinal;
+  d->cus = prop.multiProcessorCount;
+  HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreate(&d->ev0));
+  HIPCHK(hipEventCreate(&d->ev1));
+  d->counters.ensure(8);
+  upload_qmc();
+  *out = d;
+  return YK_OK;
+  YK_GUARD_END
+}
+
+void yk_device_close(yk_device* d) {
+  if (!d) return;
+  (void)hipSetDevice(d->ordinal);
+  (void)hipStreamSynchronize(d->stream);
+  delete d;
+}
+
+void* yk_device_stream(yk_device* d) { return d ? (void*)d->stream : nullptr; }
+
+int yk_device_sync(yk_device* d) {
+  if (!d) return set_error(YK_ERR_ARG, "yk_device_sync: NULL device");
+  YK_GUARD_BEGIN
+  HIPCHK(hipStreamSynchronize(d->stream));
+  return YK_OK;
+  YK_GUARD_END
+}
+
+int yk_device_upload(yk_device* d, const yk_scene* s) {
+  if (!d || !s) return set_error(YK_ERR_ARG, "yk_device_upload: NULL argument");
+  const Scene& S = s->s;
+  if (!S.built) return set_error(YK_ERR_STATE, "yk_device_upload: scene not built (call yk_scene_build)");
+  if (!S.has_camera) return set_error(YK_ERR_STATE, "yk_device_upload: scene has no camera");
+  if ((int)S.materials.size() > kMaxMats) return set_error(YK_ERR_UNSUPPORTED, "too many materials");
+  if ((int)S.lights.size() > kMaxLights) return set_error(YK_ERR_UNSUPPORTED, "too many lights");
+  YK_GUARD_BEGIN
+  HIPCHK(hipSetDevice(d->ordinal));
+  const int nt = (int)S.tri_material.size();
+  std::vector<float4> tris((size_t)nt * 3), ng(nt);
+  for (int p = 0; p < nt; ++p) {
+    const float* t = &S.tri_verts[9 * (size_t)p];
+    tris[3 * p] = make_float4(t[0], t[1], t[2], 0.f);
+    tris[3 * p + 1] = make_float4(t[3] - t[0], t[4] - t[1], t[5] - t[2], 0.f);
+    tris[3 * p + 2] = make_float4(t[6] - t[0], t[7] - t[1], t[8] - t[2], 0.f);
+    float nw;
+    int m = S.tri_material[p];
+    std::memcpy(&nw, &m, 4);
+    ng[p] = make_float4(S.tri_normal[3 * p], S.tri_normal[3 * p + 1], S.tri_normal[3 * p + 2], nw);
+  }
+  d->tris.ensure(tris.size());
+  d->ng.ensure(ng.size());
+  const size_t nn = S.tree.nodes.size() / 2;
+  d->nodes.ensure(nn);
+  d->leaf.ensure(std::max<size_t>(S.tree.leaf_prims.size(), 1));
+  HIPCHK(hipMemcpy(d->tris.p, tris.data(), tris.size() * sizeof(float4), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d->ng.p, ng.data(), ng.size() * sizeof(float4), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d->nodes.p, S.tree.nodes.data(), nn * sizeof(uint2), hipMemcpyHostToDevice));
+  if (!S.tree.leaf_prims.empty())
+    HIPCHK(hipMemcpy(d->leaf.p, S.tree.leaf_prims.data(), S.tree.leaf_prims.size() * sizeof(uint32_t),
+                     hipMemcpyHostToDevice));
+  std::vector<DMat> mats;
+  for (const auto& m : S.materials) mats.push_back(make_mat(m));
+  if (!mats.empty()) HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_mats), mats.data(), mats.size() * sizeof(DMat)));
+  std::vector<DLight> lights;
+  int sum_samples = 0;
+  for (const auto& l : S.lights) {
+    if (l.samples < 1) return set_error(YK_ERR_ARG, "light samples must be >= 1");
+    lights.push_back(make_light(l));
+    sum_samples += l.samples;
+  }
+  if (sum_samples > 4096) return set_error(YK_ERR_UNSUPPORTED, "too many light samples per shading point");
+  d->sum_light_samples = sum_samples;
+  if (!lights.empty())
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_lights), lights.data(), lights.size() * sizeof(DLight)));
+  const DCam cam = make_cam(S.camera);
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_cam), &cam, sizeof cam));
+  d->S.tris = d->tris.p;
+  d->S.nodes = d->nodes.p;
+  d->S.leaf = d->leaf.p;
+  d->S.ng = d->ng.p;
+  std::memcpy(d->S.bound, S.tree.bound, sizeof d->S.bound);
+  d->S.nlights = (int)S.lights.size();
+  d->S.nnodes = (unsigned)nn;
+  d->nlights = (int)S.lights.size();
+  d->ntris = nt;
+  d->max_depth = S.tree.max_depth;
+  d->uploaded = true;
+  return YK_OK;
+  YK_GUARD_END
+}
+
+int yk_trace_closest(yk_device* d, const yk_ray* d_rays, int64_t n, yk_hit* d_hits, yk_stats* st) {
+  if (!d || (n > 0 && (!d_rays || !d_hits)) || n < 0) return set_error(YK_ERR_ARG, "yk_trace_closest: bad arguments");
+  if (!d->uploaded) return set_error(YK_ERR_STATE, "yk_trace_closest: no scene uploaded");
+  YK_GUARD_BEGIN
+  HIPCHK(hipSetDevice(d->ordinal));
+  yk_stats local{};
+  launch_trace<true>(d, d_rays, nullptr, n, d_hits, nullptr, st ? st : &local);
+  return YK_OK;
+  YK_GUARD_END
+}
+
+int yk_trace_shadow(yk_device* d, const yk_ray* d_rays, int64_t n, uint8_t* d_occ, yk_stats* st) {
+  if (!d || (n > 0 && (!d_rays || !d_occ)) || n < 0) return set_error(YK_ERR_ARG, "yk_trace_shadow: bad arguments");
+  if (!d->uploaded) return set_error(YK_ERR_STATE, "yk_trace_shadow: no scene uploaded");
+  YK_GUARD_BEGIN
+  HIPCHK(hipSetDevice(d->ordinal));
+  yk_stats local{};
+  launch_trace<false>(d, d_rays, nullptr, n, nullptr, d_occ, st ? st : &local);
+  return YK_OK;
+  YK_GUARD_END
+}
+
+static FilmConst make_film(const yk_render_params* p) {
+  FilmConst F{};
+  F.cx0 = p->xstart;
+  F.cy0 = p->ystart;
+  F.w = p->width;
+  F.h = p->height;
+  F.cx1 = p->xstart + p->width;
+  F.cy1 = p->ystart + p->height;
+  F.tile = p->tile_size > 0 ? p->tile_size : 32;
+  F.ntx = (p->width + F.tile - 1) / F.tile;
+  float fw = (float)((double)p->aa_pixelwidth * 0.5);
+  if (p->filter == YK_FILTER_MITCHELL) fw *= 2.6f;
+  else if (p->filter == YK_FILTER_GAUSS) fw *= 2.f;
+  if (fw < 0.501f) fw = 0.501f;
+  if (fw > 4.f) fw = 4.f;
+  F.filterw = fw;
+  F.tableScale = 0.9999 * 16 / F.filterw;
+  auto r2i = [](double v) { return (int)(v + (0.5 - 1.4e-11)); };
+  // target - source offsets reachable by Round2Int extents for dx in [0,1)
+  F.olo_x = F.olo_y = r2i(0.0 - fw);
+  F.ohi_x = F.ohi_y = r2i(1.0 + fw - 1.0);
+  const float scale = 1.f / 16.f;
+  for (int y = 0; y < 16; ++y)
+    for (int x = 0; x < 16; ++x) {
+      const float fx = (x + .5f) * scale, fy = (y + .5f) * scale;
+      float v = 1.f;
+      if (p->filter == YK_FILTER_MITCHELL) {
+        const float xx = 2.f * std::sqrt(fx * fx + fy * fy);
+        if (xx >= 2.f) v = 0.f;
+        else if (xx >= 1.f) v = (float)(xx * (xx * (xx * -0.38888889f + 2.0f) - 3.33333333f) + 1.77777778f);
+        else v = (float)(xx * xx * (1.16666666f * xx - 2.0f) + 0.88888889f);
+      }
+      F.table[y * 16 + x] = v;
+    }
+  F.spp = p->aa_samples > 0 ? p->aa_samples : 1;
+  F.d1 = (float)(1.0 / (double)(float)F.spp);
+  return F;
+}
+
+int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int32_t nshards, float* d_film,
+                    yk_stats* st) {
+  if (!d || !p || !d_film || nshards < 1 || shard < 0 || shard >= nshards)
+    return set_error(YK_ERR_ARG, "yk_render_shard: bad arguments");
+  if (!d->uploaded) return set_error(YK_ERR_STATE, "yk_render_shard: no scene uploaded");
+  if (p->aa_passes != 1) return set_error(YK_ERR_UNSUPPORTED, "only AA_passes = 1 is supported");
+  if (p->filter != YK_FILTER_BOX && p->filter != YK_FILTER_MITCHELL)
+    return set_error(YK_ERR_UNSUPPORTED, "filter not supported (box, mitchell)");
+  if (p->integrator != YK_INTEGRATOR_PATH && p->integrator != YK_INTEGRATOR_DIRECT)
+    return set_error(YK_ERR_ARG, "unknown integrator");
+  if (p->integrator == YK_INTEGRATOR_PATH && p->caustic_type != YK_CAUSTIC_NONE)
+    return set_error(YK_ERR_UNSUPPORTED, "pathtracing needs caustic_type none");
+  if (p->integrator == YK_INTEGRATOR_PATH && (p->bounces < 1 || 4 * p->bounces + 4 >= 50))
+    return set_error(YK_ERR_UNSUPPORTED, "bounces must be in [1, 11]");
+  if (p->width <= 0 || p->height <= 0) return set_error(YK_ERR_ARG, "empty render area");
+  YK_GUARD_BEGIN
+  HIPCHK(hipSetDevice(d->ordinal));
+  auto t0 = std::chrono::steady_clock::now();
+  FilmConst F = make_film(p);
+  if ((F.ohi_x - F.olo_x + 1) * (F.ohi_y - F.olo_y + 1) > 64)
+    return set_error(YK_ERR_UNSUPPORTED, "filter window too large");
+  if (F.tile > 64) return set_error(YK_ERR_UNSUPPORTED, "tile_size > 64");
+  F.shard = shard;
+  F.nshards = nshards;
+  const int spp = F.spp;
+  const int nty = (p->height + F.tile - 1) / F.tile;
+  const int ntiles = F.ntx * nty;
+  if (ntiles >= (1 << 19)) return set_error(YK_ERR_UNSUPPORTED, "too many tiles");
+  std::vector<int> owned;
+  for (int t = shard; t < ntiles; t += nshards) owned.push_back(t);
+  RenderConst R{};
+  R.spp = spp;
+  R.nsub = p->integrator == YK_INTEGRATOR_PATH ? std::max(1, p->path_samples) : 1;
+  R.bounces = p->bounces;
+  R.integrator = p->integrator;
+  R.transp_bg = p->transp_background;
+  R.nlights = d->nlights;
+  R.d1 = F.d1;
+  const int K = std::max(1, 2 * d->sum_light_samples);
+  // batch = whole tiles, about 2M camera samples
+  const long long target = 2ll << 20;
+  const long long tile_samples = (long long)F.tile * F.tile * spp;
+  const int tiles_per_batch = (int)std::max<long long>(1, target / tile_samples);
+  const long long maxc = (long long)tiles_per_batch * tile_samples;
+  d->soffs.ensure(maxc);
+  d->col.ensure(3 * maxc);
+  d->alpha.ensure(maxc);
+  d->prim_hit.ensure(maxc);
+  d->p_rays.ensure(maxc);
+  d->p_hits.ensure(maxc);
+  d->thr.ensure(3 * maxc);
+  d->pathcol.ensure(3 * maxc);
+  d->scol_next.ensure(3 * maxc);
+  d->wlast.ensure(maxc);
+  d->emit_b.ensure(3 * maxc);
+  d->pstate.ensure(maxc);
+  d->lsel.ensure(maxc);
+  d->qidx.ensure(maxc);
+  d->qr0.ensure(maxc);
+  d->qr1.ensure(maxc);
+  d->qh0.ensure(maxc);
+  d->qh1.ensure(maxc);
+  d->qcount.ensure(4);
+  d->s_rays.ensure(maxc * K);
+  d->s_occl.ensure(maxc * K);
+  d->s_idx.ensure(maxc * K);
+  d->sl_contrib.ensure(3 * maxc * K);
+  d->sl_flags.ensure(maxc * K);
+  d->samples.ensure(maxc);
+  d->tiles.ensure(tiles_per_batch);
+  d->tile_base.ensure(tiles_per_batch + 1);
+  Batch B{};
+  B.prim_hit = d->prim_hit.p;
+  B.soffs = d->soffs.p;
+  B.col = d->col.p;
+  B.alpha = d->alpha.p;
+  B.p_rays = d->p_rays.p;
+  B.p_hits = d->p_hits.p;
+  B.thr = d->thr.p;
+  B.pathcol = d->pathcol.p;
+  B.scol_next = d->scol_next.p;
+  B.wlast = d->wlast.p;
+  B.emit_b = d->emit_b.p;
+  B.pstate = d->pstate.p;
+  B.lsel = d->lsel.p;
+  B.qidx = d->qidx.p;
+  B.q_rays[0] = d->qr0.p;
+  B.q_rays[1] = d->qr1.p;
+  B.q_hits[0] = d->qh0.p;
+  B.q_hits[1] = d->qh1.p;
+  B.q_count = d->qcount.p;
+  B.s_rays = d->s_rays.p;
+  B.s_occl = d->s_occl.p;
+  B.s_idx = d->s_idx.p;
+  B.sl_contrib = d->sl_contrib.p;
+  B.sl_flags = d->sl_flags.p;
+  B.samples = d->samples.p;
+  B.K = K;
+  yk_stats local{};
+  yk_stats* S = st ? st : &local;
+  unsigned qc[4];
+  auto read_counts = [&]() {
+    HIPCHK(hipMemcpyAsync(qc, d->qcount.p, sizeof qc, hipMemcpyDeviceToHost, d->stream));
+    HIPCHK(hipStreamSynchronize(d->stream));
+  };
+  auto trace_shadow_queue = [&]() {
+    read_counts();
+    launch_trace<false>(d, B.s_rays, B.s_idx, qc[2], nullptr, B.s_occl, S);
+  };
+  for (size_t tb0 = 0; tb0 < owned.size(); tb0 += tiles_per_batch) {
+    const size_t tb1 = std::min(owned.size(), tb0 + (size_t)tiles_per_batch);
+    std::vector<int4> tl;
+    std::vector<int> base;
+    long long nc = 0;
+    int rx0 = 1 << 30, ry0 = 1 << 30, rx1 = -(1 << 30), ry1 = -(1 << 30);
+    for (size_t k = tb0; k < tb1; ++k) {
+      const int t = owned[k];
+      const int X = F.cx0 + (t % F.ntx) * F.tile, Y = F.cy0 + (t / F.ntx) * F.tile;
+      const int W = std::min(F.tile, F.cx1 - X), H = std::min(F.tile, F.cy1 - Y);
+      tl.push_back(make_int4(X, Y, W, H));
+      base.push_back((int)nc);
+      nc += (long long)W * H * spp;
+      rx0 = std::min(rx0, X);
+      ry0 = std::min(ry0, Y);
+      rx1 = std::max(rx1, X + W);
+      ry1 = std::max(ry1, Y + H);
+    }
+    base.push_back((int)nc);
+    HIPCHK(hipMemcpyAsync(d->tiles.p, tl.data(), tl.size() * sizeof(int4), hipMemcpyHostToDevice, d->stream));
+    HIPCHK(hipMemcpyAsync(d->tile_base.p, base.data(), base.size() * sizeof(int), hipMemcpyHostToDevice, d->stream));
+    HIPCHK(hipStreamSynchronize(d->stream));  // host vectors die with this iteration
+    TileList TL{d->tiles.p, d->tile_base.p, (int)tl.size()};
+    HIPCHK(hipMemsetAsync(d->qcount.p, 0, 4 * sizeof(unsigned), d->stream));
+    hipLaunchKernelGGL(k_camera, dim3(grid_for(nc)), dim3(256), 0, d->stream, TL, B, R, nc);
+    HIPCHK(hipGetLastError());
+    launch_trace<true>(d, B.p_rays, nullptr, nc, B.p_hits, nullptr, S);
+    hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(nc)), dim3(256), 0, d->stream, d->S, B, R, nc);
+    HIPCHK(hipGetLastError());
+    trace_shadow_queue();
+    hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(nc)), dim3(256), 0, d->stream, B, R, nc);
+    HIPCHK(hipGetLastError());
+    if (p->integrator == YK_INTEGRATOR_PATH) {
+      // sub-path index outermost: pathCol is shared across sub-paths and
+      // accumulated in the reference's order (pathtracer.cc:164-298)
+      for (int isub = 0; isub < R.nsub; ++isub) {
+        HIPCHK(hipMemsetAsync(d->qcount.p, 0, 4 * sizeof(unsigned), d->stream));
+        hipLaunchKernelGGL(k_path_start, dim3(grid_for(nc)), dim3(256), 0, d->stream, d->S, B, R, nc, isub);
+        HIPCHK(hipGetLastError());
+        int qin = 1;
+        for (int depth = 1; depth <= R.bounces; ++depth) {
+          read_counts();
+          const unsigned nq = qc[qin];
+          if (nq == 0) break;
+          launch_trace<true>(d, B.q_rays[qin], nullptr, nq, B.q_hits[qin], nullptr, S);
+          HIPCHK(hipMemsetAsync(d->qcount.p + 2, 0, sizeof(unsigned), d->stream));
+          HIPCHK(hipMemsetAsync(d->qcount.p + (qin ^ 1), 0, sizeof(unsigned), d->stream));
+          hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(nc)), dim3(256), 0, d->stream, d->S, B, R, nc, depth, isub,
+                             qin);
+          HIPCHK(hipGetLastError());
+          trace_shadow_queue();
+          hipLaunchKernelGGL(k_resolve_bounce, dim3(grid_for(nc)), dim3(256), 0, d->stream, B, R, nc, depth);
+          HIPCHK(hipGetLastError());
+          qin ^= 1;
+        }
+      }
+    }
+    hipLaunchKernelGGL(k_finish, dim3(grid_for(nc)), dim3(256), 0, d->stream, B, R, nc);
+    HIPCHK(hipGetLastError());
+    // film: targets = batch rect grown by the filter window
+    FilmConst Fb = F;
+    Fb.tb0 = (int)tb0;
+    Fb.tb1 = (int)tb1;
+    const int gx0 = std::max(F.cx0, rx0 + F.olo_x), gy0 = std::max(F.cy0, ry0 + F.olo_y);
+    const int gx1 = std::min(F.cx1, rx1 + F.ohi_x), gy1 = std::min(F.cy1, ry1 + F.ohi_y);
+    const int gw = gx1 - gx0, gh = gy1 - gy0;
+    if (gw > 0 && gh > 0) {
+      hipLaunchKernelGGL(k_film_gather, dim3(grid_for((long long)gw * gh)), dim3(256), 0, d->stream, Fb, B.samples,
+                         d->tile_base.p, d_film, gx0, gy0, gw, gh);
+      HIPCHK(hipGetLastError());
+    }
+    S->camera_samples += (uint64_t)nc;
+  }
+  HIPCHK(hipStreamSynchronize(d->stream));
+  S->ms_total += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return YK_OK;
+  YK_GUARD_END
+}
+
+int yk_film_resolve(yk_device* d, const yk_render_params* p, const float* d_film, float* d_rgba) {
+  if (!d || !p || !d_film || !d_rgba) return set_error(YK_ERR_ARG, "yk_film_resolve: NULL argument");
+  YK_GUARD_BEGIN
+  HIPCHK(hipSetDevice(d->ordinal));
+  const long long npx = (long long)p->width * p->height;
+  hipLaunchKernelGGL(k_film_resolve, dim3(grid_for(npx)), dim3(256), 0, d->stream, d_film, d_rgba, npx);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(d->stream));
+  return YK_OK;
+  YK_GUARD_END
+}
+
+int yk_render(yk_device* d, const yk_render_params* p, float* rgba_host, yk_stats* st) {
+  if (!d || !p || !rgba_host) return set_error(YK_ERR_ARG, "yk_render: NULL argument");
+  YK_GUARD_BEGIN
+  HIPCHK(hipSetDevice(d->ordinal));
+  const size_t npx = (size_t)p->width * p->height;
+  float *film = nullptr, *rgba = nullptr;
+  HIPCHK(hipMalloc(&film, npx * 5 * sizeof(float)));
+  HIPCHK(hipMalloc(&rgba, npx * 4 * sizeof(float)));
+  HIPCHK(hipMemsetAsync(film, 0, npx * 5 * sizeof(float), d->stream));
+  int rc = yk_render_shard(d, p, 0, 1, film, st);
+  if (rc == YK_OK) rc = yk_film_resolve(d, p, film, rgba);
+  if (rc == YK_OK) HIPCHK(hipMemcpy(rgba_host, rgba, npx * 4 * sizeof(float), hipMemcpyDeviceToHost));
+  (void)hipFree(film);
+  (void)hipFree(rgba);
+  return rc;
+  YK_GUARD_END
+}
+
+}  // extern "C"

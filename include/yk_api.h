@@ -164,7 +164,10 @@ int yk_device_sync(yk_device* d);
 void* yk_device_stream(yk_device* d);
 
 /* batched ray queries on device memory; bit-exact with the reference
- * triKdTree_t::Intersect (closest) and scene_t::isShadowed (any hit). */
+ * triKdTree_t::Intersect (closest) and scene_t::isShadowed (any hit).
+ * Closest: hits with tmin <= t < (tmax < 0 ? inf : tmax); prim -1 = miss.
+ * Shadow: isShadowed(from, dir, tmin, tmax) semantics -- the query ray
+ * starts at from + tmin*dir and reaches tmax - 2*tmin (scene.cc:884-889). */
 int yk_trace_closest(yk_device* d, const yk_ray* d_rays, int64_t n, yk_hit* d_hits, yk_stats* st);
 int yk_trace_shadow(yk_device* d, const yk_ray* d_rays, int64_t n, uint8_t* d_occluded, yk_stats* st);
 

@@ -45,8 +45,12 @@ def lib():
     return _lib
 
 
+_active = None
+
+
 class Oracle:
-    """Holds one scene; arrays are kept alive for the C side."""
+    """Holds one scene; arrays are kept alive for the C side. The C oracle has
+    a single global scene, so every query re-activates its own scene first."""
 
     def __init__(self, scene):
         from core_amd import _abi as A
@@ -58,12 +62,22 @@ class Oracle:
         self._mats = (A.yk_material * max(len(mats), 1))(*mats)
         self._lights = (A.yk_light * max(len(lights), 1))(*lights)
         self._cam = scene.camera()
+        self._nmats, self._nlights = len(mats), len(lights)
+        self._activate()
+
+    def _activate(self):
+        global _active
+        if _active is self:
+            return
+        e = self.arrays
         lib().orc_load(e["tri_verts"].ctypes.data, e["tri_material"].ctypes.data, len(e["tri_material"]),
                        e["nodes"].ctypes.data, e["leaf_prims"].ctypes.data, e["bound"].ctypes.data,
-                       C.addressof(self._mats), len(mats), C.addressof(self._lights), len(lights),
+                       C.addressof(self._mats), self._nmats, C.addressof(self._lights), self._nlights,
                        C.addressof(self._cam))
+        _active = self
 
     def render(self, params):
+        self._activate()
         A = self._A
         w, h = params.width, params.height
         rgba = np.zeros((h, w, 4), np.float32)
@@ -78,6 +92,7 @@ class Oracle:
 
     def intersect(self, rays):
         """rays: (n,8) float32 [from, dir, tmin, tmax] -> (prim int32, t, b1, b2), counters"""
+        self._activate()
         rays = np.ascontiguousarray(rays, np.float32)
         n = len(rays)
         hits = np.zeros((n, 4), np.float32)
@@ -86,6 +101,7 @@ class Oracle:
         return hits.view(np.int32)[:, 0].copy(), hits[:, 1].copy(), hits[:, 2].copy(), hits[:, 3].copy(), cnt
 
     def shadow(self, rays):
+        self._activate()
         rays = np.ascontiguousarray(rays, np.float32)
         n = len(rays)
         occ = np.zeros(n, np.uint8)
@@ -94,6 +110,7 @@ class Oracle:
         return occ, cnt
 
     def camera_rays(self, x0, y0, w, h, spp):
+        self._activate()
         out = np.zeros((h * w * spp, 8), np.float32)
         lib().orc_camera_rays(x0, y0, w, h, spp, out.ctypes.data)
         return out

@@ -1,0 +1,137 @@
+"""HIP path vs the CPU oracle, through the C-ABI (libyk.so).
+
+Traversal: prim id, t, b1, b2 bit-exact, and the per-batch kd-tree work
+counters (nodes visited, triangle tests) equal to the oracle's -- the device
+walks exactly the reference's node sequence (kdtree.cc:675-947).
+Rendering: film sums (R,G,B,A,weight per pixel) bit-exact on 1-device runs;
+ray counts (scene_t::intersect / isShadowed calls) exact.
+"""
+import numpy as np
+import pytest
+
+from core_amd import _abi as A
+from core_amd.scene import probe_scene
+from oracle.oracle import Oracle
+from tests.raygen import edge_rays, random_rays
+
+pytestmark = pytest.mark.gpu
+
+_SCENES = {}
+
+
+def scene(name, resx, resy, nu=0, nv=0):
+    key = (name, resx, resy, nu, nv)
+    if key not in _SCENES:
+        s, p = probe_scene(name, resx, resy, nu, nv)
+        _SCENES[key] = (s, p, Oracle(s))
+    return _SCENES[key]
+
+
+SCENE_CASES = [("cornell_pt", 64, 64, 0, 0), ("bumpy", 64, 64, 120, 61), ("bumpy", 64, 64, 1000, 501)]
+
+
+def _ray_batch(s, seed):
+    e = s.export()
+    b = e["bound"]
+    return np.concatenate([random_rays(b, 20000, seed), random_rays(b, 4000, seed + 1, tmax=0.5),
+                           edge_rays(b, e["nodes"], seed + 2)])
+
+
+@pytest.mark.parametrize("case", SCENE_CASES, ids=lambda c: f"{c[0]}{c[3]}")
+def test_trace_closest_bit_exact(gpu_device, case):
+    s, _, orc = scene(*case)
+    rays = _ray_batch(s, 11)
+    prim, t, b1, b2, cnt = orc.intersect(rays)
+    gpu_device.upload(s)
+    st = A.yk_stats()
+    hits = gpu_device.trace_closest(gpu_device.rays_to_device(rays), st)
+    gp, gt, gb1, gb2 = gpu_device.split_hits(hits)
+    assert (gp == prim).all(), f"{(gp != prim).sum()} prim mismatches"
+    hit = prim >= 0
+    assert hit.sum() > len(rays) // 4
+    for a, b in ((gt, t), (gb1, b1), (gb2, b2)):
+        assert (a[hit].view(np.uint32) == b[hit].view(np.uint32)).all()
+    assert st.closest_nodes == cnt[0] and st.closest_tris == cnt[1]
+
+
+@pytest.mark.parametrize("case", SCENE_CASES, ids=lambda c: f"{c[0]}{c[3]}")
+def test_trace_shadow_bit_exact(gpu_device, case):
+    s, _, orc = scene(*case)
+    rays = _ray_batch(s, 23)
+    rays[:, 6] = 0.0005  # isShadowed bias as the integrators pass it
+    rays[::2, 7] = np.abs(rays[::2, 7]) + 0.3  # bounded segments
+    occ, cnt = orc.shadow(rays)
+    gpu_device.upload(s)
+    st = A.yk_stats()
+    gocc = gpu_device.trace_shadow(gpu_device.rays_to_device(rays), st).cpu().numpy()
+    assert (gocc == occ).all(), f"{(gocc != occ).sum()} mismatches"
+    assert 0 < occ.sum() < len(occ)
+    assert st.shadow_nodes == cnt[0] and st.shadow_tris == cnt[1]
+
+
+def test_trace_empty_and_degenerate(gpu_device):
+    s, _, orc = scene("cornell_pt", 64, 64)
+    gpu_device.upload(s)
+    d = gpu_device.rays_to_device(np.zeros((0, 8), np.float32))
+    assert gpu_device.trace_closest(d).shape == (0, 4)
+    # zero direction: bound_cross rejects -> miss; NaN-free result
+    rays = np.zeros((64, 8), np.float32)
+    rays[:, 7] = -1
+    prim, *_ = orc.intersect(rays)
+    gp, *_ = gpu_device.split_hits(gpu_device.trace_closest(gpu_device.rays_to_device(rays)))
+    assert (gp == prim).all()
+
+
+def _render_pair(gpu_device, case, crop, **over):
+    s, p, orc = scene(*case)
+    p = A.yk_render_params.from_buffer_copy(p)
+    p.xstart, p.ystart, p.width, p.height = crop
+    for k, v in over.items():
+        setattr(p, k, v)
+    rgba_o, sums_o, cnt_o = orc.render(p)
+    gpu_device.upload(s)
+    film = gpu_device.new_film(p)
+    st = gpu_device.render_shard(p, film)
+    rgba_g = gpu_device.film_resolve(p, film).cpu().numpy()
+    return sums_o, film.cpu().numpy(), rgba_o, rgba_g, cnt_o, st
+
+
+RENDER_CASES = [
+    ("dl_cornell", ("cornell_dl", 128, 128, 0, 0), (16, 20, 80, 72), {}),
+    ("pt_cornell", ("cornell_pt", 64, 64, 0, 0), (0, 0, 64, 64), {}),
+    ("pt_cornell_mitchell", ("cornell_pt", 64, 64, 0, 0), (5, 3, 50, 45), {"filter": A.YK_FILTER_MITCHELL}),
+    ("pt_cornell_2sub", ("cornell_pt", 48, 48, 0, 0), (0, 0, 48, 48), {"path_samples": 2, "aa_samples": 3}),
+    ("pt_bumpy", ("bumpy", 96, 54, 120, 61), (0, 0, 96, 54), {}),
+    ("pt_bumpy_tile16", ("bumpy", 96, 54, 120, 61), (10, 5, 70, 40), {"tile_size": 16, "bounces": 5}),
+]
+
+
+@pytest.mark.parametrize("name,case,crop,over", RENDER_CASES, ids=[c[0] for c in RENDER_CASES])
+def test_render_bit_exact(gpu_device, name, case, crop, over):
+    sums_o, sums_g, rgba_o, rgba_g, cnt, st = _render_pair(gpu_device, case, crop, **over)
+    assert st.closest_rays == cnt["closest"], (st.closest_rays, cnt["closest"])
+    assert st.shadow_rays == cnt["shadow"], (st.shadow_rays, cnt["shadow"])
+    diff = sums_g.view(np.uint32) != sums_o.view(np.uint32)
+    assert not diff.any(), f"{diff.sum()} film floats differ; max abs {np.abs(sums_g - sums_o).max()}"
+    assert (rgba_g.view(np.uint32) == rgba_o.view(np.uint32)).all()
+    assert st.closest_nodes == cnt["closest_nodes"] and st.shadow_tris == cnt["shadow_tris"]
+
+
+def test_render_sharded_sum(gpu_device):
+    """Tile sharding (tile t -> shard t % n): per-shard films summed equal the
+    1-shard film within float reassociation, and rays split exactly."""
+    s, p, orc = scene("cornell_pt", 64, 64)
+    p = A.yk_render_params.from_buffer_copy(p)
+    gpu_device.upload(s)
+    f1 = gpu_device.new_film(p)
+    st1 = gpu_device.render_shard(p, f1)
+    tot = None
+    rays = 0
+    for k in range(3):
+        f = gpu_device.new_film(p)
+        st = gpu_device.render_shard(p, f, k, 3)
+        rays += st.closest_rays + st.shadow_rays
+        tot = f if tot is None else tot + f
+    assert rays == st1.closest_rays + st1.shadow_rays
+    a, b = tot.cpu().numpy(), f1.cpu().numpy()
+    assert np.allclose(a, b, rtol=1e-6, atol=1e-6)
