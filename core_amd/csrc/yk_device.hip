@@ -109,9 +109,34 @@ __device__ __forceinline__ bool bound_cross(const float* bb, v3 from, v3 dir, fl
 
 // Exit-point stack. The reference keeps {node*, t, pb[3], prev} per entry
 // (kdtree.h:103-109); exits form a LIFO (prev links). Here the current entry
-// and exit live in registers and older exits in LDS as {t, split, node|code}:
-// on pop, pb is regenerated bit-exactly as pb[code] = split and the other
-// axes from + t*dir (code 3 = the initial exit, all three axes from t).
+// and exit live in registers and older exits on a per-lane stack of 8-byte
+// entries {split, far node | axis<<30}. On pop, t is recomputed with the
+// push-time expression (split - from[axis]) * invDir[axis] and pb as
+// pb[axis] = split, other axes from + t*dir -- the same float operations on
+// the same inputs, so bit-identical. Axis code 3 is the initial exit, whose
+// entry stores t itself. The top kStackLds entries of every lane live in an
+// LDS ring; deeper ones spill to a global overflow area (rare: a 1M-tri tree
+// has depth ~40 but a ray rarely holds more than a dozen pending exits).
+constexpr int kStackLds = 16;
+
+struct LaneStack {
+  uint2* lds;       // [kStackLds][64]
+  uint2* ovf;       // [depth - kStackLds][ovf_stride]
+  unsigned stride;  // lanes in the grid
+  unsigned gl;      // this lane's global index
+  int lane;
+  __device__ __forceinline__ void push(int sp, uint2 e) const {
+    uint2* slot = lds + (sp & (kStackLds - 1)) * 64 + lane;
+    if (sp >= kStackLds) ovf[(size_t)(sp - kStackLds) * stride + gl] = *slot;
+    *slot = e;
+  }
+  __device__ __forceinline__ uint2 pop(int sp) const {  // sp = index of the entry to pop
+    uint2* slot = lds + (sp & (kStackLds - 1)) * 64 + lane;
+    const uint2 e = *slot;
+    if (sp >= kStackLds) *slot = ovf[(size_t)(sp - kStackLds) * stride + gl];
+    return e;
+  }
+};
 struct Trav {
   v3 o, d, inv;
   float tmin, dist;
@@ -153,7 +178,7 @@ __device__ __forceinline__ bool trav_begin(const DScene& S, Trav& st, const yk_r
   st.en_pb = (a >= 0.0f) ? vadd(st.o, vmul(a, st.d)) : st.o;
   st.ex_t = b;
   st.ex_code = 3;
-  st.ex_split = 0.f;
+  st.ex_split = b;  // code 3 entries carry t
   st.ex_node = -1;
   exit_pb(st);
   st.node = 0;
@@ -165,9 +190,8 @@ __device__ __forceinline__ bool trav_begin(const DScene& S, Trav& st, const yk_r
 // descend to a leaf, test its primitives, then stop or pop. Returns true when
 // the ray is finished.
 template <bool CLOSEST>
-__device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, float* __restrict__ st_t,
-                                          float* __restrict__ st_s, uint32_t* __restrict__ st_n, int lane,
-                                          unsigned& nnodes, unsigned& ntris, bool& occluded) {
+__device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneStack& stk, unsigned& nnodes,
+                                          unsigned& ntris, bool& occluded) {
   if (st.dist < st.en_t) return true;
   int node = st.node;
   uint2 nd = S.nodes[node];
@@ -204,10 +228,7 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, float* __re
       node = right;
     }
     const float t = (split - vget(st.o, axis)) * vget(st.inv, axis);
-    const int slot = st.sp * 64 + lane;
-    st_t[slot] = st.ex_t;
-    st_s[slot] = st.ex_split;
-    st_n[slot] = ((uint32_t)(st.ex_node + 1)) | ((uint32_t)st.ex_code << 30);
+    stk.push(st.sp, make_uint2(__float_as_uint(st.ex_split), ((uint32_t)(st.ex_node + 1)) | ((uint32_t)st.ex_code << 30)));
     st.sp++;
     st.ex_t = t;
     st.ex_split = split;
@@ -248,12 +269,11 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, float* __re
     return true;
   }
   st.sp--;
-  const int slot = st.sp * 64 + lane;
-  st.ex_t = st_t[slot];
-  st.ex_split = st_s[slot];
-  const uint32_t w = st_n[slot];
-  st.ex_node = (int)(w & 0x3FFFFFFFu) - 1;
-  st.ex_code = (int)(w >> 30);
+  const uint2 e = stk.pop(st.sp);
+  st.ex_split = __uint_as_float(e.x);
+  st.ex_node = (int)(e.y & 0x3FFFFFFFu) - 1;
+  st.ex_code = (int)(e.y >> 30);
+  st.ex_t = (st.ex_code == 3) ? st.ex_split : (st.ex_split - vget(st.o, st.ex_code)) * vget(st.inv, st.ex_code);
   exit_pb(st);
   return false;
 }
@@ -275,12 +295,10 @@ __global__ void __launch_bounds__(64) k_trace(DScene S, const yk_ray* __restrict
                                               const unsigned* __restrict__ idx, long long n,
                                               yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
                                               unsigned long long* __restrict__ work,
-                                              unsigned long long* __restrict__ ctr, int D) {
-  extern __shared__ uint32_t lds[];
-  float* st_t = reinterpret_cast<float*>(lds);
-  float* st_s = reinterpret_cast<float*>(lds + D * 64);
-  uint32_t* st_n = lds + 2 * D * 64;
+                                              unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf) {
+  __shared__ uint2 lds[kStackLds * 64];
   const int lane = threadIdx.x;
+  const LaneStack stk{lds, ovf, gridDim.x * 64u, blockIdx.x * 64u + (unsigned)lane, lane};
   long long rid = -1;
   bool exhausted = false;
   Trav st;
@@ -318,7 +336,7 @@ __global__ void __launch_bounds__(64) k_trace(DScene S, const yk_ray* __restrict
     }
     if (rid >= 0) {
       bool occ = false;
-      bool done = trav_step<CLOSEST>(S, st, st_t, st_s, st_n, lane, nnodes, ntris, occ);
+      bool done = trav_step<CLOSEST>(S, st, stk, nnodes, ntris, occ);
       if (++steps > (1u << 22)) {  // watchdog: no ray of a valid tree gets near this
         st.prim = -2;
         done = true;
@@ -535,6 +553,7 @@ struct Batch {
   float* sl_contrib;    // 3 floats per slot
   uint8_t* sl_flags;    // 1 per slot
   float4* samples;      // final RGBA per camera sample
+  float2* sxy;          // (dx, dy) of the sample inside its pixel
   int K;
 };
 
@@ -579,6 +598,7 @@ __global__ void __launch_bounds__(256) k_camera(TileList TL, Batch B, RenderCons
     dx = (0.5f + (float)s) * R.d1;
     dy = ri_lp((unsigned)s + so, 0u);
   }
+  B.sxy[c] = make_float2(dx, dy);
   const float px = (float)j + dx, py = (float)i + dy;
   const v3 vr = ld3(c_cam.vright), vu = ld3(c_cam.vup), vt = ld3(c_cam.vto), cz = ld3(c_cam.camZ);
   v3 d = vadd(vadd(vmul(px, vr), vmul(py, vu)), vt);
@@ -950,71 +970,64 @@ __device__ __forceinline__ int round2int(double v) { return (int)(v + (0.5 - 1.4
 __device__ __forceinline__ int floor2int(double v) { return (int)floor(v); }
 
 // imageFilm_t::addSample as a gather (imagefilm.cc:453-511): each thread owns
-// one target pixel and adds every covering sample of the batch's source pixels
-// in the reference's single-thread order (tile, row, column, sample), so the
-// float sums match the sequential CPU splat bit for bit.
+// one target pixel and adds every covering sample of the batch in the
+// reference's single-thread order -- tiles row-major, then rows, columns and
+// samples -- so the float sums match the sequential CPU splat bit for bit.
+// Candidate sources are walked in that order directly: the tiles the filter
+// window touches in row-major tile order, inside each its window rows and
+// columns.
 __global__ void __launch_bounds__(256) k_film_gather(FilmConst F, const float4* __restrict__ samples,
-                                                     const int* __restrict__ tile_base, float* __restrict__ film,
-                                                     int rx0, int ry0, int rw, int rh) {
+                                                     const float2* __restrict__ sxy, const int* __restrict__ tile_base,
+                                                     float* __restrict__ film, int rx0, int ry0, int rw, int rh) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (tid >= rw * rh) return;
   const int tx = rx0 + tid % rw, ty = ry0 + tid / rw;
   if (tx < F.cx0 || tx >= F.cx1 || ty < F.cy0 || ty >= F.cy1) return;
-  // candidate sources, ordered by reference processing order
-  int keys[64];
-  int nk = 0;
-  for (int oy = F.olo_y; oy <= F.ohi_y; ++oy)
-    for (int ox = F.olo_x; ox <= F.ohi_x; ++ox) {
-      const int sx = tx - ox, sy = ty - oy;
-      if (sx < F.cx0 || sx >= F.cx1 || sy < F.cy0 || sy >= F.cy1) continue;
-      const int ti = ((sy - F.cy0) / F.tile) * F.ntx + (sx - F.cx0) / F.tile;
+  // sources s with target - s in [olo, ohi]
+  const int sx0 = max(F.cx0, tx - F.ohi_x), sx1 = min(F.cx1 - 1, tx - F.olo_x);
+  const int sy0 = max(F.cy0, ty - F.ohi_y), sy1 = min(F.cy1 - 1, ty - F.olo_y);
+  if (sx0 > sx1 || sy0 > sy1) return;
+  const int tc0 = (sx0 - F.cx0) / F.tile, tc1 = (sx1 - F.cx0) / F.tile;
+  const int tr0 = (sy0 - F.cy0) / F.tile, tr1 = (sy1 - F.cy0) / F.tile;
+  float* px = film + 5 * ((size_t)(ty - F.cy0) * F.w + (tx - F.cx0));
+  float aR = px[0], aG = px[1], aB = px[2], aA = px[3], aW = px[4];
+  bool any = false;
+  for (int tr = tr0; tr <= tr1; ++tr)
+    for (int tc = tc0; tc <= tc1; ++tc) {
+      const int ti = tr * F.ntx + tc;
       if (ti % F.nshards != F.shard) continue;
       const int rank = ti / F.nshards;
       if (rank < F.tb0 || rank >= F.tb1) continue;
-      const int key = (ti << 12) | (((sy - F.cy0) % F.tile) << 6) | ((sx - F.cx0) % F.tile);
-      int k = nk++;
-      while (k > 0 && keys[k - 1] > key) {
-        keys[k] = keys[k - 1];
-        --k;
-      }
-      keys[k] = key;
+      const int X = F.cx0 + tc * F.tile, Y = F.cy0 + tr * F.tile;
+      const int W = min(F.tile, F.cx1 - X);
+      const int ya = max(sy0, Y), yb = min(sy1, Y + F.tile - 1);
+      const int xa = max(sx0, X), xb = min(sx1, X + F.tile - 1);
+      const long long tb = tile_base[rank - F.tb0];
+      for (int sy = ya; sy <= yb; ++sy)
+        for (int sx = xa; sx <= xb; ++sx) {
+          const long long cbase = tb + (long long)((sy - Y) * W + (sx - X)) * F.spp;
+          const int ox = tx - sx, oy = ty - sy;
+          for (int s = 0; s < F.spp; ++s) {
+            const float2 dd = sxy[cbase + s];
+            const double dx = dd.x, dy = dd.y;
+            int dx0 = round2int(dx - F.filterw), dx1 = round2int(dx + F.filterw - 1.0);
+            int dy0 = round2int(dy - F.filterw), dy1 = round2int(dy + F.filterw - 1.0);
+            // film-edge clamps (cx0 - x etc.) hold by construction: tx, ty lie inside the film
+            if (ox < dx0 || ox > dx1 || oy < dy0 || oy > dy1) continue;
+            const int xi = floor2int(fabs(((double)ox - (dx - 0.5)) * F.tableScale));
+            const int yi = floor2int(fabs(((double)oy - (dy - 0.5)) * F.tableScale));
+            const float wt = F.table[yi * 16 + xi];
+            const float4 col = samples[cbase + s];
+            aR = aR + wt * col.x;
+            aG = aG + wt * col.y;
+            aB = aB + wt * col.z;
+            aA = aA + wt * col.w;
+            aW = aW + wt;
+            any = true;
+          }
+        }
     }
-  if (nk == 0) return;
-  float* px = film + 5 * ((size_t)(ty - F.cy0) * F.w + (tx - F.cx0));
-  float aR = px[0], aG = px[1], aB = px[2], aA = px[3], aW = px[4];
-  for (int q = 0; q < nk; ++q) {
-    const int ti = keys[q] >> 12, ly = (keys[q] >> 6) & 63, lx = keys[q] & 63;
-    const int tcol = ti % F.ntx, trow = ti / F.ntx;
-    const int X = F.cx0 + tcol * F.tile, Y = F.cy0 + trow * F.tile;
-    const int W = min(F.tile, F.cx1 - X);
-    const int sx = X + lx, sy = Y + ly;
-    const unsigned so = fnv32a((unsigned)sy * fnv32a((unsigned)sx));
-    const long long cbase = tile_base[ti / F.nshards - F.tb0] + (long long)(ly * W + lx) * F.spp;
-    for (int s = 0; s < F.spp; ++s) {
-      float dx = 0.5f, dy = 0.5f;
-      if (F.spp > 1) {
-        dx = (0.5f + (float)s) * F.d1;
-        dy = ri_lp((unsigned)s + so, 0u);
-      }
-      int dx0 = round2int((double)dx - F.filterw), dx1 = round2int((double)dx + F.filterw - 1.0);
-      int dy0 = round2int((double)dy - F.filterw), dy1 = round2int((double)dy + F.filterw - 1.0);
-      dx0 = max(F.cx0 - sx, dx0);
-      dx1 = min(F.cx1 - sx - 1, dx1);
-      dy0 = max(F.cy0 - sy, dy0);
-      dy1 = min(F.cy1 - sy - 1, dy1);
-      const int ox = tx - sx, oy = ty - sy;
-      if (ox < dx0 || ox > dx1 || oy < dy0 || oy > dy1) continue;
-      const int xi = floor2int(fabs(((double)ox - ((double)dx - 0.5)) * F.tableScale));
-      const int yi = floor2int(fabs(((double)oy - ((double)dy - 0.5)) * F.tableScale));
-      const float wt = F.table[yi * 16 + xi];
-      const float4 col = samples[cbase + s];
-      aR = aR + wt * col.x;
-      aG = aG + wt * col.y;
-      aB = aB + wt * col.z;
-      aA = aA + wt * col.w;
-      aW = aW + wt;
-    }
-  }
+  if (!any) return;
   px[0] = aR;
   px[1] = aG;
   px[2] = aB;
@@ -1097,6 +1110,7 @@ struct yk_device {
   int ntris = 0, max_depth = 0, nlights = 0, sum_light_samples = 0;
   // traversal work counter + node/tri counters
   DBuf<unsigned long long> counters;
+  DBuf<uint2> ovf;  // traversal stack overflow (entries deeper than the LDS ring)
   // batch buffers (grown on demand, kept across renders)
   DBuf<unsigned> soffs, qcount, s_idx;
   DBuf<float> col, alpha, thr, pathcol, scol_next, wlast, emit_b, sl_contrib;
@@ -1106,6 +1120,7 @@ struct yk_device {
   DBuf<yk_hit> p_hits, qh0, qh1;
   DBuf<uint8_t> sl_flags, s_occl;
   DBuf<float4> samples;
+  DBuf<float2> sxy;
   ~yk_device() {
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -1278,17 +1293,21 @@ void launch_trace(yk_device* d, const yk_ray* rays, const unsigned* idx, long lo
   if (n <= 0) return;
   unsigned long long* ctr = d->counters.p;
   HIPCHK(hipMemsetAsync(ctr, 0, 4 * sizeof(unsigned long long), d->stream));
-  const int D = stack_depth(d);
-  const size_t lds = (size_t)3 * D * 64 * sizeof(uint32_t);
-  // persistent grid: enough waves to fill every CU at the LDS-limited occupancy
-  int per_cu = (int)std::min<size_t>(32, (160 * 1024) / std::max<size_t>(lds, 1));
-  if (per_cu < 1) per_cu = 1;
-  long long grid = (long long)d->cus * per_cu;
+  // persistent grid: as many waves as the chip keeps resident (VGPR/LDS bound)
+  static int per_cu[2] = {0, 0};
+  if (!per_cu[CLOSEST]) {
+    int blocks = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace<CLOSEST>, 64, 0));
+    per_cu[CLOSEST] = std::max(1, blocks);
+  }
+  long long grid = (long long)d->cus * per_cu[CLOSEST];
   grid = std::min<long long>(grid, (n + 63) / 64);
   if (grid < 1) grid = 1;
+  const int D = stack_depth(d);
+  if (D > kStackLds) d->ovf.ensure((size_t)(D - kStackLds) * (size_t)grid * 64);
   HIPCHK(hipEventRecord(d->ev0, d->stream));
-  hipLaunchKernelGGL(k_trace<CLOSEST>, dim3((unsigned)grid), dim3(64), lds, d->stream, d->S, rays, idx, n, hits, occ,
-                     ctr, ctr + 1, D);
+  hipLaunchKernelGGL(k_trace<CLOSEST>, dim3((unsigned)grid), dim3(64), 0, d->stream, d->S, rays, idx, n, hits, occ,
+                     ctr, ctr + 1, d->ovf.p);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(d->ev1, d->stream));
   unsigned long long h[4];
@@ -1503,9 +1522,7 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   HIPCHK(hipSetDevice(d->ordinal));
   auto t0 = std::chrono::steady_clock::now();
   FilmConst F = make_film(p);
-  if ((F.ohi_x - F.olo_x + 1) * (F.ohi_y - F.olo_y + 1) > 64)
-    return set_error(YK_ERR_UNSUPPORTED, "filter window too large");
-  if (F.tile > 64) return set_error(YK_ERR_UNSUPPORTED, "tile_size > 64");
+  if (F.tile > 4096) return set_error(YK_ERR_UNSUPPORTED, "tile_size > 4096");
   F.shard = shard;
   F.nshards = nshards;
   const int spp = F.spp;
@@ -1553,6 +1570,7 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   d->sl_contrib.ensure(3 * maxc * K);
   d->sl_flags.ensure(maxc * K);
   d->samples.ensure(maxc);
+  d->sxy.ensure(maxc);
   d->tiles.ensure(tiles_per_batch);
   d->tile_base.ensure(tiles_per_batch + 1);
   Batch B{};
@@ -1581,6 +1599,7 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   B.sl_contrib = d->sl_contrib.p;
   B.sl_flags = d->sl_flags.p;
   B.samples = d->samples.p;
+  B.sxy = d->sxy.p;
   B.K = K;
   yk_stats local{};
   yk_stats* S = st ? st : &local;
@@ -1661,7 +1680,7 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
     const int gw = gx1 - gx0, gh = gy1 - gy0;
     if (gw > 0 && gh > 0) {
       hipLaunchKernelGGL(k_film_gather, dim3(grid_for((long long)gw * gh)), dim3(256), 0, d->stream, Fb, B.samples,
-                         d->tile_base.p, d_film, gx0, gy0, gw, gh);
+                         B.sxy, d->tile_base.p, d_film, gx0, gy0, gw, gh);
       HIPCHK(hipGetLastError());
     }
     S->camera_samples += (uint64_t)nc;
