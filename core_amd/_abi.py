@@ -12,6 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libyk.so")
 
 YK_OK = 0
+YK_ERR_ARG, YK_ERR_STATE, YK_ERR_HIP, YK_ERR_UNSUPPORTED, YK_ERR_ALLOC, YK_ERR_INTERNAL = 1, 2, 3, 4, 5, 6
 YK_MAT_SHINYDIFFUSE, YK_MAT_LIGHT = 0, 1
 YK_LIGHT_AREA = 0
 YK_INTEGRATOR_DIRECT, YK_INTEGRATOR_PATH = 0, 1

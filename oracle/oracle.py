@@ -29,6 +29,7 @@ def lib():
         L.orc_intersect.argtypes = [vp, C.c_int64, vp, vp]
         L.orc_shadow.argtypes = [vp, C.c_int64, vp, vp]
         L.orc_render.argtypes = [vp, vp, vp, vp]
+        L.orc_render_shard.argtypes = [vp, C.c_int32, C.c_int32, vp, vp]
         L.orc_camera_rays.argtypes = [C.c_int32] * 5 + [vp]
         L.orc_scrhalton.restype = C.c_double
         L.orc_scrhalton.argtypes = [C.c_int, C.c_uint]
@@ -89,6 +90,16 @@ class Oracle:
         return rgba, sums, dict(closest=int(counts[0]), shadow=int(counts[1]), closest_nodes=int(counts[2]),
                                 closest_tris=int(counts[3]), shadow_nodes=int(counts[4]),
                                 shadow_tris=int(counts[5]))
+
+    def render_shard(self, params, shard, nshards):
+        """Film sums (h, w, 5) of the tiles t % nshards == shard, and ray counts."""
+        self._activate()
+        sums = np.zeros((params.height, params.width, 5), np.float32)
+        counts = np.zeros(6, np.uint64)
+        rc = lib().orc_render_shard(C.addressof(params), shard, nshards, sums.ctypes.data, counts.ctypes.data)
+        if rc:
+            raise RuntimeError(f"orc_render_shard failed ({rc})")
+        return sums, dict(closest=int(counts[0]), shadow=int(counts[1]))
 
     def intersect(self, rays):
         """rays: (n,8) float32 [from, dir, tmin, tmax] -> (prim int32, t, b1, b2), counters"""

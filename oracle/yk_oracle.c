@@ -1023,7 +1023,22 @@ int orc_camera_rays(int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t spp, y
  * rgba (w*h*4, imageFilm_t::flush + clampRGB0); optional film sums (w*h*5);
  * counts[0..5] = closest, shadow, closest nodes, closest tris, shadow nodes,
  * shadow tris. */
+/* tiles t (row-major tile index) with t % nshards == shard only; film sums
+ * of the other tiles' samples stay 0 (the multi-GPU tile split) */
+static int render_tiles(const yk_render_params* P, int shard, int nshards, float* rgba_out, float* film_sums,
+                        uint64_t* counts);
+
 int orc_render(const yk_render_params* P, float* rgba_out, float* film_sums, uint64_t* counts) {
+  return render_tiles(P, 0, 1, rgba_out, film_sums, counts);
+}
+
+int orc_render_shard(const yk_render_params* P, int32_t shard, int32_t nshards, float* film_sums, uint64_t* counts) {
+  if (nshards < 1 || shard < 0 || shard >= nshards) return 2;
+  return render_tiles(P, shard, nshards, NULL, film_sums, counts);
+}
+
+static int render_tiles(const yk_render_params* P, int shard, int nshards, float* rgba_out, float* film_sums,
+                        uint64_t* counts) {
   if (P->aa_passes != 1) return 4;
   film_t F;
   film_init(&F, P);
@@ -1034,6 +1049,7 @@ int orc_render(const yk_render_params* P, float* rgba_out, float* film_sums, uin
   int nx = (F.w + ts - 1) / ts, ny = (F.h + ts - 1) / ts;
   for (int ty = 0; ty < ny; ++ty)
     for (int tx = 0; tx < nx; ++tx) {
+      if ((ty * nx + tx) % nshards != shard) continue;
       int X = F.cx0 + tx * ts, Y = F.cy0 + ty * ts;
       int W = (F.cx0 + F.w - X) < ts ? (F.cx0 + F.w - X) : ts;
       int H = (F.cy0 + F.h - Y) < ts ? (F.cy0 + F.h - Y) : ts;
