@@ -38,6 +38,20 @@ class yk_camera(C.Structure):
                 ("far_clip", C.c_float)]
 
 
+class yk_material_state(C.Structure):
+    _fields_ = [("type", C.c_int32), ("bsdf_flags", C.c_uint32), ("color", f3),
+                ("diffuse_strength", C.c_float), ("emit_color", f3), ("double_sided", C.c_int32)]
+
+
+class yk_area_light_state(C.Structure):
+    _fields_ = [("corner", f3), ("to_x", f3), ("to_y", f3), ("color", f3), ("samples", C.c_int32)]
+
+
+class yk_camera_state(C.Structure):
+    _fields_ = [("position", f3), ("vright", f3), ("vup", f3), ("vto", f3), ("cam_z", f3),
+                ("near_p", f3), ("far_p", f3), ("resx", C.c_int32), ("resy", C.c_int32)]
+
+
 class yk_render_params(C.Structure):
     _fields_ = [("integrator", C.c_int32), ("raydepth", C.c_int32), ("path_samples", C.c_int32),
                 ("bounces", C.c_int32), ("caustic_type", C.c_int32), ("width", C.c_int32),
@@ -98,6 +112,12 @@ SIGNATURES = {
     "yk_scene_get_material": (C.c_int, [P, i32, C.POINTER(yk_material)]),
     "yk_scene_get_light": (C.c_int, [P, i32, C.POINTER(yk_light)]),
     "yk_scene_get_camera": (C.c_int, [P, C.POINTER(yk_camera)]),
+    "yk_scene_add_material_state": (C.c_int, [P, C.POINTER(yk_material_state), i32p]),
+    "yk_scene_add_area_light_state": (C.c_int, [P, C.POINTER(yk_area_light_state)]),
+    "yk_scene_set_camera_state": (C.c_int, [P, C.POINTER(yk_camera_state)]),
+    "yk_scene_get_material_state": (C.c_int, [P, i32, C.POINTER(yk_material_state)]),
+    "yk_scene_get_area_light_state": (C.c_int, [P, i32, C.POINTER(yk_area_light_state)]),
+    "yk_scene_get_camera_state": (C.c_int, [P, C.POINTER(yk_camera_state)]),
     "yk_scene_generate": (C.c_int, [P, C.c_char_p, i32, i32, i32, i32, C.POINTER(yk_render_params)]),
     "yk_render_params_default": (None, [C.POINTER(yk_render_params)]),
     "yk_device_open": (C.c_int, [i32, C.POINTER(P)]),

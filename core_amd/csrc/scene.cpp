@@ -9,6 +9,126 @@
 
 namespace yk {
 
+// ---- reference constructor arithmetic --------------------------------------
+namespace {
+struct hv3 {
+  float x, y, z;
+};
+hv3 H(const float* p) { return {p[0], p[1], p[2]}; }
+hv3 hsub(hv3 a, hv3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+hv3 hadd(hv3 a, hv3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+hv3 hmul(float f, hv3 b) { return {f * b.x, f * b.y, f * b.z}; }
+hv3 hcross(hv3 a, hv3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+hv3 hnorm(hv3 a) {  // vector3d_t::normalize, vector3d.h:249-260
+  float len = a.x * a.x + a.y * a.y + a.z * a.z;
+  if (len != 0.f) {
+    len = 1.0f / std::sqrt(len);
+    a.x *= len;
+    a.y *= len;
+    a.z *= len;
+  }
+  return a;
+}
+void put(float* d, hv3 v) {
+  d[0] = v.x;
+  d[1] = v.y;
+  d[2] = v.z;
+}
+constexpr unsigned kDiffuse = 0x4u, kReflect = 0x10u, kEmit = 0x80u;  // material.h:49-66
+}  // namespace
+
+yk_material_state material_state(const yk_material& m) {
+  yk_material_state o{};
+  o.type = m.type;
+  if (m.type == YK_MAT_LIGHT) {  // lightMat_t(color * power, double_sided), simple.cc:80-90
+    o.bsdf_flags = kEmit;
+    for (int k = 0; k < 3; ++k) o.color[k] = m.color[k] * m.power;
+    o.double_sided = m.double_sided;
+  } else {  // shinyDiffuseMat_t ctor, shinydiffuse.cc:9-60
+    if (m.emit > 0.f) o.bsdf_flags |= kEmit;
+    if (m.diffuse_reflect > 0.00001f) o.bsdf_flags |= kDiffuse | kReflect;
+    for (int k = 0; k < 3; ++k) {
+      o.color[k] = m.color[k];
+      o.emit_color[k] = m.emit * m.color[k];
+    }
+    o.diffuse_strength = m.diffuse_reflect;
+  }
+  return o;
+}
+
+yk_area_light_state light_state(const yk_light& l) {  // areaLight_t::factory + ctor, arealight.cc:30-49,171-192
+  yk_area_light_state o{};
+  const hv3 c = H(l.corner);
+  put(o.corner, c);
+  put(o.to_x, hsub(H(l.point1), c));
+  put(o.to_y, hsub(H(l.point2), c));
+  const float pi = (float)3.14159265358979323846;
+  for (int k = 0; k < 3; ++k) o.color[k] = pi * (l.color[k] * l.power);
+  o.samples = l.samples;
+  return o;
+}
+
+yk_camera_state camera_state(const yk_camera& c) {  // camera_t ctor + setAxis
+  yk_camera_state o{};
+  const hv3 pos = H(c.from), look = H(c.to), up = H(c.up);
+  const float aspect = c.aspect_ratio * (float)c.resy / (float)c.resx;  // camera.h:44
+  hv3 camY = hsub(up, pos), camZ = hsub(look, pos);
+  hv3 camX = hcross(camZ, camY);
+  camY = hcross(camZ, camX);
+  camX = hnorm(camX);
+  camY = hnorm(camY);
+  camZ = hnorm(camZ);
+  put(o.position, pos);
+  put(o.cam_z, camZ);
+  put(o.near_p, hadd(pos, hmul(c.near_clip, camZ)));
+  put(o.far_p, hadd(pos, hmul(c.far_clip, camZ)));
+  const hv3 vright = camX, vup = hmul(aspect, camY);
+  put(o.vto, hsub(hmul(c.focal, camZ), hmul(0.5f, hadd(vup, vright))));
+  const float ry = 1.0f / (float)c.resy, rx = 1.0f / (float)c.resx;  // compiled form of "/= res"
+  put(o.vup, {vup.x * ry, vup.y * ry, vup.z * ry});
+  put(o.vright, {vright.x * rx, vright.y * rx, vright.z * rx});
+  o.resx = c.resx;
+  o.resy = c.resy;
+  return o;
+}
+
+int Scene::add_material(const yk_material& m) {
+  materials.push_back(m);
+  material_has_params.push_back(true);
+  material_states.push_back(material_state(m));
+  built = false;
+  return (int)material_states.size() - 1;
+}
+int Scene::add_material_state(const yk_material_state& m) {
+  materials.push_back(yk_material{});
+  material_has_params.push_back(false);
+  material_states.push_back(m);
+  built = false;
+  return (int)material_states.size() - 1;
+}
+void Scene::add_light(const yk_light& l) {
+  lights.push_back(l);
+  light_has_params.push_back(true);
+  light_states.push_back(light_state(l));
+}
+void Scene::add_light_state(const yk_area_light_state& l) {
+  lights.push_back(yk_light{});
+  light_has_params.push_back(false);
+  light_states.push_back(l);
+}
+void Scene::set_camera(const yk_camera& c) {
+  camera = c;
+  camera_has_params = true;
+  camera_state = yk::camera_state(c);
+  has_camera = true;
+}
+void Scene::set_camera_state(const yk_camera_state& c) {
+  camera = yk_camera{};
+  camera_has_params = false;
+  camera_state = c;
+  has_camera = true;
+}
+
 void rec_normal(const float* t, float* n) {
   // triangle_t::recNormal, triangle_inline.h:100-107
   float e1x = t[3] - t[0], e1y = t[4] - t[1], e1z = t[5] - t[2];
@@ -100,8 +220,7 @@ int add_mat(Scene& s, int type, float r, float g, float b, float power) {
   m.emit = 0.f;
   m.power = power;
   m.double_sided = 0;
-  s.materials.push_back(m);
-  return (int)s.materials.size() - 1;
+  return s.add_material(m);
 }
 
 // value as the XML loader sees a "%.6f" formatted coordinate: strtod of the
@@ -147,7 +266,7 @@ void gen_cornell(Scene& s, int resx, int resy) {
   }
   l.power = 10.f;
   l.samples = 4;
-  s.lights.push_back(l);
+  s.add_light(l);
   yk_camera cam{};
   const float from[3] = {0, 1, -3.6f}, to[3] = {0, 1, 0}, up[3] = {0, 2, -3.6f};
   for (int k = 0; k < 3; ++k) {
@@ -161,8 +280,7 @@ void gen_cornell(Scene& s, int resx, int resy) {
   cam.aspect_ratio = 1.f;
   cam.near_clip = 0.f;
   cam.far_clip = -1.f;
-  s.camera = cam;
-  s.has_camera = true;
+  s.set_camera(cam);
 }
 
 // 1M-triangle probe of BASELINE.md: displaced UV sphere (NU x NV grid,
@@ -217,7 +335,7 @@ void gen_bumpy(Scene& s, int nu, int nv, int resx, int resy) {
   }
   l.power = 8.f;
   l.samples = 1;
-  s.lights.push_back(l);
+  s.add_light(l);
   yk_camera cam{};
   const float from[3] = {0, 1.5f, -4.f}, to[3] = {0, 1.2f, 0}, up[3] = {0, 2.5f, -4.f};
   for (int k = 0; k < 3; ++k) {
@@ -231,8 +349,7 @@ void gen_bumpy(Scene& s, int nu, int nv, int resx, int resy) {
   cam.aspect_ratio = 1.f;
   cam.near_clip = 0.f;
   cam.far_clip = -1.f;
-  s.camera = cam;
-  s.has_camera = true;
+  s.set_camera(cam);
 }
 
 }  // namespace yk

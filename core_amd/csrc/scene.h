@@ -21,10 +21,25 @@ struct Mesh {
 
 struct Scene {
   std::vector<Mesh> meshes;          // object-id order
+  // parameter-level descriptions (when the caller gave them) ...
   std::vector<yk_material> materials;
+  std::vector<bool> material_has_params;
   std::vector<yk_light> lights;
+  std::vector<bool> light_has_params;
   yk_camera camera{};
+  bool camera_has_params = false;
+  // ... and the reference object state the kernels consume
+  std::vector<yk_material_state> material_states;
+  std::vector<yk_area_light_state> light_states;
+  yk_camera_state camera_state{};
   bool has_camera = false;
+
+  int add_material(const yk_material& m);
+  int add_material_state(const yk_material_state& m);
+  void add_light(const yk_light& l);
+  void add_light_state(const yk_area_light_state& l);
+  void set_camera(const yk_camera& c);
+  void set_camera_state(const yk_camera_state& c);
 
   // built by finalize(): flattened prim arrays + kd-tree
   std::vector<float> tri_verts;      // 9 floats per prim
@@ -40,6 +55,13 @@ struct Scene {
 // Procedural fixtures (deterministic, no RNG): the probe scenes of BASELINE.md.
 void gen_cornell(Scene& s, int resx, int resy);
 void gen_bumpy(Scene& s, int nu, int nv, int resx, int resy);
+
+// Reference constructor arithmetic (IEEE, no contraction):
+// shinyDiffuseMat_t / lightMat_t factories, areaLight_t ctor (arealight.cc:30-49),
+// camera_t ctor + perspectiveCam_t::setAxis (camera.h:41-60, perspectiveCamera.cc:28-71).
+yk_material_state material_state(const yk_material& m);
+yk_area_light_state light_state(const yk_light& l);
+yk_camera_state camera_state(const yk_camera& c);
 
 // recNormal: ((b-a)^(c-a)).normalize() with the reference's float op order
 // (triangle_inline.h:100-107, vector3d.h:176-260).

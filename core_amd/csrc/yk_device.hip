@@ -1139,99 +1139,61 @@ namespace {
   catch (const std::exception& e) { return set_error(YK_ERR_INTERNAL, e.what()); }               \
   catch (...) { return set_error(YK_ERR_INTERNAL, "unknown C++ exception"); }
 
-// host float helpers with the reference's operation order (compiled with
-// -ffp-contract=off, IEEE)
-struct hv3 {
-  float x, y, z;
-};
-hv3 hsub(hv3 a, hv3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
-hv3 hadd(hv3 a, hv3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
-hv3 hmul(float f, hv3 b) { return {f * b.x, f * b.y, f * b.z}; }
-hv3 hcross(hv3 a, hv3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
-hv3 hnorm(hv3 a) {
-  float len = a.x * a.x + a.y * a.y + a.z * a.z;
-  if (len != 0.f) {
-    len = 1.0f / std::sqrt(len);
-    a.x *= len;
-    a.y *= len;
-    a.z *= len;
-  }
-  return a;
-}
-void put3(float* d, hv3 v) {
-  d[0] = v.x;
-  d[1] = v.y;
-  d[2] = v.z;
-}
-
-DCam make_cam(const yk_camera& c) {
+// Device records from the reference object state (yk_material_state etc.;
+// the parameter-level conversion is host arithmetic in scene.cpp).
+DCam make_cam(const yk_camera_state& c) {
   DCam C{};
-  hv3 pos{c.from[0], c.from[1], c.from[2]}, look{c.to[0], c.to[1], c.to[2]}, up{c.up[0], c.up[1], c.up[2]};
-  const float aspect = c.aspect_ratio * (float)c.resy / (float)c.resx;  // camera.h:44
-  hv3 camY = hsub(up, pos), camZ = hsub(look, pos);
-  hv3 camX = hcross(camZ, camY);
-  camY = hcross(camZ, camX);
-  camX = hnorm(camX);
-  camY = hnorm(camY);
-  camZ = hnorm(camZ);
-  put3(C.pos, pos);
-  put3(C.camZ, camZ);
-  put3(C.near_p, hadd(pos, hmul(c.near_clip, camZ)));
-  put3(C.far_p, hadd(pos, hmul(c.far_clip, camZ)));
-  hv3 vright = camX, vup = hmul(aspect, camY);
-  hv3 vto = hsub(hmul(c.focal, camZ), hmul(0.5f, hadd(vup, vright)));
-  const float ry = 1.0f / (float)c.resy, rx = 1.0f / (float)c.resx;  // compiled form of "/= res"
-  put3(C.vup, {vup.x * ry, vup.y * ry, vup.z * ry});
-  put3(C.vright, {vright.x * rx, vright.y * rx, vright.z * rx});
-  put3(C.vto, vto);
+  std::memcpy(C.pos, c.position, sizeof C.pos);
+  std::memcpy(C.vright, c.vright, sizeof C.vright);
+  std::memcpy(C.vup, c.vup, sizeof C.vup);
+  std::memcpy(C.vto, c.vto, sizeof C.vto);
+  std::memcpy(C.camZ, c.cam_z, sizeof C.camZ);
+  std::memcpy(C.near_p, c.near_p, sizeof C.near_p);
+  std::memcpy(C.far_p, c.far_p, sizeof C.far_p);
   return C;
 }
 
-DLight make_light(const yk_light& L) {
+// areaLight_t ctor tail (arealight.cc:36-49): fnormal = toY ^ toX, normLen,
+// corners c2..c4 -- IEEE host arithmetic, -ffp-contract=off
+DLight make_light(const yk_area_light_state& L) {
   DLight D{};
-  hv3 corner{L.corner[0], L.corner[1], L.corner[2]}, p1{L.point1[0], L.point1[1], L.point1[2]},
-      p2{L.point2[0], L.point2[1], L.point2[2]};
-  hv3 toX = hsub(p1, corner), toY = hsub(p2, corner);
-  hv3 f = hcross(toY, toX);
-  float vl = f.x * f.x + f.y * f.y + f.z * f.z;  // normLen, vector3d.h:61-70
+  const float* c = L.corner;
+  const float* x = L.to_x;
+  const float* y = L.to_y;
+  float f[3] = {y[1] * x[2] - y[2] * x[1], y[2] * x[0] - y[0] * x[2], y[0] * x[1] - y[1] * x[0]};
+  float vl = f[0] * f[0] + f[1] * f[1] + f[2] * f[2];  // normLen, vector3d.h:61-70
   if (vl != 0.f) {
     vl = std::sqrt(vl);
     const float d = 1.0f / vl;
-    f.x *= d;
-    f.y *= d;
-    f.z *= d;
+    f[0] *= d;
+    f[1] *= d;
+    f[2] *= d;
   }
-  put3(D.corner, corner);
-  put3(D.toX, toX);
-  put3(D.toY, toY);
-  put3(D.fnormal, f);
-  put3(D.c2, hadd(corner, toX));
-  put3(D.c3, hadd(corner, hadd(toX, toY)));
-  put3(D.c4, hadd(corner, toY));
-  const float pi = (float)3.14159265358979323846;
-  for (int k = 0; k < 3; ++k) D.color[k] = pi * (L.color[k] * L.power);
+  for (int k = 0; k < 3; ++k) {
+    D.corner[k] = c[k];
+    D.toX[k] = x[k];
+    D.toY[k] = y[k];
+    D.fnormal[k] = f[k];
+    D.c2[k] = c[k] + x[k];
+    D.c3[k] = c[k] + (x[k] + y[k]);
+    D.c4[k] = c[k] + y[k];
+    D.color[k] = L.color[k];
+  }
   D.area = vl;
   D.samples = L.samples;
   return D;
 }
 
-DMat make_mat(const yk_material& m) {
+DMat make_mat(const yk_material_state& m) {
   DMat M{};
   M.type = m.type;
-  if (m.type == YK_MAT_LIGHT) {
-    M.flags = BSDF_EMIT;
-    for (int k = 0; k < 3; ++k) M.col[k] = m.color[k] * m.power;
-    M.double_sided = m.double_sided;
-  } else {
-    M.flags = 0;
-    if (m.emit > 0.f) M.flags |= BSDF_EMIT;
-    if (m.diffuse_reflect > 0.00001f) M.flags |= BSDF_DIFFUSE | BSDF_REFLECT;
-    for (int k = 0; k < 3; ++k) {
-      M.col[k] = m.color[k];
-      M.emit_col[k] = m.emit * m.color[k];
-    }
-    M.diffuse = m.diffuse_reflect;
+  M.flags = m.bsdf_flags;
+  for (int k = 0; k < 3; ++k) {
+    M.col[k] = m.color[k];
+    M.emit_col[k] = m.emit_color[k];
   }
+  M.diffuse = m.diffuse_strength;
+  M.double_sided = m.double_sided;
   return M;
 }
 
@@ -1384,8 +1346,8 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   const Scene& S = s->s;
   if (!S.built) return set_error(YK_ERR_STATE, "yk_device_upload: scene not built (call yk_scene_build)");
   if (!S.has_camera) return set_error(YK_ERR_STATE, "yk_device_upload: scene has no camera");
-  if ((int)S.materials.size() > kMaxMats) return set_error(YK_ERR_UNSUPPORTED, "too many materials");
-  if ((int)S.lights.size() > kMaxLights) return set_error(YK_ERR_UNSUPPORTED, "too many lights");
+  if ((int)S.material_states.size() > kMaxMats) return set_error(YK_ERR_UNSUPPORTED, "too many materials");
+  if ((int)S.light_states.size() > kMaxLights) return set_error(YK_ERR_UNSUPPORTED, "too many lights");
   YK_GUARD_BEGIN
   HIPCHK(hipSetDevice(d->ordinal));
   const int nt = (int)S.tri_material.size();
@@ -1412,11 +1374,11 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
     HIPCHK(hipMemcpy(d->leaf.p, S.tree.leaf_prims.data(), S.tree.leaf_prims.size() * sizeof(uint32_t),
                      hipMemcpyHostToDevice));
   std::vector<DMat> mats;
-  for (const auto& m : S.materials) mats.push_back(make_mat(m));
+  for (const auto& m : S.material_states) mats.push_back(make_mat(m));
   if (!mats.empty()) HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_mats), mats.data(), mats.size() * sizeof(DMat)));
   std::vector<DLight> lights;
   int sum_samples = 0;
-  for (const auto& l : S.lights) {
+  for (const auto& l : S.light_states) {
     if (l.samples < 1) return set_error(YK_ERR_ARG, "light samples must be >= 1");
     lights.push_back(make_light(l));
     sum_samples += l.samples;
@@ -1425,16 +1387,16 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   d->sum_light_samples = sum_samples;
   if (!lights.empty())
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_lights), lights.data(), lights.size() * sizeof(DLight)));
-  const DCam cam = make_cam(S.camera);
+  const DCam cam = make_cam(S.camera_state);
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_cam), &cam, sizeof cam));
   d->S.tris = d->tris.p;
   d->S.nodes = d->nodes.p;
   d->S.leaf = d->leaf.p;
   d->S.ng = d->ng.p;
   std::memcpy(d->S.bound, S.tree.bound, sizeof d->S.bound);
-  d->S.nlights = (int)S.lights.size();
+  d->S.nlights = (int)S.light_states.size();
   d->S.nnodes = (unsigned)nn;
-  d->nlights = (int)S.lights.size();
+  d->nlights = (int)S.light_states.size();
   d->ntris = nt;
   d->max_depth = S.tree.max_depth;
   d->uploaded = true;

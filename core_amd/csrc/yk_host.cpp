@@ -53,9 +53,19 @@ int yk_scene_add_material(yk_scene* s, const yk_material* m, int32_t* id_out) {
   if (m->type != YK_MAT_SHINYDIFFUSE && m->type != YK_MAT_LIGHT)
     return set_error(YK_ERR_UNSUPPORTED, "material type not supported by the GPU path");
   YK_GUARD_BEGIN
-  s->s.materials.push_back(*m);
-  s->s.built = false;
-  if (id_out) *id_out = (int32_t)s->s.materials.size() - 1;
+  const int id = s->s.add_material(*m);
+  if (id_out) *id_out = id;
+  return YK_OK;
+  YK_GUARD_END
+}
+
+int yk_scene_add_material_state(yk_scene* s, const yk_material_state* m, int32_t* id_out) {
+  if (!s || !m) return set_error(YK_ERR_ARG, "yk_scene_add_material_state: NULL argument");
+  if (m->type != YK_MAT_SHINYDIFFUSE && m->type != YK_MAT_LIGHT)
+    return set_error(YK_ERR_UNSUPPORTED, "material type not supported by the GPU path");
+  YK_GUARD_BEGIN
+  const int id = s->s.add_material_state(*m);
+  if (id_out) *id_out = id;
   return YK_OK;
   YK_GUARD_END
 }
@@ -64,7 +74,7 @@ int yk_scene_add_mesh(yk_scene* s, const float* points, int32_t npoints, const i
                       int32_t nfaces, int32_t material, int32_t* obj_id_out) {
   if (!s || (npoints > 0 && !points) || (nfaces > 0 && !faces) || npoints < 0 || nfaces < 0)
     return set_error(YK_ERR_ARG, "yk_scene_add_mesh: bad arguments");
-  if (material < 0 || material >= (int32_t)s->s.materials.size())
+  if (material < 0 || material >= (int32_t)s->s.material_states.size())
     return set_error(YK_ERR_ARG, "yk_scene_add_mesh: unknown material id");
   for (int64_t i = 0; i < 3 * (int64_t)nfaces; ++i)
     if (faces[i] < 0 || faces[i] >= npoints)
@@ -86,7 +96,16 @@ int yk_scene_add_light(yk_scene* s, const yk_light* l) {
   if (l->type != YK_LIGHT_AREA) return set_error(YK_ERR_UNSUPPORTED, "light type not supported");
   if (l->samples < 1) return set_error(YK_ERR_ARG, "area light needs samples >= 1");
   YK_GUARD_BEGIN
-  s->s.lights.push_back(*l);
+  s->s.add_light(*l);
+  return YK_OK;
+  YK_GUARD_END
+}
+
+int yk_scene_add_area_light_state(yk_scene* s, const yk_area_light_state* l) {
+  if (!s || !l) return set_error(YK_ERR_ARG, "yk_scene_add_area_light_state: NULL argument");
+  if (l->samples < 1) return set_error(YK_ERR_ARG, "area light needs samples >= 1");
+  YK_GUARD_BEGIN
+  s->s.add_light_state(*l);
   return YK_OK;
   YK_GUARD_END
 }
@@ -94,8 +113,37 @@ int yk_scene_add_light(yk_scene* s, const yk_light* l) {
 int yk_scene_set_camera(yk_scene* s, const yk_camera* c) {
   if (!s || !c) return set_error(YK_ERR_ARG, "yk_scene_set_camera: NULL argument");
   if (c->resx <= 0 || c->resy <= 0) return set_error(YK_ERR_ARG, "camera resolution must be > 0");
-  s->s.camera = *c;
-  s->s.has_camera = true;
+  YK_GUARD_BEGIN
+  s->s.set_camera(*c);
+  return YK_OK;
+  YK_GUARD_END
+}
+
+int yk_scene_set_camera_state(yk_scene* s, const yk_camera_state* c) {
+  if (!s || !c) return set_error(YK_ERR_ARG, "yk_scene_set_camera_state: NULL argument");
+  if (c->resx <= 0 || c->resy <= 0) return set_error(YK_ERR_ARG, "camera resolution must be > 0");
+  s->s.set_camera_state(*c);
+  return YK_OK;
+}
+
+int yk_scene_get_material_state(const yk_scene* s, int32_t i, yk_material_state* out) {
+  if (!s || !out || i < 0 || i >= (int32_t)s->s.material_states.size())
+    return set_error(YK_ERR_ARG, "yk_scene_get_material_state: bad arguments");
+  *out = s->s.material_states[i];
+  return YK_OK;
+}
+
+int yk_scene_get_area_light_state(const yk_scene* s, int32_t i, yk_area_light_state* out) {
+  if (!s || !out || i < 0 || i >= (int32_t)s->s.light_states.size())
+    return set_error(YK_ERR_ARG, "yk_scene_get_area_light_state: bad arguments");
+  *out = s->s.light_states[i];
+  return YK_OK;
+}
+
+int yk_scene_get_camera_state(const yk_scene* s, yk_camera_state* out) {
+  if (!s || !out) return set_error(YK_ERR_ARG, "yk_scene_get_camera_state: NULL argument");
+  if (!s->s.has_camera) return set_error(YK_ERR_STATE, "scene has no camera");
+  *out = s->s.camera_state;
   return YK_OK;
 }
 
@@ -147,6 +195,7 @@ int yk_scene_export(const yk_scene* s, float* tri_verts, int32_t* tri_material, 
 int yk_scene_get_material(const yk_scene* s, int32_t i, yk_material* out) {
   if (!s || !out || i < 0 || i >= (int32_t)s->s.materials.size())
     return set_error(YK_ERR_ARG, "yk_scene_get_material: bad index");
+  if (!s->s.material_has_params[i]) return set_error(YK_ERR_STATE, "material was given as object state only");
   *out = s->s.materials[i];
   return YK_OK;
 }
@@ -154,13 +203,15 @@ int yk_scene_get_material(const yk_scene* s, int32_t i, yk_material* out) {
 int yk_scene_get_light(const yk_scene* s, int32_t i, yk_light* out) {
   if (!s || !out || i < 0 || i >= (int32_t)s->s.lights.size())
     return set_error(YK_ERR_ARG, "yk_scene_get_light: bad index");
+  if (!s->s.light_has_params[i]) return set_error(YK_ERR_STATE, "light was given as object state only");
   *out = s->s.lights[i];
   return YK_OK;
 }
 
 int yk_scene_get_camera(const yk_scene* s, yk_camera* out) {
   if (!s || !out) return set_error(YK_ERR_ARG, "yk_scene_get_camera: NULL argument");
-  if (!s->s.has_camera) return set_error(YK_ERR_STATE, "scene has no camera");
+  if (!s->s.has_camera || !s->s.camera_has_params)
+    return set_error(YK_ERR_STATE, "scene has no parameter-level camera");
   *out = s->s.camera;
   return YK_OK;
 }

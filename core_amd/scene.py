@@ -63,6 +63,39 @@ class Scene:
         self.params = p
         return p
 
+    # -- reference object state (what a plugin reads from live objects) ---
+    def add_material_state(self, st):
+        mid = C.c_int32()
+        A.check(A.lib().yk_scene_add_material_state(self._p, C.byref(st), C.byref(mid)))
+        return mid.value
+
+    def add_area_light_state(self, st):
+        A.check(A.lib().yk_scene_add_area_light_state(self._p, C.byref(st)))
+
+    def set_camera_state(self, st):
+        A.check(A.lib().yk_scene_set_camera_state(self._p, C.byref(st)))
+
+    def material_states(self):
+        out = []
+        for k in range(self.info().nmaterials):
+            m = A.yk_material_state()
+            A.check(A.lib().yk_scene_get_material_state(self._p, k, C.byref(m)))
+            out.append(m)
+        return out
+
+    def light_states(self):
+        out = []
+        for k in range(self.info().nlights):
+            m = A.yk_area_light_state()
+            A.check(A.lib().yk_scene_get_area_light_state(self._p, k, C.byref(m)))
+            out.append(m)
+        return out
+
+    def camera_state(self):
+        c = A.yk_camera_state()
+        A.check(A.lib().yk_scene_get_camera_state(self._p, C.byref(c)))
+        return c
+
     def build(self):
         A.check(A.lib().yk_scene_build(self._p))
         return self.info()

@@ -155,6 +155,39 @@ int yk_scene_generate(yk_scene* s, const char* name, int32_t p0, int32_t p1, int
                       int32_t resy, yk_render_params* params_out);
 void yk_render_params_default(yk_render_params* p);
 
+/* ---- reference object state ----
+ * What the reference's constructors computed, for a plugin that reads it out
+ * of the live objects: re-deriving it from the XML
+ * parameters would not round-trip in float. The parameter-level calls above
+ * convert to these states with the reference's constructor arithmetic. */
+typedef struct yk_material_state {
+  int32_t type;             /* YK_MAT_*                                                  */
+  uint32_t bsdf_flags;      /* material_t::bsdfFlags (material.h:49-66)                 */
+  float color[3];           /* shinyDiffuseMat_t::mDiffuseColor | lightMat_t::lightCol  */
+  float diffuse_strength;   /* shinyDiffuseMat_t::mDiffuseStrength                      */
+  float emit_color[3];      /* shinyDiffuseMat_t::mEmitColor (= emit strength * color)  */
+  int32_t double_sided;     /* lightMat_t::doubleSided                                  */
+} yk_material_state;
+
+typedef struct yk_area_light_state { /* areaLight_t members (arealight.h:45-53) */
+  float corner[3], to_x[3], to_y[3];
+  float color[3];           /* includes pi * power (arealight.cc:38)                    */
+  int32_t samples;
+} yk_area_light_state;
+
+typedef struct yk_camera_state { /* perspectiveCam_t after setAxis (perspectiveCamera.cc:57-71) */
+  float position[3], vright[3], vup[3], vto[3], cam_z[3];
+  float near_p[3], far_p[3]; /* near_plane.p / far_plane.p (camera.h:54-57)            */
+  int32_t resx, resy;
+} yk_camera_state;
+
+int yk_scene_add_material_state(yk_scene* s, const yk_material_state* m, int32_t* id_out);
+int yk_scene_add_area_light_state(yk_scene* s, const yk_area_light_state* l);
+int yk_scene_set_camera_state(yk_scene* s, const yk_camera_state* c);
+int yk_scene_get_material_state(const yk_scene* s, int32_t i, yk_material_state* out);
+int yk_scene_get_area_light_state(const yk_scene* s, int32_t i, yk_area_light_state* out);
+int yk_scene_get_camera_state(const yk_scene* s, yk_camera_state* out);
+
 /* ---- device ---- */
 int yk_device_open(int32_t ordinal, yk_device** out);
 void yk_device_close(yk_device* d);

@@ -92,3 +92,54 @@ def test_render_params_default():
     p = A.yk_render_params()
     A.lib().yk_render_params_default(C.byref(p))
     assert p.aa_passes == 1 and p.tile_size == 32 and p.filter == A.YK_FILTER_BOX
+
+
+def _state_copy(s):
+    """Rebuild scene s through the object-state entry points only."""
+    e = s.export()
+    t = Scene()
+    for m in s.material_states():
+        t.add_material_state(m)
+    tv, tm = e["tri_verts"], e["tri_material"]
+    # one mesh per run of equal material ids: same prims in the same order
+    start = 0
+    while start < len(tm):
+        end = start
+        while end < len(tm) and tm[end] == tm[start]:
+            end += 1
+        pts = tv[start:end].reshape(-1, 3)
+        faces = np.arange(len(pts), dtype=np.int32).reshape(-1, 3)
+        t.add_mesh(pts, faces, int(tm[start]))
+        start = end
+    for l in s.light_states():
+        t.add_area_light_state(l)
+    t.set_camera_state(s.camera_state())
+    t.build()
+    return t
+
+
+def test_object_state_path_equals_parameter_path():
+    """A scene given as reference object state (the plugin path) assembles to
+    the same prims, tree, materials, lights and camera as the parameter path."""
+    s, _ = probe_scene("cornell_pt", 64, 64)
+    t = _state_copy(s)
+    a, b = s.export(), t.export()
+    for k in ("tri_verts", "tri_material", "tri_normal", "nodes", "leaf_prims", "bound"):
+        assert (a[k].view(np.uint8) == b[k].view(np.uint8)).all(), k
+    assert bytes(s.camera_state()) == bytes(t.camera_state())
+    assert [bytes(x) for x in s.light_states()] == [bytes(x) for x in t.light_states()]
+    assert [bytes(x) for x in s.material_states()] == [bytes(x) for x in t.material_states()]
+    with pytest.raises(A.YkError):  # no parameter-level light to report
+        t.lights()
+
+
+def test_state_conversion_matches_reference_constructors():
+    s, _ = probe_scene("cornell_pt", 64, 64)
+    l = s.light_states()[0]
+    assert np.allclose(l.to_x[:], [0.5, 0, 0]) and np.allclose(l.to_y[:], [0, 0, 0.5])
+    assert np.float32(l.color[0]) == np.float32(np.float32(np.pi) * np.float32(10.0))
+    m = s.material_states()
+    assert m[3].type == A.YK_MAT_LIGHT and m[3].bsdf_flags == 0x80 and m[3].color[0] == 10.0
+    assert m[0].bsdf_flags == 0x14 and m[0].diffuse_strength == 1.0
+    c = s.camera_state()
+    assert c.resx == 64 and np.isclose(np.linalg.norm(c.cam_z[:]), 1.0)

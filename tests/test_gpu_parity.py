@@ -207,3 +207,16 @@ def test_c2_config_counts_and_frame(gpu_device):
     assert abs(st.shadow_rays - ref["shadow"]) <= 64
     d = np.abs(_to8(rgba).astype(int) - _golden("cornell_pt_1024_64spp_t8").astype(int))
     assert d.max() <= 1 and (d > 0).mean() < 1e-4
+
+
+def test_object_state_scene_renders_identically(gpu_device):
+    """The plugin path (scene handed over as reference object state) renders
+    the same film bits as the parameter path."""
+    from tests.test_abi import _state_copy
+    s, p, _ = scene("cornell_pt", 64, 64)
+    t = _state_copy(s)
+    gpu_device.upload(s)
+    a = gpu_device.render(p)
+    gpu_device.upload(t)
+    b = gpu_device.render(p)
+    assert (a.view(np.uint32) == b.view(np.uint32)).all()
