@@ -129,6 +129,7 @@ SIGNATURES = {
     "yk_trace_shadow": (C.c_int, [P, P, i64, P, C.POINTER(yk_stats)]),
     "yk_render_shard": (C.c_int, [P, C.POINTER(yk_render_params), i32, i32, P, C.POINTER(yk_stats)]),
     "yk_film_resolve": (C.c_int, [P, C.POINTER(yk_render_params), P, P]),
+    "yk_render_film": (C.c_int, [P, C.POINTER(yk_render_params), i32, i32, fp, C.POINTER(yk_stats)]),
     "yk_render": (C.c_int, [P, C.POINTER(yk_render_params), fp, C.POINTER(yk_stats)]),
 }
 

@@ -1665,6 +1665,23 @@ int yk_film_resolve(yk_device* d, const yk_render_params* p, const float* d_film
   YK_GUARD_END
 }
 
+int yk_render_film(yk_device* d, const yk_render_params* p, int32_t shard, int32_t nshards, float* film_host,
+                   yk_stats* st) {
+  if (!d || !p || !film_host) return set_error(YK_ERR_ARG, "yk_render_film: NULL argument");
+  if (p->width <= 0 || p->height <= 0) return set_error(YK_ERR_ARG, "empty render area");
+  YK_GUARD_BEGIN
+  HIPCHK(hipSetDevice(d->ordinal));
+  const size_t npx = (size_t)p->width * p->height;
+  DBuf<float> film;
+  film.ensure(npx * 5);
+  HIPCHK(hipMemsetAsync(film.p, 0, npx * 5 * sizeof(float), d->stream));
+  const int rc = yk_render_shard(d, p, shard, nshards, film.p, st);
+  if (rc != YK_OK) return rc;
+  HIPCHK(hipMemcpy(film_host, film.p, npx * 5 * sizeof(float), hipMemcpyDeviceToHost));
+  return YK_OK;
+  YK_GUARD_END
+}
+
 int yk_render(yk_device* d, const yk_render_params* p, float* rgba_host, yk_stats* st) {
   if (!d || !p || !rgba_host) return set_error(YK_ERR_ARG, "yk_render: NULL argument");
   YK_GUARD_BEGIN

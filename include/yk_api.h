@@ -211,6 +211,10 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
                     float* d_film, yk_stats* st);
 /* imageFilm_t::flush normalisation (+clampRGB0): film sums -> RGBA floats */
 int yk_film_resolve(yk_device* d, const yk_render_params* p, const float* d_film, float* d_rgba);
+/* convenience for host callers (the reference plugin): render the tiles of
+ * `shard` and return the film sums (width*height*5 floats) in host memory */
+int yk_render_film(yk_device* d, const yk_render_params* p, int32_t shard, int32_t nshards, float* film_host,
+                   yk_stats* st);
 /* convenience: whole frame on one device, RGBA float image to host memory */
 int yk_render(yk_device* d, const yk_render_params* p, float* rgba_host, yk_stats* st);
 

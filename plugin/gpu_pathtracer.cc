@@ -1,0 +1,290 @@
+// Reference-side integrator plugin: the drop-in that routes the reference's
+// "pathtracing" / "directlighting" integrators to libyk (include/yk_api.h).
+//
+// This file is compiled INSIDE the reference's build tree, as one more plugin
+// target next to src/integrators (it needs the reference's generated
+// yafray_config.h, so it is not built in this repository). It talks to the GPU
+// only through the C ABI, so the HIP library never sees a reference header or
+// a C++ object.
+//
+// Flow (scene_t::render, scene.cc:905-950):
+//   update() -> preprocess() -> render(film) -> cleanup() -> film->flush()
+//   preprocess(): hand prims (scene_t::update order, scene.cc:760-781),
+//                 material / area-light / camera *object state* to libyk,
+//                 build the kd-tree, upload to the device
+//   render():     yk_render_shard over all tiles, then write the film sums
+//                 into imageFilm_t's pixel buffer; the reference's own flush()
+//                 normalises them exactly as k_film_resolve does
+#include <core_api/environment.h>
+#include <core_api/imagefilm.h>
+#include <core_api/scene.h>
+#include <core_api/tiledintegrator.h>
+#include <cameras/perspectiveCamera.h>
+#include <lights/arealight.h>
+#include <materials/shinydiff.h>
+#include <yafraycore/meshtypes.h>
+#include <yafraycore/triangle.h>
+
+#include <cstring>
+#include <map>
+#include <vector>
+
+#include "yk_api.h"
+
+__BEGIN_YAFRAY
+
+// ---- read protected/private members without editing the reference -------
+// (explicit instantiation may name private members: [temp.explicit]/14)
+template <class Tag>
+struct member_of {
+  static typename Tag::type ptr;
+};
+template <class Tag>
+typename Tag::type member_of<Tag>::ptr;
+template <class Tag, typename Tag::type P>
+struct grant {
+  grant() { member_of<Tag>::ptr = P; }
+  static grant instance;
+};
+template <class Tag, typename Tag::type P>
+grant<Tag, P> grant<Tag, P>::instance;
+
+#define YK_COMMA ,
+#define YK_MEMBER(name, cls, mtype, member)             \
+  struct name {                                         \
+    typedef mtype cls::*type;                           \
+  };                                                    \
+  template struct grant<name, &cls::member>;
+YK_MEMBER(SceneMeshes, scene_t, std::map<objID_t YK_COMMA objData_t>, meshes)
+YK_MEMBER(TriPa, triangle_t, int, pa)
+YK_MEMBER(TriPb, triangle_t, int, pb)
+YK_MEMBER(TriPc, triangle_t, int, pc)
+YK_MEMBER(MeshPoints, triangleObject_t, std::vector<point3d_t>, points)
+YK_MEMBER(SdColor, shinyDiffuseMat_t, color_t, mDiffuseColor)
+YK_MEMBER(SdStrength, shinyDiffuseMat_t, float, mDiffuseStrength)
+YK_MEMBER(SdEmit, shinyDiffuseMat_t, color_t, mEmitColor)
+YK_MEMBER(AlCorner, areaLight_t, point3d_t, corner)
+YK_MEMBER(AlToX, areaLight_t, vector3d_t, toX)
+YK_MEMBER(AlToY, areaLight_t, vector3d_t, toY)
+YK_MEMBER(AlColor, areaLight_t, color_t, color)
+YK_MEMBER(AlSamples, areaLight_t, int, samples)
+YK_MEMBER(CamPos, camera_t, point3d_t, position)
+YK_MEMBER(CamZ, camera_t, vector3d_t, camZ)
+YK_MEMBER(CamVto, camera_t, vector3d_t, vto)
+YK_MEMBER(CamVup, camera_t, vector3d_t, vup)
+YK_MEMBER(CamVright, camera_t, vector3d_t, vright)
+YK_MEMBER(CamNear, camera_t, plane_t, near_plane)
+YK_MEMBER(CamFar, camera_t, plane_t, far_plane)
+YK_MEMBER(FilmImage, imageFilm_t, rgba2DImage_t*, image)
+YK_MEMBER(FilmCx0, imageFilm_t, int, cx0)
+YK_MEMBER(FilmCy0, imageFilm_t, int, cy0)
+YK_MEMBER(FilmFilterW, imageFilm_t, float, filterw)
+YK_MEMBER(FilmTable, imageFilm_t, float*, filterTable)
+YK_MEMBER(FilmTileSize, imageFilm_t, int, tileSize)
+#define GET(obj, Tag) ((obj).*member_of<Tag>::ptr)
+
+static void put3(float* d, float x, float y, float z) { d[0] = x; d[1] = y; d[2] = z; }
+
+class gpuTiledIntegrator_t : public tiledIntegrator_t {
+ public:
+  gpuTiledIntegrator_t(const yk_render_params& p, const char* name) : params(p) {
+    type = SURFACE;
+    integratorName = name;
+    integratorShortName = name;
+  }
+  ~gpuTiledIntegrator_t() { release(); }
+
+  bool preprocess() override {
+    release();
+    if (yk_scene_create(&ys) != YK_OK) return fail();
+    // materials: object state of the materials the prims reference
+    std::map<const material_t*, int32_t> mat_ids;
+    std::map<objID_t, objData_t>& meshes = GET(*scene, SceneMeshes);
+    for (auto& kv : meshes) {
+      objData_t& dat = kv.second;
+      if (!dat.obj->isVisible() || dat.obj->isBaseObject() || dat.type != TRIM) continue;
+      const int n = dat.obj->numPrimitives();
+      std::vector<const triangle_t*> prims(n);
+      dat.obj->getPrimitives(prims.data());
+      const std::vector<point3d_t>& pts = GET(*dat.obj, MeshPoints);
+      std::vector<float> xyz(3 * pts.size());
+      for (size_t i = 0; i < pts.size(); ++i) put3(&xyz[3 * i], pts[i].x, pts[i].y, pts[i].z);
+      // one yk mesh per run of prims with the same material, prim order kept
+      for (int a = 0; a < n;) {
+        const material_t* m = prims[a]->getMaterial();
+        int b = a;
+        std::vector<int32_t> faces;
+        while (b < n && prims[b]->getMaterial() == m) {
+          faces.push_back(GET(*prims[b], TriPa));
+          faces.push_back(GET(*prims[b], TriPb));
+          faces.push_back(GET(*prims[b], TriPc));
+          ++b;
+        }
+        int32_t mid;
+        if (!material_id(m, mat_ids, mid)) return false;
+        if (yk_scene_add_mesh(ys, xyz.data(), (int32_t)pts.size(), faces.data(), (int32_t)(faces.size() / 3),
+                              mid, nullptr) != YK_OK)
+          return fail();
+        a = b;
+      }
+    }
+    for (light_t* l : scene->lights) {
+      areaLight_t* al = dynamic_cast<areaLight_t*>(l);
+      if (!al) return unsupported("only area lights run on the GPU path");
+      yk_area_light_state s{};
+      const point3d_t& c = GET(*al, AlCorner);
+      const vector3d_t &x = GET(*al, AlToX), &y = GET(*al, AlToY);
+      const color_t& col = GET(*al, AlColor);
+      put3(s.corner, c.x, c.y, c.z);
+      put3(s.to_x, x.x, x.y, x.z);
+      put3(s.to_y, y.x, y.y, y.z);
+      put3(s.color, col.R, col.G, col.B);
+      s.samples = GET(*al, AlSamples);
+      if (yk_scene_add_area_light_state(ys, &s) != YK_OK) return fail();
+    }
+    const perspectiveCam_t* cam = dynamic_cast<const perspectiveCam_t*>(scene->getCamera());
+    if (!cam) return unsupported("only the perspective camera runs on the GPU path");
+    yk_camera_state cs{};
+    const camera_t& cb = *cam;
+    const point3d_t& pos = GET(cb, CamPos);
+    const vector3d_t &z = GET(cb, CamZ), &vto = GET(cb, CamVto), &vup = GET(cb, CamVup),
+                     &vr = GET(cb, CamVright);
+    put3(cs.position, pos.x, pos.y, pos.z);
+    put3(cs.cam_z, z.x, z.y, z.z);
+    put3(cs.vto, vto.x, vto.y, vto.z);
+    put3(cs.vup, vup.x, vup.y, vup.z);
+    put3(cs.vright, vr.x, vr.y, vr.z);
+    const vector3d_t &np = GET(cb, CamNear).p, &fp = GET(cb, CamFar).p;
+    put3(cs.near_p, np.x, np.y, np.z);
+    put3(cs.far_p, fp.x, fp.y, fp.z);
+    cs.resx = cam->resX();
+    cs.resy = cam->resY();
+    if (yk_scene_set_camera_state(ys, &cs) != YK_OK) return fail();
+    if (yk_scene_build(ys) != YK_OK) return fail();
+    if (yk_device_open(0, &dev) != YK_OK || yk_device_upload(dev, ys) != YK_OK) return fail();
+    return true;
+  }
+
+  bool render(imageFilm_t* film) override {
+    // render area and AA settings as the film / scene hold them
+    int aa_inc;
+    CFLOAT thr;
+    scene->getAAParameters(params.aa_samples, params.aa_passes, aa_inc, thr);
+    if (params.aa_passes != 1) return unsupported("AA_passes > 1 (adaptive AA) is not on the GPU path");
+    rgba2DImage_t* img = GET(*film, FilmImage);
+    const int w = img->getWidth(), h = img->getHeight();
+    params.width = w;
+    params.height = h;
+    params.xstart = GET(*film, FilmCx0);
+    params.ystart = GET(*film, FilmCy0);
+    params.tile_size = GET(*film, FilmTileSize);
+    // filter: the film built its table from (type, AA_pixelwidth)
+    // (imagefilm.cc:119-165); box tables are all 1, Mitchell's are not, and
+    // filterw = clamp(0.5 * pixelwidth * k, 0.501, 4) gives the width back
+    const float fw = GET(*film, FilmFilterW);
+    const bool box = GET(*film, FilmTable)[0] == 1.f && GET(*film, FilmTable)[255] == 1.f;
+    params.filter = box ? YK_FILTER_BOX : YK_FILTER_MITCHELL;
+    params.aa_pixelwidth = box ? 2.f * fw : 2.f * fw / 2.6f;
+    std::vector<float> sums((size_t)w * h * 5);
+    if (yk_render_film(dev, &params, 0, 1, sums.data(), nullptr) != YK_OK) return fail();
+    for (int j = 0; j < h; ++j)
+      for (int i = 0; i < w; ++i) {
+        const float* s = &sums[5 * ((size_t)j * w + i)];
+        pixel_t& px = (*img)(i, j);
+        px.col = colorA_t(s[0], s[1], s[2], s[3]);
+        px.weight = s[4];
+      }
+    return true;
+  }
+
+  void cleanup() override { release(); }
+
+  // unused: render() never calls renderTile()
+  colorA_t integrate(renderState_t&, diffRay_t&) const override { return colorA_t(0.f); }
+
+  static integrator_t* factory_path(paraMap_t& pm, renderEnvironment_t&) {
+    yk_render_params p;
+    yk_render_params_default(&p);  // pathIntegrator_t::factory defaults
+    p.integrator = YK_INTEGRATOR_PATH;
+    pm.getParam("raydepth", p.raydepth);
+    pm.getParam("path_samples", p.path_samples);
+    pm.getParam("bounces", p.bounces);
+    bool bg = true;
+    pm.getParam("bg_transp", bg);
+    p.transp_background = bg;
+    const std::string* cm = nullptr;
+    if (pm.getParam("caustic_type", cm)) p.caustic_type = (*cm == "none") ? YK_CAUSTIC_NONE : YK_CAUSTIC_PATH;
+    return new gpuTiledIntegrator_t(p, "PathTracer");
+  }
+  static integrator_t* factory_direct(paraMap_t& pm, renderEnvironment_t&) {
+    yk_render_params p;
+    yk_render_params_default(&p);
+    p.integrator = YK_INTEGRATOR_DIRECT;
+    pm.getParam("raydepth", p.raydepth);
+    bool bg = true;
+    pm.getParam("bg_transp", bg);
+    p.transp_background = bg;
+    return new gpuTiledIntegrator_t(p, "DirectLight");
+  }
+
+ private:
+  bool material_id(const material_t* m, std::map<const material_t*, int32_t>& ids, int32_t& id) {
+    auto it = ids.find(m);
+    if (it != ids.end()) return (id = it->second), true;
+    yk_material_state s{};
+    s.bsdf_flags = m->getFlags();
+    if (const shinyDiffuseMat_t* sd = dynamic_cast<const shinyDiffuseMat_t*>(m)) {
+      s.type = YK_MAT_SHINYDIFFUSE;
+      const color_t &c = GET(*sd, SdColor), &e = GET(*sd, SdEmit);
+      put3(s.color, c.R, c.G, c.B);
+      put3(s.emit_color, e.R, e.G, e.B);
+      s.diffuse_strength = GET(*sd, SdStrength);
+    } else if (s.bsdf_flags == BSDF_EMIT) {
+      // lightMat_t is defined in a .cc (simple.cc:36-70): read lightCol and
+      // doubleSided back through its virtual emit()
+      s.type = YK_MAT_LIGHT;
+      renderState_t st;
+      st.includeLights = true;
+      surfacePoint_t sp;
+      sp.N = vector3d_t(0, 0, 1);
+      const color_t front = m->emit(st, sp, vector3d_t(0, 0, 1));
+      const color_t back = m->emit(st, sp, vector3d_t(0, 0, -1));
+      put3(s.color, front.R, front.G, front.B);
+      s.double_sided = !back.isBlack();
+    } else {
+      return unsupported("material type not on the GPU path");
+    }
+    if (yk_scene_add_material_state(ys, &s, &id) != YK_OK) return fail();
+    ids[m] = id;
+    return true;
+  }
+  bool fail() {
+    Y_ERROR << integratorName << ": " << yk_last_error() << yendl;
+    return false;
+  }
+  bool unsupported(const char* what) {
+    Y_ERROR << integratorName << ": " << what << yendl;
+    return false;
+  }
+  void release() {
+    if (dev) yk_device_close(dev);
+    if (ys) yk_scene_destroy(ys);
+    dev = nullptr;
+    ys = nullptr;
+  }
+
+  yk_render_params params;
+  yk_scene* ys = nullptr;
+  yk_device* dev = nullptr;
+};
+
+extern "C" {
+YAFRAYPLUGIN_EXPORT void registerPlugin(renderEnvironment_t& render) {
+  // same names as the CPU plugins: loaded after them, these win
+  // (registerFactory is a map assignment, environment.cc:738-742)
+  render.registerFactory("pathtracing", gpuTiledIntegrator_t::factory_path);
+  render.registerFactory("directlighting", gpuTiledIntegrator_t::factory_direct);
+}
+}
+
+__END_YAFRAY
