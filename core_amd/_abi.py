@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libyk.so")
+LIB_PATH = os.environ.get("YK_LIB") or os.path.join(_HERE, "libyk.so")  # YK_LIB: tuning builds
 
 YK_OK = 0
 YK_ERR_ARG, YK_ERR_STATE, YK_ERR_HIP, YK_ERR_UNSUPPORTED, YK_ERR_ALLOC, YK_ERR_INTERNAL = 1, 2, 3, 4, 5, 6

@@ -18,6 +18,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -117,7 +118,11 @@ __device__ __forceinline__ bool bound_cross(const float* bb, v3 from, v3 dir, fl
 // entry stores t itself. The top kStackLds entries of every lane live in an
 // LDS ring; deeper ones spill to a global overflow area (rare: a 1M-tri tree
 // has depth ~40 but a ray rarely holds more than a dozen pending exits).
-constexpr int kStackLds = 16;
+#ifndef YK_STACK_LDS
+#define YK_STACK_LDS 16
+#endif
+constexpr int kStackLds = YK_STACK_LDS;  // power of two
+static_assert((kStackLds & (kStackLds - 1)) == 0, "LDS ring depth must be a power of two");
 
 struct LaneStack {
   uint2* lds;       // [kStackLds][64]
@@ -290,8 +295,13 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
 // packed with live rays until the queue drains. Stack: LDS, [depth][lane].
 // idx (optional): queue entry r is ray idx[r]; the result goes to the same
 // slot (used by the shadow queue, whose rays sit in per-sample slots).
+#ifdef YK_TRACE_WAVES_PER_EU
+#define YK_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(YK_TRACE_WAVES_PER_EU)))
+#else
+#define YK_TRACE_ATTR
+#endif
 template <bool CLOSEST>
-__global__ void __launch_bounds__(64) k_trace(DScene S, const yk_ray* __restrict__ rays,
+__global__ void __launch_bounds__(64) YK_TRACE_ATTR k_trace(DScene S, const yk_ray* __restrict__ rays,
                                               const unsigned* __restrict__ idx, long long n,
                                               yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
                                               unsigned long long* __restrict__ work,
@@ -543,7 +553,7 @@ struct Batch {
   float* emit_b;        // 3 floats: emission added at the current bounce
   int* pstate;          // PS_* bits
   int* lsel;            // light chosen by estimateOneDirectLight
-  int* qidx;            // index of the sample's current bounce ray in its queue
+  int* q_owner[2];      // camera sample of each bounce-queue entry
   yk_ray* q_rays[2];    // bounce queues (ping-pong)
   yk_hit* q_hits[2];
   unsigned* q_count;    // [0],[1] bounce queues, [2] shadow queue
@@ -839,27 +849,28 @@ __global__ void __launch_bounds__(256) k_path_start(DScene S, Batch B, RenderCon
   const unsigned q = wave_append(&B.q_count[1], emit ? 1u : 0u);
   if (emit) {
     B.q_rays[1][q] = r;
-    B.qidx[c] = (int)q;
+    B.q_owner[1][q] = (int)c;
   }
 }
 
 // Hit at bounce `depth` (1-based) of the current sub-path
 // (pathtracer.cc:189-298): estimateOneDirectLight shadow rays, emission,
-// and the BSDF sample of the next segment.
-__global__ void __launch_bounds__(256) k_shade_bounce(DScene S, Batch B, RenderConst R, long long nc, int depth,
+// and the BSDF sample of the next segment. One thread per live path (entry
+// qi of the input bounce queue, owned by camera sample c).
+__global__ void __launch_bounds__(256) k_shade_bounce(DScene S, Batch B, RenderConst R, long long nq, int depth,
                                                       int isub, int qin) {
-  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool valid = c < nc && (B.pstate[c] & PS_ALIVE);
+  const long long qi = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = qi < nq;
+  const long long c = valid ? B.q_owner[qin][qi] : 0;
   int nr = 0, kend = 0;
   bool emit_next = false;
   yk_ray nxt;
   if (valid) {
-    const int q = B.qidx[c];
-    const yk_hit h = B.q_hits[qin][q];
+    const yk_hit h = B.q_hits[qin][qi];
     if (h.prim < 0) {
       B.pstate[c] = 0;  // background: "continue" at depth 1, "break" later
     } else {
-      const yk_ray pr = B.q_rays[qin][q];
+      const yk_ray pr = B.q_rays[qin][qi];
       const v3 from = V3(pr.from[0], pr.from[1], pr.from[2]), dir = V3(pr.dir[0], pr.dir[1], pr.dir[2]);
       const SurfPt sp = make_surface(S, from, dir, h);
       const DMat& M = c_mats[sp.mat];
@@ -909,14 +920,16 @@ __global__ void __launch_bounds__(256) k_shade_bounce(DScene S, Batch B, RenderC
   const unsigned qn = wave_append(&B.q_count[qin ^ 1], emit_next ? 1u : 0u);
   if (emit_next) {
     B.q_rays[qin ^ 1][qn] = nxt;
-    B.qidx[c] = (int)qn;
+    B.q_owner[qin ^ 1][qn] = (int)c;
   }
 }
 
-// pathCol += lcol*throughput; throughput *= scol of the next segment.
-__global__ void __launch_bounds__(256) k_resolve_bounce(Batch B, RenderConst R, long long nc, int depth) {
-  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= nc) return;
+// pathCol += lcol*throughput; throughput *= scol of the next segment. One
+// thread per entry of the bounce queue k_shade_bounce consumed.
+__global__ void __launch_bounds__(256) k_resolve_bounce(Batch B, RenderConst R, long long nq, int depth, int qin) {
+  const long long qi = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (qi >= nq) return;
+  const long long c = B.q_owner[qin][qi];
   const int ps = B.pstate[c];
   if (!(ps & PS_RESOLVE)) return;
   c3 lcol = C3(0.f, 0.f, 0.f);
@@ -1114,7 +1127,7 @@ struct yk_device {
   // batch buffers (grown on demand, kept across renders)
   DBuf<unsigned> soffs, qcount, s_idx;
   DBuf<float> col, alpha, thr, pathcol, scol_next, wlast, emit_b, sl_contrib;
-  DBuf<int> prim_hit, pstate, lsel, qidx, tile_base;
+  DBuf<int> prim_hit, pstate, lsel, qo0, qo1, tile_base;
   DBuf<int4> tiles;
   DBuf<yk_ray> p_rays, qr0, qr1, s_rays;
   DBuf<yk_hit> p_hits, qh0, qh1;
@@ -1502,8 +1515,16 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   R.nlights = d->nlights;
   R.d1 = F.d1;
   const int K = std::max(1, 2 * d->sum_light_samples);
-  // batch = whole tiles, about 2M camera samples
-  const long long target = 2ll << 20;
+  // batch = whole tiles, about YK_BATCH_SAMPLES camera samples (default 32M:
+  // each trace launch ends in a tail of long rays, which large batches
+  // amortise), capped so per-batch buffers stay within ~24 GB of HBM
+  static const long long target_env = [] {
+    const char* e = std::getenv("YK_BATCH_SAMPLES");
+    const long long v = e ? std::atoll(e) : 0;
+    return v > 0 ? v : (32ll << 20);
+  }();
+  const long long bytes_per_sample = 400 + 52ll * K;
+  const long long target = std::max(1ll << 20, std::min(target_env, (24ll << 30) / bytes_per_sample));
   const long long tile_samples = (long long)F.tile * F.tile * spp;
   const int tiles_per_batch = (int)std::max<long long>(1, target / tile_samples);
   const long long maxc = (long long)tiles_per_batch * tile_samples;
@@ -1520,7 +1541,8 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   d->emit_b.ensure(3 * maxc);
   d->pstate.ensure(maxc);
   d->lsel.ensure(maxc);
-  d->qidx.ensure(maxc);
+  d->qo0.ensure(maxc);
+  d->qo1.ensure(maxc);
   d->qr0.ensure(maxc);
   d->qr1.ensure(maxc);
   d->qh0.ensure(maxc);
@@ -1549,7 +1571,8 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   B.emit_b = d->emit_b.p;
   B.pstate = d->pstate.p;
   B.lsel = d->lsel.p;
-  B.qidx = d->qidx.p;
+  B.q_owner[0] = d->qo0.p;
+  B.q_owner[1] = d->qo1.p;
   B.q_rays[0] = d->qr0.p;
   B.q_rays[1] = d->qr1.p;
   B.q_hits[0] = d->qh0.p;
@@ -1621,11 +1644,12 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
           launch_trace<true>(d, B.q_rays[qin], nullptr, nq, B.q_hits[qin], nullptr, S);
           HIPCHK(hipMemsetAsync(d->qcount.p + 2, 0, sizeof(unsigned), d->stream));
           HIPCHK(hipMemsetAsync(d->qcount.p + (qin ^ 1), 0, sizeof(unsigned), d->stream));
-          hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(nc)), dim3(256), 0, d->stream, d->S, B, R, nc, depth, isub,
-                             qin);
+          hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(nq)), dim3(256), 0, d->stream, d->S, B, R, (long long)nq,
+                             depth, isub, qin);
           HIPCHK(hipGetLastError());
           trace_shadow_queue();
-          hipLaunchKernelGGL(k_resolve_bounce, dim3(grid_for(nc)), dim3(256), 0, d->stream, B, R, nc, depth);
+          hipLaunchKernelGGL(k_resolve_bounce, dim3(grid_for(nq)), dim3(256), 0, d->stream, B, R, (long long)nq, depth,
+                             qin);
           HIPCHK(hipGetLastError());
           qin ^= 1;
         }
