@@ -247,7 +247,11 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t p = (n == 1) ? w0 : S.leaf[w0 + i];
     ntris++;
-    const float4 A = S.tris[3 * p], E1 = S.tris[3 * p + 1], E2 = S.tris[3 * p + 2];
+    float4 A = S.tris[3 * p], E1 = S.tris[3 * p + 1], E2 = S.tris[3 * p + 2];
+    // keep the three loads together (the compiler would otherwise sink A's
+    // load past the det test: a second dependent round trip per triangle)
+    asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x), "+v"(E2.y),
+                 "+v"(E2.z));
     float th, u, v;
     if (mt_intersect(V3(A.x, A.y, A.z), V3(E1.x, E1.y, E1.z), V3(E2.x, E2.y, E2.z), st.o, st.d, th, u, v)) {
       if (CLOSEST) {
@@ -305,7 +309,8 @@ __global__ void __launch_bounds__(64) YK_TRACE_ATTR k_trace(DScene S, const yk_r
                                               const unsigned* __restrict__ idx, long long n,
                                               yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
                                               unsigned long long* __restrict__ work,
-                                              unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf) {
+                                              unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf,
+                                              int refill_min) {
   __shared__ uint2 lds[kStackLds * 64];
   const int lane = threadIdx.x;
   const LaneStack stk{lds, ovf, gridDim.x * 64u, blockIdx.x * 64u + (unsigned)lane, lane};
@@ -313,18 +318,26 @@ __global__ void __launch_bounds__(64) YK_TRACE_ATTR k_trace(DScene S, const yk_r
   bool exhausted = false;
   Trav st;
   unsigned nnodes = 0, ntris = 0, steps = 0, nerr = 0;
+  // wave-private pool of ray indices [pool_next, pool_end): one atomic per
+  // kPoolChunk rays instead of one per refill
+  constexpr long long kPoolChunk = 64;
+  long long pool_next = 0, pool_end = 0;
   for (;;) {
     const unsigned long long want = __ballot(rid < 0 && !exhausted);
     const unsigned long long act = __ballot(rid >= 0);
-    if (want != 0ull && (act == 0ull || __popcll(want) >= 24)) {
+    if (want != 0ull && (act == 0ull || __popcll(want) >= refill_min)) {
       const int cnt = __popcll(want);
-      const int leader = __ffsll((long long)want) - 1;
-      unsigned long long base = 0;
-      if (lane == leader) base = atomicAdd(work, (unsigned long long)cnt);
-      base = shfl_u64(base, leader);
+      const long long avail = pool_end - pool_next;
+      long long chunk = pool_end;  // start of a newly grabbed chunk (if any)
+      if (avail < cnt) {
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(work, (unsigned long long)kPoolChunk);
+        base = shfl_u64(base, 0);
+        chunk = (long long)base;
+      }
       if (rid < 0 && !exhausted) {
         const int rank = __popcll(want & ((1ull << lane) - 1ull));
-        const long long q = (long long)base + rank;
+        const long long q = (rank < avail) ? pool_next + rank : chunk + (rank - avail);
         if (q < n) {
           const long long r = idx ? (long long)idx[q] : q;
           const yk_ray ray = rays[r];
@@ -338,6 +351,12 @@ __global__ void __launch_bounds__(64) YK_TRACE_ATTR k_trace(DScene S, const yk_r
         } else {
           exhausted = true;
         }
+      }
+      if (avail < cnt) {
+        pool_next = chunk + (cnt - avail);
+        pool_end = chunk + kPoolChunk;
+      } else {
+        pool_next += cnt;
       }
     }
     if (__ballot(rid >= 0) == 0ull) {
@@ -1262,6 +1281,16 @@ void upload_qmc() {
 
 int stack_depth(const yk_device* d) { return d->max_depth + 2; }
 
+// idle lanes a wave collects before it fetches new rays (YK_REFILL to tune)
+int refill_min() {
+  static const int v = [] {
+    const char* e = std::getenv("YK_REFILL");
+    const int r = e ? std::atoi(e) : 0;
+    return (r >= 1 && r <= 64) ? r : 24;
+  }();
+  return v;
+}
+
 template <bool CLOSEST>
 void launch_trace(yk_device* d, const yk_ray* rays, const unsigned* idx, long long n, yk_hit* hits, uint8_t* occ,
                   yk_stats* st) {
@@ -1282,7 +1311,7 @@ void launch_trace(yk_device* d, const yk_ray* rays, const unsigned* idx, long lo
   if (D > kStackLds) d->ovf.ensure((size_t)(D - kStackLds) * (size_t)grid * 64);
   HIPCHK(hipEventRecord(d->ev0, d->stream));
   hipLaunchKernelGGL(k_trace<CLOSEST>, dim3((unsigned)grid), dim3(64), 0, d->stream, d->S, rays, idx, n, hits, occ,
-                     ctr, ctr + 1, d->ovf.p);
+                     ctr, ctr + 1, d->ovf.p, refill_min());
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(d->ev1, d->stream));
   unsigned long long h[4];
