@@ -147,16 +147,20 @@ struct Trav {
   float tmin, dist;
   float en_t, ex_t, ex_split;
   v3 en_pb, ex_pb;
-  int ex_code, ex_node;
+  uint32_t ex_w;  // (exit far node + 1) | axis code << 30; node -1 = the initial exit
   int node, sp;
   float Z, b1, b2;
   int prim;
 };
 
+// v[axis] for axis in 0..2 via selects (no dynamic register indexing)
+__device__ __forceinline__ float sel3(v3 v, uint32_t ax) { return ax == 0u ? v.x : (ax == 1u ? v.y : v.z); }
+
+// pb of the current exit: pb[code] = split, other axes from + t*dir
 __device__ __forceinline__ void exit_pb(Trav& st) {
+  const uint32_t code = st.ex_w >> 30;
   const float x = st.o.x + st.ex_t * st.d.x, y = st.o.y + st.ex_t * st.d.y, z = st.o.z + st.ex_t * st.d.z;
-  st.ex_pb = V3(st.ex_code == 0 ? st.ex_split : x, st.ex_code == 1 ? st.ex_split : y,
-                st.ex_code == 2 ? st.ex_split : z);
+  st.ex_pb = V3(code == 0u ? st.ex_split : x, code == 1u ? st.ex_split : y, code == 2u ? st.ex_split : z);
 }
 
 // scene_t::intersect (scene.cc:852-879) / isShadowed (scene.cc:881-902)
@@ -182,9 +186,8 @@ __device__ __forceinline__ bool trav_begin(const DScene& S, Trav& st, const yk_r
   st.en_t = a;
   st.en_pb = (a >= 0.0f) ? vadd(st.o, vmul(a, st.d)) : st.o;
   st.ex_t = b;
-  st.ex_code = 3;
-  st.ex_split = b;  // code 3 entries carry t
-  st.ex_node = -1;
+  st.ex_split = b;          // code 3 entries carry t
+  st.ex_w = 3u << 30;       // node -1, code 3
   exit_pb(st);
   st.node = 0;
   st.sp = 0;
@@ -193,7 +196,12 @@ __device__ __forceinline__ bool trav_begin(const DScene& S, Trav& st, const yk_r
 
 // One iteration of the reference's outer traversal loop (kdtree.cc:707-812):
 // descend to a leaf, test its primitives, then stop or pop. Returns true when
-// the ray is finished.
+// the ray is finished. The descent's four reference cases reduce to a
+// near/far choice plus an optional push: with enter <= split the near child
+// is the left one and the far one is pushed unless exit <= split; otherwise
+// the near child is the right one and the left is pushed unless split < exit.
+// (The reference's "exit == split" branch follows "exit <= split" and is
+// never taken, NaN included.)
 template <bool CLOSEST>
 __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneStack& stk, unsigned& nnodes,
                                           unsigned& ntris, bool& occluded) {
@@ -201,45 +209,25 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
   int node = st.node;
   uint2 nd = S.nodes[node];
   nnodes++;
-  while ((nd.y & 3u) != 3u) {
-    const int axis = (int)(nd.y & 3u);
+  for (;;) {
+    const uint32_t ax = nd.y & 3u;
+    if (ax == 3u) break;
     const float split = __uint_as_float(nd.x);
     const int right = (int)(nd.y >> 2);
-    const float enp = vget(st.en_pb, axis), exq = vget(st.ex_pb, axis);
-    int far_;
-    if (enp <= split) {
-      if (exq <= split) {
-        node = node + 1;
-        nd = S.nodes[node];
-        nnodes++;
-        continue;
-      }
-      if (exq == split) {
-        node = right;
-        nd = S.nodes[node];
-        nnodes++;
-        continue;
-      }
-      far_ = right;
-      node = node + 1;
-    } else {
-      if (split < exq) {
-        node = right;
-        nd = S.nodes[node];
-        nnodes++;
-        continue;
-      }
-      far_ = node + 1;
-      node = right;
+    const float enp = sel3(st.en_pb, ax), exq = sel3(st.ex_pb, ax);
+    const bool left_first = enp <= split;
+    const bool push = left_first ? !(exq <= split) : !(split < exq);
+    if (push) {
+      const int far_ = left_first ? right : node + 1;
+      const float t = (split - sel3(st.o, ax)) * sel3(st.inv, ax);
+      stk.push(st.sp, make_uint2(__float_as_uint(st.ex_split), st.ex_w));
+      st.sp++;
+      st.ex_t = t;
+      st.ex_split = split;
+      st.ex_w = (uint32_t)(far_ + 1) | (ax << 30);
+      exit_pb(st);
     }
-    const float t = (split - vget(st.o, axis)) * vget(st.inv, axis);
-    stk.push(st.sp, make_uint2(__float_as_uint(st.ex_split), ((uint32_t)(st.ex_node + 1)) | ((uint32_t)st.ex_code << 30)));
-    st.sp++;
-    st.ex_t = t;
-    st.ex_split = split;
-    st.ex_code = axis;
-    st.ex_node = far_;
-    exit_pb(st);
+    node = left_first ? node + 1 : right;
     nd = S.nodes[node];
     nnodes++;
   }
@@ -271,7 +259,7 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
   // pop: entry := exit, exit := previous exit
   st.en_t = st.ex_t;
   st.en_pb = st.ex_pb;
-  st.node = st.ex_node;
+  st.node = (int)(st.ex_w & 0x3FFFFFFFu) - 1;
   if (st.node < 0) return true;
   if ((unsigned)st.node >= S.nnodes || st.sp <= 0) {  // corrupt state: never index out of the tree
     st.prim = -2;
@@ -280,9 +268,9 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
   st.sp--;
   const uint2 e = stk.pop(st.sp);
   st.ex_split = __uint_as_float(e.x);
-  st.ex_node = (int)(e.y & 0x3FFFFFFFu) - 1;
-  st.ex_code = (int)(e.y >> 30);
-  st.ex_t = (st.ex_code == 3) ? st.ex_split : (st.ex_split - vget(st.o, st.ex_code)) * vget(st.inv, st.ex_code);
+  st.ex_w = e.y;
+  const uint32_t code = e.y >> 30;
+  st.ex_t = (code == 3u) ? st.ex_split : (st.ex_split - sel3(st.o, code)) * sel3(st.inv, code);
   exit_pb(st);
   return false;
 }
