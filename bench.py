@@ -119,9 +119,9 @@ def main():
         return
 
     # roofline of the dominant kernel, from HIP events on the kernel's stream
-    kc = dict(name="k_trace<closest>", launches=w[6], ms=ms_c,
+    kc = dict(name="k_trace_closest", launches=w[6], ms=ms_c,
               bytes=algorithmic_bytes(w[0], w[2], w[3], 16))
-    ks = dict(name="k_trace<shadow>", launches=w[7], ms=ms_s,
+    ks = dict(name="k_trace_shadow", launches=w[7], ms=ms_s,
               bytes=algorithmic_bytes(w[1], w[4], w[5], 1))
     for k in (kc, ks):
         k["gbs"] = k["bytes"] / (k["ms"] * 1e-3) / 1e9 if k["ms"] > 0 else 0.0

@@ -119,7 +119,7 @@ __device__ __forceinline__ bool bound_cross(const float* bb, v3 from, v3 dir, fl
 // LDS ring; deeper ones spill to a global overflow area (rare: a 1M-tri tree
 // has depth ~40 but a ray rarely holds more than a dozen pending exits).
 #ifndef YK_STACK_LDS
-#define YK_STACK_LDS 16
+#define YK_STACK_LDS 8
 #endif
 constexpr int kStackLds = YK_STACK_LDS;  // power of two
 static_assert((kStackLds & (kStackLds - 1)) == 0, "LDS ring depth must be a power of two");
@@ -287,47 +287,41 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
 // packed with live rays until the queue drains. Stack: LDS, [depth][lane].
 // idx (optional): queue entry r is ray idx[r]; the result goes to the same
 // slot (used by the shadow queue, whose rays sit in per-sample slots).
-#ifdef YK_TRACE_WAVES_PER_EU
-#define YK_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(YK_TRACE_WAVES_PER_EU)))
-#else
-#define YK_TRACE_ATTR
-#endif
 template <bool CLOSEST>
-__global__ void __launch_bounds__(64) YK_TRACE_ATTR k_trace(DScene S, const yk_ray* __restrict__ rays,
-                                              const unsigned* __restrict__ idx, long long n,
-                                              yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
-                                              unsigned long long* __restrict__ work,
-                                              unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf,
-                                              int refill_min) {
+__device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx,
+                                           long long n, yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
+                                           unsigned long long* __restrict__ work, unsigned long long* __restrict__ ctr,
+                                           uint2* __restrict__ ovf, int refill_min) {
   __shared__ uint2 lds[kStackLds * 64];
   const int lane = threadIdx.x;
   const LaneStack stk{lds, ovf, gridDim.x * 64u, blockIdx.x * 64u + (unsigned)lane, lane};
-  long long rid = -1;
+  int rid = -1;  // ray of this lane (host guarantees n < 2^31)
   bool exhausted = false;
   Trav st;
-  unsigned nnodes = 0, ntris = 0, steps = 0, nerr = 0;
+  unsigned nnodes = 0, ntris = 0, nerr = 0;
   // wave-private pool of ray indices [pool_next, pool_end): one atomic per
-  // kPoolChunk rays instead of one per refill
-  constexpr long long kPoolChunk = 64;
-  long long pool_next = 0, pool_end = 0;
+  // kPoolChunk rays instead of one per refill (wave-uniform, scalar registers)
+  constexpr unsigned kPoolChunk = 64;
+  unsigned pool_next = 0, pool_end = 0;
+  unsigned iters = 0;  // wave watchdog: a valid tree never gets near the cap
   for (;;) {
     const unsigned long long want = __ballot(rid < 0 && !exhausted);
     const unsigned long long act = __ballot(rid >= 0);
     if (want != 0ull && (act == 0ull || __popcll(want) >= refill_min)) {
-      const int cnt = __popcll(want);
-      const long long avail = pool_end - pool_next;
-      long long chunk = pool_end;  // start of a newly grabbed chunk (if any)
+      const unsigned cnt = (unsigned)__popcll(want);
+      const unsigned avail = pool_end - pool_next;
+      unsigned chunk = pool_end;  // start of a newly grabbed chunk (if any)
       if (avail < cnt) {
         unsigned long long base = 0;
         if (lane == 0) base = atomicAdd(work, (unsigned long long)kPoolChunk);
         base = shfl_u64(base, 0);
-        chunk = (long long)base;
+        chunk = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)min(base, (unsigned long long)0x7FFFFFFF));
       }
       if (rid < 0 && !exhausted) {
-        const int rank = __popcll(want & ((1ull << lane) - 1ull));
-        const long long q = (rank < avail) ? pool_next + rank : chunk + (rank - avail);
-        if (q < n) {
-          const long long r = idx ? (long long)idx[q] : q;
+        const unsigned rank = (unsigned)__popcll(want & ((1ull << lane) - 1ull));
+        const unsigned q = (rank < avail) ? pool_next + rank : chunk + (rank - avail);
+        if ((long long)q < n) {
+          const int r = idx ? (int)idx[q] : (int)q;
           const yk_ray ray = rays[r];
           if (trav_begin<CLOSEST>(S, st, ray)) {
             rid = r;
@@ -346,15 +340,18 @@ __global__ void __launch_bounds__(64) YK_TRACE_ATTR k_trace(DScene S, const yk_r
       } else {
         pool_next += cnt;
       }
+      pool_next = (unsigned)__builtin_amdgcn_readfirstlane((int)pool_next);
+      pool_end = (unsigned)__builtin_amdgcn_readfirstlane((int)pool_end);
     }
     if (__ballot(rid >= 0) == 0ull) {
       if (__ballot(!exhausted) == 0ull) break;
       continue;
     }
+    const bool runaway = ++iters > (1u << 30);
     if (rid >= 0) {
       bool occ = false;
       bool done = trav_step<CLOSEST>(S, st, stk, nnodes, ntris, occ);
-      if (++steps > (1u << 22)) {  // watchdog: no ray of a valid tree gets near this
+      if (runaway) {
         st.prim = -2;
         done = true;
       }
@@ -363,7 +360,6 @@ __global__ void __launch_bounds__(64) YK_TRACE_ATTR k_trace(DScene S, const yk_r
         st.prim = -1;
       }
       if (done) {
-        steps = 0;
         if (CLOSEST) {
           hits[rid] = (st.prim >= 0) ? yk_hit{st.prim, st.Z, st.b1, st.b2} : yk_hit{-1, 0.f, 0.f, 0.f};
         } else {
@@ -372,6 +368,7 @@ __global__ void __launch_bounds__(64) YK_TRACE_ATTR k_trace(DScene S, const yk_r
         rid = -1;
       }
     }
+    if (runaway) exhausted = true;
   }
   // wave-reduced work counters (nodes visited, triangle tests)
   unsigned long long a = nnodes, b = ntris;
@@ -385,6 +382,28 @@ __global__ void __launch_bounds__(64) YK_TRACE_ATTR k_trace(DScene S, const yk_r
     atomicAdd(&ctr[1], b);
   }
   if (nerr) atomicAdd(&ctr[2], (unsigned long long)nerr);
+}
+
+// Occupancy targets (measured on MI355X, 1M-tri scene): the closest-hit
+// kernel runs best at 6 waves/SIMD, the any-hit kernel at 7 (its state is
+// smaller); with an 8-deep LDS ring (4 KB per wave) registers set the limit.
+#ifndef YK_CLOSEST_WAVES
+#define YK_CLOSEST_WAVES 6
+#endif
+#ifndef YK_SHADOW_WAVES
+#define YK_SHADOW_WAVES 7
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
+k_trace_closest(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, long long n,
+                yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
+                unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int refill_min) {
+  trace_body<true>(S, rays, idx, n, hits, occl, work, ctr, ovf, refill_min);
+}
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
+k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, long long n,
+               yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
+               unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int refill_min) {
+  trace_body<false>(S, rays, idx, n, hits, occl, work, ctr, ovf, refill_min);
 }
 
 // ============================================================ shading
@@ -1283,13 +1302,14 @@ template <bool CLOSEST>
 void launch_trace(yk_device* d, const yk_ray* rays, const unsigned* idx, long long n, yk_hit* hits, uint8_t* occ,
                   yk_stats* st) {
   if (n <= 0) return;
+  if (n > 0x7FFFFFFFll - (1ll << 24)) throw std::invalid_argument("ray batch too large (max ~2^31 rays per call)");
   unsigned long long* ctr = d->counters.p;
   HIPCHK(hipMemsetAsync(ctr, 0, 4 * sizeof(unsigned long long), d->stream));
   // persistent grid: as many waves as the chip keeps resident (VGPR/LDS bound)
   static int per_cu[2] = {0, 0};
   if (!per_cu[CLOSEST]) {
     int blocks = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace<CLOSEST>, 64, 0));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, CLOSEST ? k_trace_closest : k_trace_shadow, 64, 0));
     per_cu[CLOSEST] = std::max(1, blocks);
   }
   long long grid = (long long)d->cus * per_cu[CLOSEST];
@@ -1298,7 +1318,8 @@ void launch_trace(yk_device* d, const yk_ray* rays, const unsigned* idx, long lo
   const int D = stack_depth(d);
   if (D > kStackLds) d->ovf.ensure((size_t)(D - kStackLds) * (size_t)grid * 64);
   HIPCHK(hipEventRecord(d->ev0, d->stream));
-  hipLaunchKernelGGL(k_trace<CLOSEST>, dim3((unsigned)grid), dim3(64), 0, d->stream, d->S, rays, idx, n, hits, occ,
+  hipLaunchKernelGGL(CLOSEST ? k_trace_closest : k_trace_shadow, dim3((unsigned)grid), dim3(64), 0, d->stream, d->S, rays,
+                     idx, n, hits, occ,
                      ctr, ctr + 1, d->ovf.p, refill_min());
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(d->ev1, d->stream));

@@ -34,8 +34,10 @@ def read_counter(d, name):
 
 
 def classify(kernel):
-    if "k_trace" in kernel:
-        return "closest" if "ILb1E" in kernel or "<true>" in kernel else "shadow"
+    if "k_trace_closest" in kernel:
+        return "closest"
+    if "k_trace_shadow" in kernel:
+        return "shadow"
     return None
 
 
