@@ -126,19 +126,17 @@ static_assert((kStackLds & (kStackLds - 1)) == 0, "LDS ring depth must be a powe
 
 struct LaneStack {
   uint2* lds;       // [kStackLds][64]
-  uint2* ovf;       // [depth - kStackLds][ovf_stride]
-  unsigned stride;  // lanes in the grid
-  unsigned gl;      // this lane's global index
+  uint2* ovf;       // this lane's overflow entries, contiguous (one cache line holds 8)
   int lane;
   __device__ __forceinline__ void push(int sp, uint2 e) const {
     uint2* slot = lds + (sp & (kStackLds - 1)) * 64 + lane;
-    if (sp >= kStackLds) ovf[(size_t)(sp - kStackLds) * stride + gl] = *slot;
+    if (sp >= kStackLds) ovf[sp - kStackLds] = *slot;
     *slot = e;
   }
   __device__ __forceinline__ uint2 pop(int sp) const {  // sp = index of the entry to pop
     uint2* slot = lds + (sp & (kStackLds - 1)) * 64 + lane;
     const uint2 e = *slot;
-    if (sp >= kStackLds) *slot = ovf[(size_t)(sp - kStackLds) * stride + gl];
+    if (sp >= kStackLds) *slot = ovf[sp - kStackLds];
     return e;
   }
 };
@@ -291,10 +289,10 @@ template <bool CLOSEST>
 __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx,
                                            long long n, yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
                                            unsigned long long* __restrict__ work, unsigned long long* __restrict__ ctr,
-                                           uint2* __restrict__ ovf, int refill_min) {
+                                           uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
   __shared__ uint2 lds[kStackLds * 64];
   const int lane = threadIdx.x;
-  const LaneStack stk{lds, ovf, gridDim.x * 64u, blockIdx.x * 64u + (unsigned)lane, lane};
+  const LaneStack stk{lds, ovf + (size_t)(blockIdx.x * 64u + (unsigned)lane) * (unsigned)ovf_depth, lane};
   int rid = -1;  // ray of this lane (host guarantees n < 2^31)
   bool exhausted = false;
   Trav st;
@@ -396,14 +394,14 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
 k_trace_closest(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, long long n,
                 yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
-                unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int refill_min) {
-  trace_body<true>(S, rays, idx, n, hits, occl, work, ctr, ovf, refill_min);
+                unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
+  trace_body<true>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
 k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, long long n,
                yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
-               unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int refill_min) {
-  trace_body<false>(S, rays, idx, n, hits, occl, work, ctr, ovf, refill_min);
+               unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
+  trace_body<false>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 
 // ============================================================ shading
@@ -536,21 +534,25 @@ __device__ __forceinline__ bool light_hit(const DLight& L, v3 from, v3 dir, floa
 
 // ------------------------------------------------------------ queues
 
-// Wave-aggregated append of m items: one atomicAdd per wave, each lane gets
-// a contiguous range. Must be called by the whole wave (m may be 0).
-__device__ __forceinline__ unsigned wave_append(unsigned* counter, unsigned m) {
+// Reserves m_s shadow-queue and m_b bounce-queue entries with ONE returning
+// atomic per wave: the counter word holds (bounce count << 32) | shadow
+// count. Whole-wave call; returns each lane's first index in both queues.
+__device__ __forceinline__ void wave_append2(unsigned long long* counter, unsigned m_s, unsigned m_b,
+                                             unsigned& base_s, unsigned& base_b) {
   const int lane = threadIdx.x & 63;
-  unsigned incl = m;
+  const unsigned long long m = ((unsigned long long)m_b << 32) | m_s;
+  unsigned long long incl = m;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
-    const unsigned v = __shfl_up(incl, off);
-    if (lane >= off) incl += v;
+    const unsigned lo = __shfl_up((unsigned)incl, off), hi = __shfl_up((unsigned)(incl >> 32), off);
+    if (lane >= off) incl += ((unsigned long long)hi << 32) | lo;
   }
-  const unsigned total = __shfl(incl, 63);
-  unsigned base = 0;
+  const unsigned long long total = shfl_u64(incl, 63);
+  unsigned long long base = 0;
   if (lane == 63 && total) base = atomicAdd(counter, total);
-  base = __shfl(base, 63);
-  return base + incl - m;
+  base = shfl_u64(base, 63) + incl - m;
+  base_s = (unsigned)base;
+  base_b = (unsigned)(base >> 32);
 }
 
 // Shadow-ray slot flags
@@ -582,7 +584,7 @@ struct Batch {
   int* q_owner[2];      // camera sample of each bounce-queue entry
   yk_ray* q_rays[2];    // bounce queues (ping-pong)
   yk_hit* q_hits[2];
-  unsigned* q_count;    // [0],[1] bounce queues, [2] shadow queue
+  unsigned long long* q_count;  // [b]: (entries of bounce queue b << 32) | shadow entries of the launch filling b
   yk_ray* s_rays;       // K per camera sample
   uint8_t* s_occl;      // K per camera sample
   unsigned* s_idx;      // compacted shadow queue of slot indices
@@ -673,9 +675,11 @@ __device__ __forceinline__ void put_slot(const Batch& B, long long slot, uint8_t
 
 // mcIntegrator_t::doLightEstimation (area light), mcintegrator.cc:73-195, split
 // at its isShadowed calls: every shadow ray it would trace is written to its
-// slot with the contribution it adds when unoccluded. Returns #rays.
+// slot with the contribution it adds when unoccluded. Returns #rays; sets bit
+// k of `traced` (k < 64) for each slot that holds a ray.
 __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, int li, const SurfPt& sp, v3 wo,
-                                         unsigned pixelSample, unsigned soffs, unsigned loffs) {
+                                         unsigned pixelSample, unsigned soffs, unsigned loffs,
+                                         unsigned long long& traced) {
   const DLight& L = c_lights[li];
   const DMat& M = c_mats[sp.mat];
   const int n = L.samples;
@@ -686,6 +690,7 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
   Halton h2, h3;
   hal_start(h2, 2u, offs - 1u);
   hal_start(h3, 3u, offs - 1u);
+  const Halton h2_start = h2, h3_start = h3;  // the MIS half restarts at the same index
   for (int i = 0; i < n; ++i) {
     const float s1 = hal_next(h2), s2 = hal_next(h3);
     const long long slot = c * B.K + k0 + i;
@@ -697,6 +702,7 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
     }
     put_ray(B.s_rays[slot], sp.P, ldir, YK_SHADOW_BIAS, ltmax);
     ++nr;
+    if (k0 + i < 64) traced |= 1ull << (k0 + i);
     if (!(lpdf > 1e-6f)) {
       put_slot(B, slot, SL_TRACED, black);
       continue;
@@ -716,8 +722,8 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
     }
     put_slot(B, slot, SL_TRACED | SL_ADDS, v);
   }
-  hal_start(h2, 2u, offs - 1u);
-  hal_start(h3, 3u, offs - 1u);
+  h2 = h2_start;
+  h3 = h3_start;
   for (int i = 0; i < n; ++i) {
     const float s1 = hal_next(h2), s2 = hal_next(h3);
     const long long slot = c * B.K + k0 + n + i;
@@ -734,6 +740,7 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
     }
     put_ray(B.s_rays[slot], sp.P, bdir, YK_MIN_RAYDIST, bt);
     ++nr;
+    if (k0 + n + i < 64) traced |= 1ull << (k0 + n + i);
     if (!(lightPdf > 1e-6f)) {
       put_slot(B, slot, SL_TRACED, black);
       continue;
@@ -748,24 +755,51 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
   return nr;
 }
 
-// Appends the traced slots [kbeg,kend) of sample c to the shadow queue, in
-// slot order. Whole-wave call.
-__device__ __forceinline__ void flush_shadow(const Batch& B, long long c, int kbeg, int kend, int nr, bool valid) {
-  const unsigned base = wave_append(&B.q_count[2], valid ? (unsigned)nr : 0u);
-  if (!valid || nr == 0) return;
+// Writes the traced slots [0,kend) of sample c to the shadow queue from
+// `base`, in slot order (bit mask for the first 64 slots, flags beyond).
+__device__ __forceinline__ void flush_shadow(const Batch& B, long long c, int kend, int nr, unsigned base,
+                                             unsigned long long traced) {
+  if (nr == 0) return;
   unsigned r = base;
-  for (int k = kbeg; k < kend; ++k) {
+  for (int k = 0; k < kend; ++k) {
     const long long slot = c * B.K + k;
-    if (B.sl_flags[slot] & SL_TRACED) B.s_idx[r++] = (unsigned)slot;
+    const bool t = k < 64 ? ((traced >> k) & 1ull) != 0ull : (B.sl_flags[slot] & SL_TRACED) != 0;
+    if (t) B.s_idx[r++] = (unsigned)slot;
   }
 }
 
+// First segment of sub-path isub from a diffuse camera-ray hit: sample the
+// primary BSDF (pathtracer.cc:169-187). Returns the segment's ray.
+__device__ __forceinline__ yk_ray path_first_segment(const Batch& B, const RenderConst& R, long long c,
+                                                     const SurfPt& sp, const DMat& M, v3 dir, int isub) {
+  const unsigned s = (unsigned)(c % R.spp);
+  const unsigned offs = (unsigned)(R.nsub * (int)s) + B.soffs[c] + (unsigned)isub;
+  const float s1 = ri_vdc(offs, 0u);
+  const float s2 = (float)scr_halton(2, offs);
+  float pdf, W = B.wlast[c];
+  bool ok;
+  v3 pdir = V3(0.f, 0.f, 0.f);
+  c3 scol = mat_sample(M, sp, vneg(dir), pdir, s1, s2, BSDF_DIFFUSE | BSDF_REFLECT | BSDF_TRANSMIT, pdf, W, ok);
+  B.wlast[c] = W;
+  scol = cscale(W, scol);
+  B.thr[3 * c] = scol.r;
+  B.thr[3 * c + 1] = scol.g;
+  B.thr[3 * c + 2] = scol.b;
+  yk_ray r;
+  put_ray(r, sp.P, pdir, YK_MIN_RAYDIST, -1.0f);
+  return r;
+}
+
 // Camera-ray hit (pathtracer.cc:146-160, directlight.cc:124-135): emission
-// and the estimateAllDirectLight shadow rays.
+// and the estimateAllDirectLight shadow rays; for the path tracer also the
+// first segment of sub-path 0 (appended to bounce queue 1).
 __global__ void __launch_bounds__(256) k_shade_primary(DScene S, Batch B, RenderConst R, long long nc) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = c < nc;
   int nr = 0, kend = 0;
+  unsigned long long traced = 0;
+  bool emit = false;
+  yk_ray seg;
   if (valid) {
     const yk_hit h = B.p_hits[c];
     c3 col = C3(0.f, 0.f, 0.f);
@@ -784,10 +818,15 @@ __global__ void __launch_bounds__(256) k_shade_primary(DScene S, Batch B, Render
         const unsigned s = (unsigned)(c % R.spp);
         int k0 = 0;
         for (int l = 0; l < R.nlights; ++l) {
-          nr += gen_light(B, c, k0, l, sp, wo, s, B.soffs[c], (unsigned)l);
+          nr += gen_light(B, c, k0, l, sp, wo, s, B.soffs[c], (unsigned)l, traced);
           k0 += 2 * c_lights[l].samples;
         }
         kend = k0;
+        if (R.integrator == YK_INTEGRATOR_PATH) {
+          B.wlast[c] = 0.f;
+          seg = path_first_segment(B, R, c, sp, M, dir, 0);
+          emit = true;
+        }
       }
       alpha = 1.0f;
     }
@@ -799,9 +838,15 @@ __global__ void __launch_bounds__(256) k_shade_primary(DScene S, Batch B, Render
     B.pathcol[3 * c] = 0.f;
     B.pathcol[3 * c + 1] = 0.f;
     B.pathcol[3 * c + 2] = 0.f;
-    B.wlast[c] = 0.f;
+    if (!emit) B.wlast[c] = 0.f;
   }
-  flush_shadow(B, c, 0, kend, nr, valid);
+  unsigned sbase, q;
+  wave_append2(&B.q_count[1], valid ? (unsigned)nr : 0u, emit ? 1u : 0u, sbase, q);
+  if (valid) flush_shadow(B, c, kend, nr, sbase, traced);
+  if (emit) {
+    B.q_rays[1][q] = seg;
+    B.q_owner[1][q] = (int)c;
+  }
 }
 
 // Sums light li's unoccluded slot contributions in reference order:
@@ -839,40 +884,23 @@ __global__ void __launch_bounds__(256) k_resolve_primary(Batch B, RenderConst R,
   B.col[3 * c + 2] = B.col[3 * c + 2] + dl.b;
 }
 
-// First segment of sub-path isub: sample the primary BSDF (pathtracer.cc:169-187).
+// First segment of sub-paths isub >= 1 (sub-path 0 is fused into
+// k_shade_primary).
 __global__ void __launch_bounds__(256) k_path_start(DScene S, Batch B, RenderConst R, long long nc, int isub) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = c < nc;
   bool emit = false;
   yk_ray r;
-  if (valid) {
-    B.pstate[c] = 0;
-    if (B.prim_hit[c] & PH_DIFFUSE) {
-      const yk_hit h = B.p_hits[c];
-      const yk_ray pr = B.p_rays[c];
-      const v3 from = V3(pr.from[0], pr.from[1], pr.from[2]), dir = V3(pr.dir[0], pr.dir[1], pr.dir[2]);
-      const SurfPt sp = make_surface(S, from, dir, h);
-      const DMat& M = c_mats[sp.mat];
-      const unsigned s = (unsigned)(c % R.spp);
-      const unsigned offs = (unsigned)(R.nsub * (int)s) + B.soffs[c] + (unsigned)isub;
-      const float s1 = ri_vdc(offs, 0u);
-      const float s2 = (float)scr_halton(2, offs);
-      float pdf, W = B.wlast[c];
-      bool ok;
-      v3 pdir = V3(0.f, 0.f, 0.f);
-      c3 scol =
-          mat_sample(M, sp, vneg(dir), pdir, s1, s2, BSDF_DIFFUSE | BSDF_REFLECT | BSDF_TRANSMIT, pdf, W, ok);
-      B.wlast[c] = W;
-      scol = cscale(W, scol);
-      B.thr[3 * c] = scol.r;
-      B.thr[3 * c + 1] = scol.g;
-      B.thr[3 * c + 2] = scol.b;
-      put_ray(r, sp.P, pdir, YK_MIN_RAYDIST, -1.0f);
-      emit = true;
-      B.pstate[c] = PS_ALIVE;
-    }
+  if (valid && (B.prim_hit[c] & PH_DIFFUSE)) {
+    const yk_hit h = B.p_hits[c];
+    const yk_ray pr = B.p_rays[c];
+    const v3 from = V3(pr.from[0], pr.from[1], pr.from[2]), dir = V3(pr.dir[0], pr.dir[1], pr.dir[2]);
+    const SurfPt sp = make_surface(S, from, dir, h);
+    r = path_first_segment(B, R, c, sp, c_mats[sp.mat], dir, isub);
+    emit = true;
   }
-  const unsigned q = wave_append(&B.q_count[1], emit ? 1u : 0u);
+  unsigned sbase, q;
+  wave_append2(&B.q_count[1], 0u, emit ? 1u : 0u, sbase, q);
   if (emit) {
     B.q_rays[1][q] = r;
     B.q_owner[1][q] = (int)c;
@@ -889,6 +917,7 @@ __global__ void __launch_bounds__(256) k_shade_bounce(DScene S, Batch B, RenderC
   const bool valid = qi < nq;
   const long long c = valid ? B.q_owner[qin][qi] : 0;
   int nr = 0, kend = 0;
+  unsigned long long traced = 0;
   bool emit_next = false;
   yk_ray nxt;
   if (valid) {
@@ -911,7 +940,7 @@ __global__ void __launch_bounds__(256) k_shade_bounce(DScene S, Batch B, RenderC
         hal_start(h2, 2u, (unsigned)((int)offs - 1));
         int lnum = (int)(hal_next(h2) * (float)R.nlights);
         if (lnum > R.nlights - 1) lnum = R.nlights - 1;
-        nr = gen_light(B, c, 0, lnum, sp, pwo, s, B.soffs[c], (unsigned)lnum);
+        nr = gen_light(B, c, 0, lnum, sp, pwo, s, B.soffs[c], (unsigned)lnum, traced);
         kend = 2 * c_lights[lnum].samples;
         B.lsel[c] = lnum;
         ps |= PS_EST;
@@ -942,8 +971,9 @@ __global__ void __launch_bounds__(256) k_shade_bounce(DScene S, Batch B, RenderC
       B.pstate[c] = ps;
     }
   }
-  flush_shadow(B, c, 0, kend, nr, valid);
-  const unsigned qn = wave_append(&B.q_count[qin ^ 1], emit_next ? 1u : 0u);
+  unsigned sbase, qn;
+  wave_append2(&B.q_count[qin ^ 1], valid ? (unsigned)nr : 0u, emit_next ? 1u : 0u, sbase, qn);
+  if (valid) flush_shadow(B, c, kend, nr, sbase, traced);
   if (emit_next) {
     B.q_rays[qin ^ 1][qn] = nxt;
     B.q_owner[qin ^ 1][qn] = (int)c;
@@ -1151,7 +1181,8 @@ struct yk_device {
   DBuf<unsigned long long> counters;
   DBuf<uint2> ovf;  // traversal stack overflow (entries deeper than the LDS ring)
   // batch buffers (grown on demand, kept across renders)
-  DBuf<unsigned> soffs, qcount, s_idx;
+  DBuf<unsigned> soffs, s_idx;
+  DBuf<unsigned long long> qcount;
   DBuf<float> col, alpha, thr, pathcol, scol_next, wlast, emit_b, sl_contrib;
   DBuf<int> prim_hit, pstate, lsel, qo0, qo1, tile_base;
   DBuf<int4> tiles;
@@ -1316,11 +1347,12 @@ void launch_trace(yk_device* d, const yk_ray* rays, const unsigned* idx, long lo
   grid = std::min<long long>(grid, (n + 63) / 64);
   if (grid < 1) grid = 1;
   const int D = stack_depth(d);
-  if (D > kStackLds) d->ovf.ensure((size_t)(D - kStackLds) * (size_t)grid * 64);
+  const int ovf_depth = std::max(1, D - kStackLds);
+  d->ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
   HIPCHK(hipEventRecord(d->ev0, d->stream));
   hipLaunchKernelGGL(CLOSEST ? k_trace_closest : k_trace_shadow, dim3((unsigned)grid), dim3(64), 0, d->stream, d->S, rays,
                      idx, n, hits, occ,
-                     ctr, ctr + 1, d->ovf.p, refill_min());
+                     ctr, ctr + 1, d->ovf.p, ovf_depth, refill_min());
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(d->ev1, d->stream));
   unsigned long long h[4];
@@ -1585,7 +1617,7 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   d->qr1.ensure(maxc);
   d->qh0.ensure(maxc);
   d->qh1.ensure(maxc);
-  d->qcount.ensure(4);
+  d->qcount.ensure(2);
   d->s_rays.ensure(maxc * K);
   d->s_occl.ensure(maxc * K);
   d->s_idx.ensure(maxc * K);
@@ -1626,14 +1658,15 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   B.K = K;
   yk_stats local{};
   yk_stats* S = st ? st : &local;
-  unsigned qc[4];
+  unsigned long long qc[2];
   auto read_counts = [&]() {
     HIPCHK(hipMemcpyAsync(qc, d->qcount.p, sizeof qc, hipMemcpyDeviceToHost, d->stream));
     HIPCHK(hipStreamSynchronize(d->stream));
   };
-  auto trace_shadow_queue = [&]() {
+  // shadow rays appended by the launch that filled bounce queue b
+  auto trace_shadow_queue = [&](int b) {
     read_counts();
-    launch_trace<false>(d, B.s_rays, B.s_idx, qc[2], nullptr, B.s_occl, S);
+    launch_trace<false>(d, B.s_rays, B.s_idx, (long long)(qc[b] & 0xFFFFFFFFull), nullptr, B.s_occl, S);
   };
   for (size_t tb0 = 0; tb0 < owned.size(); tb0 += tiles_per_batch) {
     const size_t tb1 = std::min(owned.size(), tb0 + (size_t)tiles_per_batch);
@@ -1658,34 +1691,35 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
     HIPCHK(hipMemcpyAsync(d->tile_base.p, base.data(), base.size() * sizeof(int), hipMemcpyHostToDevice, d->stream));
     HIPCHK(hipStreamSynchronize(d->stream));  // host vectors die with this iteration
     TileList TL{d->tiles.p, d->tile_base.p, (int)tl.size()};
-    HIPCHK(hipMemsetAsync(d->qcount.p, 0, 4 * sizeof(unsigned), d->stream));
+    HIPCHK(hipMemsetAsync(d->qcount.p, 0, 2 * sizeof(unsigned long long), d->stream));
     hipLaunchKernelGGL(k_camera, dim3(grid_for(nc)), dim3(256), 0, d->stream, TL, B, R, nc);
     HIPCHK(hipGetLastError());
     launch_trace<true>(d, B.p_rays, nullptr, nc, B.p_hits, nullptr, S);
     hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(nc)), dim3(256), 0, d->stream, d->S, B, R, nc);
     HIPCHK(hipGetLastError());
-    trace_shadow_queue();
+    trace_shadow_queue(1);
     hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(nc)), dim3(256), 0, d->stream, B, R, nc);
     HIPCHK(hipGetLastError());
     if (p->integrator == YK_INTEGRATOR_PATH) {
       // sub-path index outermost: pathCol is shared across sub-paths and
       // accumulated in the reference's order (pathtracer.cc:164-298)
       for (int isub = 0; isub < R.nsub; ++isub) {
-        HIPCHK(hipMemsetAsync(d->qcount.p, 0, 4 * sizeof(unsigned), d->stream));
-        hipLaunchKernelGGL(k_path_start, dim3(grid_for(nc)), dim3(256), 0, d->stream, d->S, B, R, nc, isub);
-        HIPCHK(hipGetLastError());
+        if (isub > 0) {  // sub-path 0's first segment came out of k_shade_primary
+          HIPCHK(hipMemsetAsync(d->qcount.p, 0, 2 * sizeof(unsigned long long), d->stream));
+          hipLaunchKernelGGL(k_path_start, dim3(grid_for(nc)), dim3(256), 0, d->stream, d->S, B, R, nc, isub);
+          HIPCHK(hipGetLastError());
+        }
         int qin = 1;
         for (int depth = 1; depth <= R.bounces; ++depth) {
           read_counts();
-          const unsigned nq = qc[qin];
+          const unsigned nq = (unsigned)(qc[qin] >> 32);
           if (nq == 0) break;
           launch_trace<true>(d, B.q_rays[qin], nullptr, nq, B.q_hits[qin], nullptr, S);
-          HIPCHK(hipMemsetAsync(d->qcount.p + 2, 0, sizeof(unsigned), d->stream));
-          HIPCHK(hipMemsetAsync(d->qcount.p + (qin ^ 1), 0, sizeof(unsigned), d->stream));
+          HIPCHK(hipMemsetAsync(d->qcount.p + (qin ^ 1), 0, sizeof(unsigned long long), d->stream));
           hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(nq)), dim3(256), 0, d->stream, d->S, B, R, (long long)nq,
                              depth, isub, qin);
           HIPCHK(hipGetLastError());
-          trace_shadow_queue();
+          trace_shadow_queue(qin ^ 1);
           hipLaunchKernelGGL(k_resolve_bounce, dim3(grid_for(nq)), dim3(256), 0, d->stream, B, R, (long long)nq, depth,
                              qin);
           HIPCHK(hipGetLastError());

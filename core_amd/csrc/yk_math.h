@@ -57,18 +57,35 @@ struct QmcTables {
 extern __constant__ QmcTables c_qmc;
 extern __constant__ int c_faure[5600];
 
-// scrHalton, scr_halton.h:47-69
+// scrHalton, scr_halton.h:47-69. The digit recurrence (dn *= f; n = (unsigned)dn)
+// does not depend on the table, so digits are produced four at a time and
+// their Faure-table loads issued together; the sum keeps the reference's
+// order and operands, so the result is bit-identical to the plain loop.
 __device__ __forceinline__ double scr_halton(int dim, unsigned n) {
   double value = 0.0;
   const unsigned base = (unsigned)c_qmc.prims[dim];
   const int off = c_qmc.off[dim];
-  double f, factor, dn = (double)n;
-  f = factor = c_qmc.invprims[dim];
+  const double f = c_qmc.invprims[dim];
+  double factor = f, dn = (double)n;
   while (n > 0) {
-    value += (double)c_faure[off + (int)(n % base)] * factor;
+    unsigned u[4];
+    u[0] = n;
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      dn *= f;
+      u[k] = (unsigned)dn;
+    }
+    int sig[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sig[k] = c_faure[off + (int)(u[k] > 0u ? u[k] % base : 0u)];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (u[k] > 0u) value += (double)sig[k] * factor;
+      factor *= f;
+    }
     dn *= f;
     n = (unsigned)dn;
-    factor *= f;
+    if (u[3] == 0u) n = 0u;
   }
   if (value > 1.0) value = 1.0;
   if (value < 1.0e-36) value = 1.0e-36;
