@@ -168,7 +168,11 @@ def main():
                    "tris": int(info.ntris), "width": p.width, "height": p.height, "spp": p.aa_samples,
                    "parallelism": f"tiles%{world}" if world > 1 else "single",
                    "closest_rays": int(w[0]), "shadow_rays": int(w[1]),
-                   "camera_samples": int(w[8])},
+                   "camera_samples": int(w[8]),
+                   "per_ray": {"closest_nodes": round(w[2] / max(w[0], 1), 2),
+                               "closest_tri_tests": round(w[3] / max(w[0], 1), 2),
+                               "shadow_nodes": round(w[4] / max(w[1], 1), 2),
+                               "shadow_tri_tests": round(w[5] / max(w[1], 1), 2)}},
         "roofline": roofline,
         "cpu_baseline": cpu,
     }

@@ -285,7 +285,7 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
 // packed with live rays until the queue drains. Stack: LDS, [depth][lane].
 // idx (optional): queue entry r is ray idx[r]; the result goes to the same
 // slot (used by the shadow queue, whose rays sit in per-sample slots).
-template <bool CLOSEST>
+template <bool CLOSEST, int NSEG>
 __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx,
                                            long long n, yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
                                            unsigned long long* __restrict__ work, unsigned long long* __restrict__ ctr,
@@ -297,28 +297,52 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   bool exhausted = false;
   Trav st;
   unsigned nnodes = 0, ntris = 0, nerr = 0;
-  // wave-private pool of ray indices [pool_next, pool_end): one atomic per
-  // kPoolChunk rays instead of one per refill (wave-uniform, scalar registers)
+  // Ray hand-out. The queue is cut into NSEG (1 or 8) contiguous segments, one per XCD:
+  // consecutive queue entries are spatially coherent (tile / pixel order), so
+  // the rays an XCD traces touch a compact part of the tree and its private
+  // 4 MB L2 keeps it. A wave takes kPoolChunk-ray chunks of its own XCD's
+  // segment (one atomic per chunk), then steals from the other segments.
+  // Pool bounds are wave-uniform (scalar registers).
   constexpr unsigned kPoolChunk = 64;
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+  constexpr unsigned kAll = (1u << NSEG) - 1u;
+  const unsigned seg_len = (unsigned)((n + NSEG - 1) / NSEG);
   unsigned pool_next = 0, pool_end = 0;
-  unsigned iters = 0;  // wave watchdog: a valid tree never gets near the cap
+  unsigned seg_done = 0;  // bit s: segment s has no chunks left
+  unsigned iters = 0;     // wave watchdog: a valid tree never gets near the cap
   for (;;) {
     const unsigned long long want = __ballot(rid < 0 && !exhausted);
     const unsigned long long act = __ballot(rid >= 0);
     if (want != 0ull && (act == 0ull || __popcll(want) >= refill_min)) {
       const unsigned cnt = (unsigned)__popcll(want);
       const unsigned avail = pool_end - pool_next;
-      unsigned chunk = pool_end;  // start of a newly grabbed chunk (if any)
-      if (avail < cnt) {
-        unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(work, (unsigned long long)kPoolChunk);
-        base = shfl_u64(base, 0);
-        chunk = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)min(base, (unsigned long long)0x7FFFFFFF));
+      unsigned cb = 0, ce = 0;  // newly grabbed chunk [cb, ce)
+      if (avail < cnt && seg_done != kAll) {
+        for (unsigned k = 0; k < (unsigned)NSEG; ++k) {
+          const unsigned sgi = (xcc + k) % (unsigned)NSEG;
+          if (seg_done & (1u << sgi)) continue;
+          const unsigned long long s0 = (unsigned long long)sgi * seg_len;
+          const unsigned long long s1 = min(s0 + seg_len, (unsigned long long)n);
+          unsigned long long base = 0;
+          if (lane == 0) base = atomicAdd(work + 16 * sgi, (unsigned long long)kPoolChunk);
+          base = s0 + shfl_u64(base, 0);
+          if (base < s1) {
+            cb = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)base);
+            ce = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)min(base + kPoolChunk, s1));
+            break;
+          }
+          seg_done |= 1u << sgi;
+        }
       }
       if (rid < 0 && !exhausted) {
         const unsigned rank = (unsigned)__popcll(want & ((1ull << lane) - 1ull));
-        const unsigned q = (rank < avail) ? pool_next + rank : chunk + (rank - avail);
-        if ((long long)q < n) {
+        long long q = -1;
+        if (rank < avail) q = pool_next + rank;
+        else if (rank - avail < ce - cb) q = cb + (rank - avail);
+        if (q < 0) {
+          exhausted = (seg_done == kAll);  // nothing left anywhere; else retry at the next refill
+        } else {
           const int r = idx ? (int)idx[q] : (int)q;
           const yk_ray ray = rays[r];
           if (trav_begin<CLOSEST>(S, st, ray)) {
@@ -328,13 +352,12 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
           } else {
             occl[r] = 0;
           }
-        } else {
-          exhausted = true;
         }
       }
       if (avail < cnt) {
-        pool_next = chunk + (cnt - avail);
-        pool_end = chunk + kPoolChunk;
+        const unsigned take = min(cnt - avail, ce - cb);
+        pool_next = cb + take;
+        pool_end = ce;
       } else {
         pool_next += cnt;
       }
@@ -382,9 +405,12 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   if (nerr) atomicAdd(&ctr[2], (unsigned long long)nerr);
 }
 
-// Occupancy targets (measured on MI355X, 1M-tri scene): the closest-hit
-// kernel runs best at 6 waves/SIMD, the any-hit kernel at 7 (its state is
-// smaller); with an 8-deep LDS ring (4 KB per wave) registers set the limit.
+// Occupancy targets and ray hand-out (measured on MI355X, 1M-tri scene): the
+// closest-hit kernel runs best at 6 waves/SIMD with per-XCD ray segments
+// (+12% from L2 locality), the any-hit kernel at 7 waves with one shared
+// segment (its smaller state leaves room for the extra waves, which the
+// segment logic's registers would take away); with an 8-deep LDS ring (4 KB
+// per wave) registers set the limit.
 #ifndef YK_CLOSEST_WAVES
 #define YK_CLOSEST_WAVES 6
 #endif
@@ -395,13 +421,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOS
 k_trace_closest(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, long long n,
                 yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                 unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<true>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+  trace_body<true, 8>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
 k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, long long n,
                yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+  trace_body<false, 1>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 
 // ============================================================ shading
@@ -1334,8 +1360,11 @@ void launch_trace(yk_device* d, const yk_ray* rays, const unsigned* idx, long lo
                   yk_stats* st) {
   if (n <= 0) return;
   if (n > 0x7FFFFFFFll - (1ll << 24)) throw std::invalid_argument("ray batch too large (max ~2^31 rays per call)");
-  unsigned long long* ctr = d->counters.p;
-  HIPCHK(hipMemsetAsync(ctr, 0, 4 * sizeof(unsigned long long), d->stream));
+  // [0,128): 8 per-XCD segment counters, one per 128-B line; [128,131): node /
+  // triangle-test / error counters
+  unsigned long long* work = d->counters.p;
+  unsigned long long* ctr = d->counters.p + 128;
+  HIPCHK(hipMemsetAsync(work, 0, 132 * sizeof(unsigned long long), d->stream));
   // persistent grid: as many waves as the chip keeps resident (VGPR/LDS bound)
   static int per_cu[2] = {0, 0};
   if (!per_cu[CLOSEST]) {
@@ -1352,26 +1381,26 @@ void launch_trace(yk_device* d, const yk_ray* rays, const unsigned* idx, long lo
   HIPCHK(hipEventRecord(d->ev0, d->stream));
   hipLaunchKernelGGL(CLOSEST ? k_trace_closest : k_trace_shadow, dim3((unsigned)grid), dim3(64), 0, d->stream, d->S, rays,
                      idx, n, hits, occ,
-                     ctr, ctr + 1, d->ovf.p, ovf_depth, refill_min());
+                     work, ctr, d->ovf.p, ovf_depth, refill_min());
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(d->ev1, d->stream));
-  unsigned long long h[4];
+  unsigned long long h[3];
   HIPCHK(hipMemcpyAsync(h, ctr, sizeof h, hipMemcpyDeviceToHost, d->stream));
   HIPCHK(hipStreamSynchronize(d->stream));
-  if (h[3]) throw std::runtime_error("kd-tree traversal watchdog fired on " + std::to_string(h[3]) + " rays");
+  if (h[2]) throw std::runtime_error("kd-tree traversal watchdog fired on " + std::to_string(h[2]) + " rays");
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, d->ev0, d->ev1));
   if (!st) return;
   if (CLOSEST) {
     st->closest_rays += (uint64_t)n;
-    st->closest_nodes += h[1];
-    st->closest_tris += h[2];
+    st->closest_nodes += h[0];
+    st->closest_tris += h[1];
     st->ms_closest += ms;
     st->closest_launches++;
   } else {
     st->shadow_rays += (uint64_t)n;
-    st->shadow_nodes += h[1];
-    st->shadow_tris += h[2];
+    st->shadow_nodes += h[0];
+    st->shadow_tris += h[1];
     st->ms_shadow += ms;
     st->shadow_launches++;
   }
@@ -1400,7 +1429,7 @@ int yk_device_open(int32_t ordinal, yk_device** out) {
   HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
   HIPCHK(hipEventCreate(&d->ev0));
   HIPCHK(hipEventCreate(&d->ev1));
-  d->counters.ensure(8);
+  d->counters.ensure(136);
   upload_qmc();
   *out = d;
   return YK_OK;
