@@ -16,6 +16,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1191,22 +1194,14 @@ struct DBuf {
 
 }  // namespace
 
-struct yk_device {
-  int ordinal = 0;
-  int cus = 0;
+// One batch pipeline: a stream with its own queues, counters and scratch.
+// Two pipes run alternate batches so one batch's kernels fill the other's
+// launch tails; film gathers stay in batch order through events.
+struct Pipe {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool uploaded = false;
-  // scene
-  DBuf<float4> tris, ng;
-  DBuf<uint2> nodes;
-  DBuf<uint32_t> leaf;
-  DScene S{};
-  int ntris = 0, max_depth = 0, nlights = 0, sum_light_samples = 0;
-  // traversal work counter + node/tri counters
-  DBuf<unsigned long long> counters;
-  DBuf<uint2> ovf;  // traversal stack overflow (entries deeper than the LDS ring)
-  // batch buffers (grown on demand, kept across renders)
+  DBuf<unsigned long long> counters;  // per-XCD ray segments + work counters
+  DBuf<uint2> ovf;                    // traversal stack overflow (entries deeper than the LDS ring)
   DBuf<unsigned> soffs, s_idx;
   DBuf<unsigned long long> qcount;
   DBuf<float> col, alpha, thr, pathcol, scol_next, wlast, emit_b, sl_contrib;
@@ -1217,10 +1212,99 @@ struct yk_device {
   DBuf<uint8_t> sl_flags, s_occl;
   DBuf<float4> samples;
   DBuf<float2> sxy;
-  ~yk_device() {
+  void create() {
+    HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&ev0));
+    HIPCHK(hipEventCreate(&ev1));
+    counters.ensure(136);
+  }
+  ~Pipe() {
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (stream) (void)hipStreamDestroy(stream);
+  }
+  Batch bind(long long maxc, int K, int tiles_per_batch) {
+    soffs.ensure(maxc);
+    col.ensure(3 * maxc);
+    alpha.ensure(maxc);
+    prim_hit.ensure(maxc);
+    p_rays.ensure(maxc);
+    p_hits.ensure(maxc);
+    thr.ensure(3 * maxc);
+    pathcol.ensure(3 * maxc);
+    scol_next.ensure(3 * maxc);
+    wlast.ensure(maxc);
+    emit_b.ensure(3 * maxc);
+    pstate.ensure(maxc);
+    lsel.ensure(maxc);
+    qo0.ensure(maxc);
+    qo1.ensure(maxc);
+    qr0.ensure(maxc);
+    qr1.ensure(maxc);
+    qh0.ensure(maxc);
+    qh1.ensure(maxc);
+    qcount.ensure(2);
+    s_rays.ensure(maxc * K);
+    s_occl.ensure(maxc * K);
+    s_idx.ensure(maxc * K);
+    sl_contrib.ensure(3 * maxc * K);
+    sl_flags.ensure(maxc * K);
+    samples.ensure(maxc);
+    sxy.ensure(maxc);
+    tiles.ensure(tiles_per_batch);
+    tile_base.ensure(tiles_per_batch + 1);
+    Batch B{};
+    B.prim_hit = prim_hit.p;
+    B.soffs = soffs.p;
+    B.col = col.p;
+    B.alpha = alpha.p;
+    B.p_rays = p_rays.p;
+    B.p_hits = p_hits.p;
+    B.thr = thr.p;
+    B.pathcol = pathcol.p;
+    B.scol_next = scol_next.p;
+    B.wlast = wlast.p;
+    B.emit_b = emit_b.p;
+    B.pstate = pstate.p;
+    B.lsel = lsel.p;
+    B.q_owner[0] = qo0.p;
+    B.q_owner[1] = qo1.p;
+    B.q_rays[0] = qr0.p;
+    B.q_rays[1] = qr1.p;
+    B.q_hits[0] = qh0.p;
+    B.q_hits[1] = qh1.p;
+    B.q_count = qcount.p;
+    B.s_rays = s_rays.p;
+    B.s_occl = s_occl.p;
+    B.s_idx = s_idx.p;
+    B.sl_contrib = sl_contrib.p;
+    B.sl_flags = sl_flags.p;
+    B.samples = samples.p;
+    B.sxy = sxy.p;
+    B.K = K;
+    return B;
+  }
+};
+
+constexpr int kPipes = 2;
+
+struct yk_device {
+  int ordinal = 0;
+  int cus = 0;
+  int per_cu[2] = {1, 1};  // resident trace waves per CU: [0] any-hit, [1] closest
+  hipStream_t stream = nullptr;  // = pipe[0].stream (ray queries, film resolve)
+  bool uploaded = false;
+  // scene
+  DBuf<float4> tris, ng;
+  DBuf<uint2> nodes;
+  DBuf<uint32_t> leaf;
+  DScene S{};
+  int ntris = 0, max_depth = 0, nlights = 0, sum_light_samples = 0;
+  Pipe pipe[kPipes];
+  hipEvent_t gather_ev[kPipes] = {nullptr, nullptr};
+  ~yk_device() {
+    for (auto& e : gather_ev)
+      if (e) (void)hipEventDestroy(e);
   }
 };
 
@@ -1356,40 +1440,33 @@ int refill_min() {
 }
 
 template <bool CLOSEST>
-void launch_trace(yk_device* d, const yk_ray* rays, const unsigned* idx, long long n, yk_hit* hits, uint8_t* occ,
-                  yk_stats* st) {
+void launch_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* idx, long long n, yk_hit* hits,
+                  uint8_t* occ, yk_stats* st) {
   if (n <= 0) return;
   if (n > 0x7FFFFFFFll - (1ll << 24)) throw std::invalid_argument("ray batch too large (max ~2^31 rays per call)");
   // [0,128): 8 per-XCD segment counters, one per 128-B line; [128,131): node /
   // triangle-test / error counters
-  unsigned long long* work = d->counters.p;
-  unsigned long long* ctr = d->counters.p + 128;
-  HIPCHK(hipMemsetAsync(work, 0, 132 * sizeof(unsigned long long), d->stream));
+  unsigned long long* work = P.counters.p;
+  unsigned long long* ctr = P.counters.p + 128;
+  HIPCHK(hipMemsetAsync(work, 0, 132 * sizeof(unsigned long long), P.stream));
   // persistent grid: as many waves as the chip keeps resident (VGPR/LDS bound)
-  static int per_cu[2] = {0, 0};
-  if (!per_cu[CLOSEST]) {
-    int blocks = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, CLOSEST ? k_trace_closest : k_trace_shadow, 64, 0));
-    per_cu[CLOSEST] = std::max(1, blocks);
-  }
-  long long grid = (long long)d->cus * per_cu[CLOSEST];
+  long long grid = (long long)d->cus * d->per_cu[CLOSEST];
   grid = std::min<long long>(grid, (n + 63) / 64);
   if (grid < 1) grid = 1;
   const int D = stack_depth(d);
   const int ovf_depth = std::max(1, D - kStackLds);
-  d->ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
-  HIPCHK(hipEventRecord(d->ev0, d->stream));
-  hipLaunchKernelGGL(CLOSEST ? k_trace_closest : k_trace_shadow, dim3((unsigned)grid), dim3(64), 0, d->stream, d->S, rays,
-                     idx, n, hits, occ,
-                     work, ctr, d->ovf.p, ovf_depth, refill_min());
+  P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
+  HIPCHK(hipEventRecord(P.ev0, P.stream));
+  hipLaunchKernelGGL(CLOSEST ? k_trace_closest : k_trace_shadow, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays,
+                     idx, n, hits, occ, work, ctr, P.ovf.p, ovf_depth, refill_min());
   HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(d->ev1, d->stream));
+  HIPCHK(hipEventRecord(P.ev1, P.stream));
   unsigned long long h[3];
-  HIPCHK(hipMemcpyAsync(h, ctr, sizeof h, hipMemcpyDeviceToHost, d->stream));
-  HIPCHK(hipStreamSynchronize(d->stream));
+  HIPCHK(hipMemcpyAsync(h, ctr, sizeof h, hipMemcpyDeviceToHost, P.stream));
+  HIPCHK(hipStreamSynchronize(P.stream));
   if (h[2]) throw std::runtime_error("kd-tree traversal watchdog fired on " + std::to_string(h[2]) + " rays");
   float ms = 0.f;
-  HIPCHK(hipEventElapsedTime(&ms, d->ev0, d->ev1));
+  HIPCHK(hipEventElapsedTime(&ms, P.ev0, P.ev1));
   if (!st) return;
   if (CLOSEST) {
     st->closest_rays += (uint64_t)n;
@@ -1426,10 +1503,14 @@ int yk_device_open(int32_t ordinal, yk_device** out) {
   yk_device* d = new yk_device();
   d->ordinal = ordinal;
   d->cus = prop.multiProcessorCount;
-  HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
-  HIPCHK(hipEventCreate(&d->ev0));
-  HIPCHK(hipEventCreate(&d->ev1));
-  d->counters.ensure(136);
+  for (auto& P : d->pipe) P.create();
+  for (auto& e : d->gather_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  d->stream = d->pipe[0].stream;
+  int blocks = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow, 64, 0));
+  d->per_cu[0] = std::max(1, blocks);
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_closest, 64, 0));
+  d->per_cu[1] = std::max(1, blocks);
   upload_qmc();
   *out = d;
   return YK_OK;
@@ -1522,7 +1603,7 @@ int yk_trace_closest(yk_device* d, const yk_ray* d_rays, int64_t n, yk_hit* d_hi
   YK_GUARD_BEGIN
   HIPCHK(hipSetDevice(d->ordinal));
   yk_stats local{};
-  launch_trace<true>(d, d_rays, nullptr, n, d_hits, nullptr, st ? st : &local);
+  launch_trace<true>(d, d->pipe[0], d_rays, nullptr, n, d_hits, nullptr, st ? st : &local);
   return YK_OK;
   YK_GUARD_END
 }
@@ -1533,7 +1614,7 @@ int yk_trace_shadow(yk_device* d, const yk_ray* d_rays, int64_t n, uint8_t* d_oc
   YK_GUARD_BEGIN
   HIPCHK(hipSetDevice(d->ordinal));
   yk_stats local{};
-  launch_trace<false>(d, d_rays, nullptr, n, nullptr, d_occ, st ? st : &local);
+  launch_trace<false>(d, d->pipe[0], d_rays, nullptr, n, nullptr, d_occ, st ? st : &local);
   return YK_OK;
   YK_GUARD_END
 }
@@ -1627,152 +1708,159 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   const long long tile_samples = (long long)F.tile * F.tile * spp;
   const int tiles_per_batch = (int)std::max<long long>(1, target / tile_samples);
   const long long maxc = (long long)tiles_per_batch * tile_samples;
-  d->soffs.ensure(maxc);
-  d->col.ensure(3 * maxc);
-  d->alpha.ensure(maxc);
-  d->prim_hit.ensure(maxc);
-  d->p_rays.ensure(maxc);
-  d->p_hits.ensure(maxc);
-  d->thr.ensure(3 * maxc);
-  d->pathcol.ensure(3 * maxc);
-  d->scol_next.ensure(3 * maxc);
-  d->wlast.ensure(maxc);
-  d->emit_b.ensure(3 * maxc);
-  d->pstate.ensure(maxc);
-  d->lsel.ensure(maxc);
-  d->qo0.ensure(maxc);
-  d->qo1.ensure(maxc);
-  d->qr0.ensure(maxc);
-  d->qr1.ensure(maxc);
-  d->qh0.ensure(maxc);
-  d->qh1.ensure(maxc);
-  d->qcount.ensure(2);
-  d->s_rays.ensure(maxc * K);
-  d->s_occl.ensure(maxc * K);
-  d->s_idx.ensure(maxc * K);
-  d->sl_contrib.ensure(3 * maxc * K);
-  d->sl_flags.ensure(maxc * K);
-  d->samples.ensure(maxc);
-  d->sxy.ensure(maxc);
-  d->tiles.ensure(tiles_per_batch);
-  d->tile_base.ensure(tiles_per_batch + 1);
-  Batch B{};
-  B.prim_hit = d->prim_hit.p;
-  B.soffs = d->soffs.p;
-  B.col = d->col.p;
-  B.alpha = d->alpha.p;
-  B.p_rays = d->p_rays.p;
-  B.p_hits = d->p_hits.p;
-  B.thr = d->thr.p;
-  B.pathcol = d->pathcol.p;
-  B.scol_next = d->scol_next.p;
-  B.wlast = d->wlast.p;
-  B.emit_b = d->emit_b.p;
-  B.pstate = d->pstate.p;
-  B.lsel = d->lsel.p;
-  B.q_owner[0] = d->qo0.p;
-  B.q_owner[1] = d->qo1.p;
-  B.q_rays[0] = d->qr0.p;
-  B.q_rays[1] = d->qr1.p;
-  B.q_hits[0] = d->qh0.p;
-  B.q_hits[1] = d->qh1.p;
-  B.q_count = d->qcount.p;
-  B.s_rays = d->s_rays.p;
-  B.s_occl = d->s_occl.p;
-  B.s_idx = d->s_idx.p;
-  B.sl_contrib = d->sl_contrib.p;
-  B.sl_flags = d->sl_flags.p;
-  B.samples = d->samples.p;
-  B.sxy = d->sxy.p;
-  B.K = K;
+  const int nbatch = (int)((owned.size() + tiles_per_batch - 1) / tiles_per_batch);
+  const int npipes = std::min(kPipes, std::max(1, nbatch));
+
+  // film gathers must run in batch order: batch b waits (on the host) until
+  // batch b-1's gather is enqueued, then (on its stream) for that gather's event
+  std::mutex mu;
+  std::condition_variable cv;
+  int gathers_enqueued = 0;
+  std::string err;
+  int err_code = YK_OK;
+  yk_stats pstats[kPipes] = {};
+
+  auto run_pipe = [&](int pi) {
+    Pipe& P = d->pipe[pi];
+    yk_stats* S = &pstats[pi];
+    try {
+      HIPCHK(hipSetDevice(d->ordinal));
+      Batch B = P.bind(maxc, K, tiles_per_batch);
+      unsigned long long qc[2];
+      auto read_counts = [&]() {
+        HIPCHK(hipMemcpyAsync(qc, P.qcount.p, sizeof qc, hipMemcpyDeviceToHost, P.stream));
+        HIPCHK(hipStreamSynchronize(P.stream));
+      };
+      // shadow rays appended by the launch that filled bounce queue b
+      auto trace_shadow_queue = [&](int b) {
+        read_counts();
+        launch_trace<false>(d, P, B.s_rays, B.s_idx, (long long)(qc[b] & 0xFFFFFFFFull), nullptr, B.s_occl, S);
+      };
+      for (int bi = pi; bi < nbatch; bi += npipes) {
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          if (err_code != YK_OK) return;
+        }
+        const size_t tb0 = (size_t)bi * tiles_per_batch;
+        const size_t tb1 = std::min(owned.size(), tb0 + (size_t)tiles_per_batch);
+        std::vector<int4> tl;
+        std::vector<int> base;
+        long long nc = 0;
+        int rx0 = 1 << 30, ry0 = 1 << 30, rx1 = -(1 << 30), ry1 = -(1 << 30);
+        for (size_t k = tb0; k < tb1; ++k) {
+          const int t = owned[k];
+          const int X = F.cx0 + (t % F.ntx) * F.tile, Y = F.cy0 + (t / F.ntx) * F.tile;
+          const int W = std::min(F.tile, F.cx1 - X), H = std::min(F.tile, F.cy1 - Y);
+          tl.push_back(make_int4(X, Y, W, H));
+          base.push_back((int)nc);
+          nc += (long long)W * H * spp;
+          rx0 = std::min(rx0, X);
+          ry0 = std::min(ry0, Y);
+          rx1 = std::max(rx1, X + W);
+          ry1 = std::max(ry1, Y + H);
+        }
+        base.push_back((int)nc);
+        HIPCHK(hipMemcpyAsync(P.tiles.p, tl.data(), tl.size() * sizeof(int4), hipMemcpyHostToDevice, P.stream));
+        HIPCHK(hipMemcpyAsync(P.tile_base.p, base.data(), base.size() * sizeof(int), hipMemcpyHostToDevice, P.stream));
+        HIPCHK(hipStreamSynchronize(P.stream));  // host vectors die with this iteration
+        TileList TL{P.tiles.p, P.tile_base.p, (int)tl.size()};
+        HIPCHK(hipMemsetAsync(P.qcount.p, 0, 2 * sizeof(unsigned long long), P.stream));
+        hipLaunchKernelGGL(k_camera, dim3(grid_for(nc)), dim3(256), 0, P.stream, TL, B, R, nc);
+        HIPCHK(hipGetLastError());
+        launch_trace<true>(d, P, B.p_rays, nullptr, nc, B.p_hits, nullptr, S);
+        hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, d->S, B, R, nc);
+        HIPCHK(hipGetLastError());
+        trace_shadow_queue(1);
+        hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
+        HIPCHK(hipGetLastError());
+        if (p->integrator == YK_INTEGRATOR_PATH) {
+          // sub-path index outermost: pathCol is shared across sub-paths and
+          // accumulated in the reference's order (pathtracer.cc:164-298)
+          for (int isub = 0; isub < R.nsub; ++isub) {
+            if (isub > 0) {  // sub-path 0's first segment came out of k_shade_primary
+              HIPCHK(hipMemsetAsync(P.qcount.p, 0, 2 * sizeof(unsigned long long), P.stream));
+              hipLaunchKernelGGL(k_path_start, dim3(grid_for(nc)), dim3(256), 0, P.stream, d->S, B, R, nc, isub);
+              HIPCHK(hipGetLastError());
+            }
+            int qin = 1;
+            for (int depth = 1; depth <= R.bounces; ++depth) {
+              read_counts();
+              const unsigned nq = (unsigned)(qc[qin] >> 32);
+              if (nq == 0) break;
+              launch_trace<true>(d, P, B.q_rays[qin], nullptr, nq, B.q_hits[qin], nullptr, S);
+              HIPCHK(hipMemsetAsync(P.qcount.p + (qin ^ 1), 0, sizeof(unsigned long long), P.stream));
+              hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(nq)), dim3(256), 0, P.stream, d->S, B, R,
+                                 (long long)nq, depth, isub, qin);
+              HIPCHK(hipGetLastError());
+              trace_shadow_queue(qin ^ 1);
+              hipLaunchKernelGGL(k_resolve_bounce, dim3(grid_for(nq)), dim3(256), 0, P.stream, B, R, (long long)nq,
+                                 depth, qin);
+              HIPCHK(hipGetLastError());
+              qin ^= 1;
+            }
+          }
+        }
+        hipLaunchKernelGGL(k_finish, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
+        HIPCHK(hipGetLastError());
+        // film: targets = batch rect grown by the filter window, after batch bi-1's gather
+        {
+          std::unique_lock<std::mutex> lk(mu);
+          cv.wait(lk, [&] { return gathers_enqueued == bi || err_code != YK_OK; });
+          if (err_code != YK_OK) return;
+        }
+        if (bi > 0) HIPCHK(hipStreamWaitEvent(P.stream, d->gather_ev[(bi - 1) % kPipes], 0));
+        FilmConst Fb = F;
+        Fb.tb0 = (int)tb0;
+        Fb.tb1 = (int)tb1;
+        const int gx0 = std::max(F.cx0, rx0 + F.olo_x), gy0 = std::max(F.cy0, ry0 + F.olo_y);
+        const int gx1 = std::min(F.cx1, rx1 + F.ohi_x), gy1 = std::min(F.cy1, ry1 + F.ohi_y);
+        const int gw = gx1 - gx0, gh = gy1 - gy0;
+        if (gw > 0 && gh > 0) {
+          hipLaunchKernelGGL(k_film_gather, dim3(grid_for((long long)gw * gh)), dim3(256), 0, P.stream, Fb,
+                             B.samples, B.sxy, P.tile_base.p, d_film, gx0, gy0, gw, gh);
+          HIPCHK(hipGetLastError());
+        }
+        HIPCHK(hipEventRecord(d->gather_ev[bi % kPipes], P.stream));
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          gathers_enqueued = bi + 1;
+        }
+        cv.notify_all();
+        S->camera_samples += (uint64_t)nc;
+        // the pipe's buffers are reused by its next batch: its stream keeps
+        // the order, no host wait needed
+      }
+      HIPCHK(hipStreamSynchronize(P.stream));
+    } catch (const std::exception& e) {
+      std::lock_guard<std::mutex> lk(mu);
+      if (err_code == YK_OK) {
+        err_code = dynamic_cast<const std::invalid_argument*>(&e) ? YK_ERR_ARG : YK_ERR_HIP;
+        err = e.what();
+      }
+      cv.notify_all();
+    }
+  };
+  std::vector<std::thread> workers;
+  for (int pi = 1; pi < npipes; ++pi) workers.emplace_back(run_pipe, pi);
+  run_pipe(0);
+  for (auto& w : workers) w.join();
+  if (err_code != YK_OK) return set_error(err_code, err);
   yk_stats local{};
   yk_stats* S = st ? st : &local;
-  unsigned long long qc[2];
-  auto read_counts = [&]() {
-    HIPCHK(hipMemcpyAsync(qc, d->qcount.p, sizeof qc, hipMemcpyDeviceToHost, d->stream));
-    HIPCHK(hipStreamSynchronize(d->stream));
-  };
-  // shadow rays appended by the launch that filled bounce queue b
-  auto trace_shadow_queue = [&](int b) {
-    read_counts();
-    launch_trace<false>(d, B.s_rays, B.s_idx, (long long)(qc[b] & 0xFFFFFFFFull), nullptr, B.s_occl, S);
-  };
-  for (size_t tb0 = 0; tb0 < owned.size(); tb0 += tiles_per_batch) {
-    const size_t tb1 = std::min(owned.size(), tb0 + (size_t)tiles_per_batch);
-    std::vector<int4> tl;
-    std::vector<int> base;
-    long long nc = 0;
-    int rx0 = 1 << 30, ry0 = 1 << 30, rx1 = -(1 << 30), ry1 = -(1 << 30);
-    for (size_t k = tb0; k < tb1; ++k) {
-      const int t = owned[k];
-      const int X = F.cx0 + (t % F.ntx) * F.tile, Y = F.cy0 + (t / F.ntx) * F.tile;
-      const int W = std::min(F.tile, F.cx1 - X), H = std::min(F.tile, F.cy1 - Y);
-      tl.push_back(make_int4(X, Y, W, H));
-      base.push_back((int)nc);
-      nc += (long long)W * H * spp;
-      rx0 = std::min(rx0, X);
-      ry0 = std::min(ry0, Y);
-      rx1 = std::max(rx1, X + W);
-      ry1 = std::max(ry1, Y + H);
-    }
-    base.push_back((int)nc);
-    HIPCHK(hipMemcpyAsync(d->tiles.p, tl.data(), tl.size() * sizeof(int4), hipMemcpyHostToDevice, d->stream));
-    HIPCHK(hipMemcpyAsync(d->tile_base.p, base.data(), base.size() * sizeof(int), hipMemcpyHostToDevice, d->stream));
-    HIPCHK(hipStreamSynchronize(d->stream));  // host vectors die with this iteration
-    TileList TL{d->tiles.p, d->tile_base.p, (int)tl.size()};
-    HIPCHK(hipMemsetAsync(d->qcount.p, 0, 2 * sizeof(unsigned long long), d->stream));
-    hipLaunchKernelGGL(k_camera, dim3(grid_for(nc)), dim3(256), 0, d->stream, TL, B, R, nc);
-    HIPCHK(hipGetLastError());
-    launch_trace<true>(d, B.p_rays, nullptr, nc, B.p_hits, nullptr, S);
-    hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(nc)), dim3(256), 0, d->stream, d->S, B, R, nc);
-    HIPCHK(hipGetLastError());
-    trace_shadow_queue(1);
-    hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(nc)), dim3(256), 0, d->stream, B, R, nc);
-    HIPCHK(hipGetLastError());
-    if (p->integrator == YK_INTEGRATOR_PATH) {
-      // sub-path index outermost: pathCol is shared across sub-paths and
-      // accumulated in the reference's order (pathtracer.cc:164-298)
-      for (int isub = 0; isub < R.nsub; ++isub) {
-        if (isub > 0) {  // sub-path 0's first segment came out of k_shade_primary
-          HIPCHK(hipMemsetAsync(d->qcount.p, 0, 2 * sizeof(unsigned long long), d->stream));
-          hipLaunchKernelGGL(k_path_start, dim3(grid_for(nc)), dim3(256), 0, d->stream, d->S, B, R, nc, isub);
-          HIPCHK(hipGetLastError());
-        }
-        int qin = 1;
-        for (int depth = 1; depth <= R.bounces; ++depth) {
-          read_counts();
-          const unsigned nq = (unsigned)(qc[qin] >> 32);
-          if (nq == 0) break;
-          launch_trace<true>(d, B.q_rays[qin], nullptr, nq, B.q_hits[qin], nullptr, S);
-          HIPCHK(hipMemsetAsync(d->qcount.p + (qin ^ 1), 0, sizeof(unsigned long long), d->stream));
-          hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(nq)), dim3(256), 0, d->stream, d->S, B, R, (long long)nq,
-                             depth, isub, qin);
-          HIPCHK(hipGetLastError());
-          trace_shadow_queue(qin ^ 1);
-          hipLaunchKernelGGL(k_resolve_bounce, dim3(grid_for(nq)), dim3(256), 0, d->stream, B, R, (long long)nq, depth,
-                             qin);
-          HIPCHK(hipGetLastError());
-          qin ^= 1;
-        }
-      }
-    }
-    hipLaunchKernelGGL(k_finish, dim3(grid_for(nc)), dim3(256), 0, d->stream, B, R, nc);
-    HIPCHK(hipGetLastError());
-    // film: targets = batch rect grown by the filter window
-    FilmConst Fb = F;
-    Fb.tb0 = (int)tb0;
-    Fb.tb1 = (int)tb1;
-    const int gx0 = std::max(F.cx0, rx0 + F.olo_x), gy0 = std::max(F.cy0, ry0 + F.olo_y);
-    const int gx1 = std::min(F.cx1, rx1 + F.ohi_x), gy1 = std::min(F.cy1, ry1 + F.ohi_y);
-    const int gw = gx1 - gx0, gh = gy1 - gy0;
-    if (gw > 0 && gh > 0) {
-      hipLaunchKernelGGL(k_film_gather, dim3(grid_for((long long)gw * gh)), dim3(256), 0, d->stream, Fb, B.samples,
-                         B.sxy, d->tile_base.p, d_film, gx0, gy0, gw, gh);
-      HIPCHK(hipGetLastError());
-    }
-    S->camera_samples += (uint64_t)nc;
+  for (int pi = 0; pi < npipes; ++pi) {
+    const yk_stats& q = pstats[pi];
+    S->closest_rays += q.closest_rays;
+    S->shadow_rays += q.shadow_rays;
+    S->closest_nodes += q.closest_nodes;
+    S->closest_tris += q.closest_tris;
+    S->shadow_nodes += q.shadow_nodes;
+    S->shadow_tris += q.shadow_tris;
+    S->camera_samples += q.camera_samples;
+    S->ms_closest += q.ms_closest;
+    S->ms_shadow += q.ms_shadow;
+    S->closest_launches += q.closest_launches;
+    S->shadow_launches += q.shadow_launches;
   }
-  HIPCHK(hipStreamSynchronize(d->stream));
   S->ms_total += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return YK_OK;
   YK_GUARD_END
