@@ -16,9 +16,6 @@
 
 #include <algorithm>
 #include <chrono>
-#include <condition_variable>
-#include <mutex>
-#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -288,13 +285,26 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
 // packed with live rays until the queue drains. Stack: LDS, [depth][lane].
 // idx (optional): queue entry r is ray idx[r]; the result goes to the same
 // slot (used by the shadow queue, whose rays sit in per-sample slots).
+// Number of rays of a launch: a host value, or a 32-bit field of a device
+// queue-count word (so launches need no host round trip).
+struct RayCount {
+  const unsigned long long* word;
+  int shift;
+  long long host;
+  __device__ __forceinline__ long long get() const {
+    return word ? (long long)((*word >> shift) & 0xFFFFFFFFull) : host;
+  }
+};
+
 template <bool CLOSEST, int NSEG>
 __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx,
-                                           long long n, yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
+                                           RayCount rc, yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
                                            unsigned long long* __restrict__ work, unsigned long long* __restrict__ ctr,
                                            uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
   __shared__ uint2 lds[kStackLds * 64];
   const int lane = threadIdx.x;
+  const long long n = __builtin_amdgcn_readfirstlane((int)rc.get());
+  if (blockIdx.x == 0 && lane == 0 && n > 0) atomicAdd(&ctr[3], (unsigned long long)n);  // rays traced
   const LaneStack stk{lds, ovf + (size_t)(blockIdx.x * 64u + (unsigned)lane) * (unsigned)ovf_depth, lane};
   int rid = -1;  // ray of this lane (host guarantees n < 2^31)
   bool exhausted = false;
@@ -421,13 +431,13 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 #define YK_SHADOW_WAVES 7
 #endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
-k_trace_closest(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, long long n,
+k_trace_closest(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                 yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                 unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
   trace_body<true, 8>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
-k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, long long n,
+k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
   trace_body<false, 1>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
@@ -613,7 +623,6 @@ struct Batch {
   int* q_owner[2];      // camera sample of each bounce-queue entry
   yk_ray* q_rays[2];    // bounce queues (ping-pong)
   yk_hit* q_hits[2];
-  unsigned long long* q_count;  // [b]: (entries of bounce queue b << 32) | shadow entries of the launch filling b
   yk_ray* s_rays;       // K per camera sample
   uint8_t* s_occl;      // K per camera sample
   unsigned* s_idx;      // compacted shadow queue of slot indices
@@ -822,7 +831,8 @@ __device__ __forceinline__ yk_ray path_first_segment(const Batch& B, const Rende
 // Camera-ray hit (pathtracer.cc:146-160, directlight.cc:124-135): emission
 // and the estimateAllDirectLight shadow rays; for the path tracer also the
 // first segment of sub-path 0 (appended to bounce queue 1).
-__global__ void __launch_bounds__(256) k_shade_primary(DScene S, Batch B, RenderConst R, long long nc) {
+__global__ void __launch_bounds__(256) k_shade_primary(DScene S, Batch B, RenderConst R, long long nc,
+                                                       unsigned long long* __restrict__ qword) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = c < nc;
   int nr = 0, kend = 0;
@@ -870,7 +880,7 @@ __global__ void __launch_bounds__(256) k_shade_primary(DScene S, Batch B, Render
     if (!emit) B.wlast[c] = 0.f;
   }
   unsigned sbase, q;
-  wave_append2(&B.q_count[1], valid ? (unsigned)nr : 0u, emit ? 1u : 0u, sbase, q);
+  wave_append2(qword, valid ? (unsigned)nr : 0u, emit ? 1u : 0u, sbase, q);
   if (valid) flush_shadow(B, c, kend, nr, sbase, traced);
   if (emit) {
     B.q_rays[1][q] = seg;
@@ -915,7 +925,8 @@ __global__ void __launch_bounds__(256) k_resolve_primary(Batch B, RenderConst R,
 
 // First segment of sub-paths isub >= 1 (sub-path 0 is fused into
 // k_shade_primary).
-__global__ void __launch_bounds__(256) k_path_start(DScene S, Batch B, RenderConst R, long long nc, int isub) {
+__global__ void __launch_bounds__(256) k_path_start(DScene S, Batch B, RenderConst R, long long nc, int isub,
+                                                    unsigned long long* __restrict__ qword) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = c < nc;
   bool emit = false;
@@ -929,7 +940,7 @@ __global__ void __launch_bounds__(256) k_path_start(DScene S, Batch B, RenderCon
     emit = true;
   }
   unsigned sbase, q;
-  wave_append2(&B.q_count[1], 0u, emit ? 1u : 0u, sbase, q);
+  wave_append2(qword, 0u, emit ? 1u : 0u, sbase, q);
   if (emit) {
     B.q_rays[1][q] = r;
     B.q_owner[1][q] = (int)c;
@@ -940,8 +951,11 @@ __global__ void __launch_bounds__(256) k_path_start(DScene S, Batch B, RenderCon
 // (pathtracer.cc:189-298): estimateOneDirectLight shadow rays, emission,
 // and the BSDF sample of the next segment. One thread per live path (entry
 // qi of the input bounce queue, owned by camera sample c).
-__global__ void __launch_bounds__(256) k_shade_bounce(DScene S, Batch B, RenderConst R, long long nq, int depth,
-                                                      int isub, int qin) {
+__global__ void __launch_bounds__(256) k_shade_bounce(DScene S, Batch B, RenderConst R,
+                                                      const unsigned long long* __restrict__ qin_word, int depth,
+                                                      int isub, int qin, unsigned long long* __restrict__ qword) {
+  const long long nq = (long long)(*qin_word >> 32);  // live paths (device-side count)
+  if ((long long)blockIdx.x * blockDim.x >= nq) return;  // whole block past the queue
   const long long qi = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = qi < nq;
   const long long c = valid ? B.q_owner[qin][qi] : 0;
@@ -1001,7 +1015,7 @@ __global__ void __launch_bounds__(256) k_shade_bounce(DScene S, Batch B, RenderC
     }
   }
   unsigned sbase, qn;
-  wave_append2(&B.q_count[qin ^ 1], valid ? (unsigned)nr : 0u, emit_next ? 1u : 0u, sbase, qn);
+  wave_append2(qword, valid ? (unsigned)nr : 0u, emit_next ? 1u : 0u, sbase, qn);
   if (valid) flush_shadow(B, c, kend, nr, sbase, traced);
   if (emit_next) {
     B.q_rays[qin ^ 1][qn] = nxt;
@@ -1011,7 +1025,10 @@ __global__ void __launch_bounds__(256) k_shade_bounce(DScene S, Batch B, RenderC
 
 // pathCol += lcol*throughput; throughput *= scol of the next segment. One
 // thread per entry of the bounce queue k_shade_bounce consumed.
-__global__ void __launch_bounds__(256) k_resolve_bounce(Batch B, RenderConst R, long long nq, int depth, int qin) {
+__global__ void __launch_bounds__(256) k_resolve_bounce(Batch B, RenderConst R,
+                                                        const unsigned long long* __restrict__ qin_word, int depth,
+                                                        int qin) {
+  const long long nq = (long long)(*qin_word >> 32);
   const long long qi = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (qi >= nq) return;
   const long long c = B.q_owner[qin][qi];
@@ -1195,15 +1212,18 @@ struct DBuf {
 }  // namespace
 
 // One batch pipeline: a stream with its own queues, counters and scratch.
-// Two pipes run alternate batches so one batch's kernels fill the other's
-// launch tails; film gathers stay in batch order through events.
+// Pipes run alternate batches so one batch's kernels fill the other's launch
+// tails; film gathers stay in batch order through events. Every launch reads
+// its ray / path count from device memory, so a whole render is enqueued
+// without a host round trip and synchronised once.
 struct Pipe {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  DBuf<unsigned long long> counters;  // per-XCD ray segments + work counters
+  DBuf<unsigned long long> counters;  // [0,136): per-call ray segments + counters (ray queries)
+  DBuf<unsigned long long> words;     // per-render: queue-count words, ray segments, accumulators
   DBuf<uint2> ovf;                    // traversal stack overflow (entries deeper than the LDS ring)
+  std::vector<hipEvent_t> evpool;     // per-launch timing events of one render
   DBuf<unsigned> soffs, s_idx;
-  DBuf<unsigned long long> qcount;
   DBuf<float> col, alpha, thr, pathcol, scol_next, wlast, emit_b, sl_contrib;
   DBuf<int> prim_hit, pstate, lsel, qo0, qo1, tile_base;
   DBuf<int4> tiles;
@@ -1218,7 +1238,16 @@ struct Pipe {
     HIPCHK(hipEventCreate(&ev1));
     counters.ensure(136);
   }
+  hipEvent_t event(size_t i) {
+    while (evpool.size() <= i) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      evpool.push_back(e);
+    }
+    return evpool[i];
+  }
   ~Pipe() {
+    for (auto e : evpool) (void)hipEventDestroy(e);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (stream) (void)hipStreamDestroy(stream);
@@ -1243,7 +1272,6 @@ struct Pipe {
     qr1.ensure(maxc);
     qh0.ensure(maxc);
     qh1.ensure(maxc);
-    qcount.ensure(2);
     s_rays.ensure(maxc * K);
     s_occl.ensure(maxc * K);
     s_idx.ensure(maxc * K);
@@ -1273,7 +1301,6 @@ struct Pipe {
     B.q_rays[1] = qr1.p;
     B.q_hits[0] = qh0.p;
     B.q_hits[1] = qh1.p;
-    B.q_count = qcount.p;
     B.s_rays = s_rays.p;
     B.s_occl = s_occl.p;
     B.s_idx = s_idx.p;
@@ -1286,7 +1313,10 @@ struct Pipe {
   }
 };
 
-constexpr int kPipes = 2;
+#ifndef YK_PIPES
+#define YK_PIPES 2
+#endif
+constexpr int kPipes = YK_PIPES;
 
 struct yk_device {
   int ordinal = 0;
@@ -1301,7 +1331,7 @@ struct yk_device {
   DScene S{};
   int ntris = 0, max_depth = 0, nlights = 0, sum_light_samples = 0;
   Pipe pipe[kPipes];
-  hipEvent_t gather_ev[kPipes] = {nullptr, nullptr};
+  hipEvent_t gather_ev[kPipes] = {};
   ~yk_device() {
     for (auto& e : gather_ev)
       if (e) (void)hipEventDestroy(e);
@@ -1439,30 +1469,33 @@ int refill_min() {
   return v;
 }
 
+// Enqueues one persistent traversal launch; no host synchronisation.
+// work: 128 zeroed words (per-XCD segment counters); acc: this kernel kind's
+// accumulators {nodes, triangle tests, errors, rays}. ev: timing pair or null.
 template <bool CLOSEST>
-void launch_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* idx, long long n, yk_hit* hits,
-                  uint8_t* occ, yk_stats* st) {
+void enqueue_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* idx, RayCount n, yk_hit* hits,
+                   uint8_t* occ, unsigned long long* work, unsigned long long* acc, hipEvent_t ev0, hipEvent_t ev1) {
+  const long long grid = (long long)d->cus * d->per_cu[CLOSEST];
+  const int ovf_depth = std::max(1, stack_depth(d) - kStackLds);
+  P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
+  if (ev0) HIPCHK(hipEventRecord(ev0, P.stream));
+  hipLaunchKernelGGL(CLOSEST ? k_trace_closest : k_trace_shadow, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays,
+                     idx, n, hits, occ, work, acc, P.ovf.p, ovf_depth, refill_min());
+  HIPCHK(hipGetLastError());
+  if (ev1) HIPCHK(hipEventRecord(ev1, P.stream));
+}
+
+// Ray-query entry points: one launch, synchronised, statistics added to st.
+template <bool CLOSEST>
+void launch_trace(yk_device* d, Pipe& P, const yk_ray* rays, long long n, yk_hit* hits, uint8_t* occ, yk_stats* st) {
   if (n <= 0) return;
   if (n > 0x7FFFFFFFll - (1ll << 24)) throw std::invalid_argument("ray batch too large (max ~2^31 rays per call)");
-  // [0,128): 8 per-XCD segment counters, one per 128-B line; [128,131): node /
-  // triangle-test / error counters
   unsigned long long* work = P.counters.p;
-  unsigned long long* ctr = P.counters.p + 128;
-  HIPCHK(hipMemsetAsync(work, 0, 132 * sizeof(unsigned long long), P.stream));
-  // persistent grid: as many waves as the chip keeps resident (VGPR/LDS bound)
-  long long grid = (long long)d->cus * d->per_cu[CLOSEST];
-  grid = std::min<long long>(grid, (n + 63) / 64);
-  if (grid < 1) grid = 1;
-  const int D = stack_depth(d);
-  const int ovf_depth = std::max(1, D - kStackLds);
-  P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
-  HIPCHK(hipEventRecord(P.ev0, P.stream));
-  hipLaunchKernelGGL(CLOSEST ? k_trace_closest : k_trace_shadow, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays,
-                     idx, n, hits, occ, work, ctr, P.ovf.p, ovf_depth, refill_min());
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(P.ev1, P.stream));
-  unsigned long long h[3];
-  HIPCHK(hipMemcpyAsync(h, ctr, sizeof h, hipMemcpyDeviceToHost, P.stream));
+  unsigned long long* acc = P.counters.p + 128;
+  HIPCHK(hipMemsetAsync(work, 0, 136 * sizeof(unsigned long long), P.stream));
+  enqueue_trace<CLOSEST>(d, P, rays, nullptr, RayCount{nullptr, 0, n}, hits, occ, work, acc, P.ev0, P.ev1);
+  unsigned long long h[4];
+  HIPCHK(hipMemcpyAsync(h, acc, sizeof h, hipMemcpyDeviceToHost, P.stream));
   HIPCHK(hipStreamSynchronize(P.stream));
   if (h[2]) throw std::runtime_error("kd-tree traversal watchdog fired on " + std::to_string(h[2]) + " rays");
   float ms = 0.f;
@@ -1603,7 +1636,7 @@ int yk_trace_closest(yk_device* d, const yk_ray* d_rays, int64_t n, yk_hit* d_hi
   YK_GUARD_BEGIN
   HIPCHK(hipSetDevice(d->ordinal));
   yk_stats local{};
-  launch_trace<true>(d, d->pipe[0], d_rays, nullptr, n, d_hits, nullptr, st ? st : &local);
+  launch_trace<true>(d, d->pipe[0], d_rays, n, d_hits, nullptr, st ? st : &local);
   return YK_OK;
   YK_GUARD_END
 }
@@ -1614,7 +1647,7 @@ int yk_trace_shadow(yk_device* d, const yk_ray* d_rays, int64_t n, uint8_t* d_oc
   YK_GUARD_BEGIN
   HIPCHK(hipSetDevice(d->ordinal));
   yk_stats local{};
-  launch_trace<false>(d, d->pipe[0], d_rays, nullptr, n, nullptr, d_occ, st ? st : &local);
+  launch_trace<false>(d, d->pipe[0], d_rays, n, nullptr, d_occ, st ? st : &local);
   return YK_OK;
   YK_GUARD_END
 }
@@ -1710,157 +1743,164 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   const long long maxc = (long long)tiles_per_batch * tile_samples;
   const int nbatch = (int)((owned.size() + tiles_per_batch - 1) / tiles_per_batch);
   const int npipes = std::min(kPipes, std::max(1, nbatch));
+  const bool path = p->integrator == YK_INTEGRATOR_PATH;
+  const int bounces = path ? R.bounces : 0;
+  const int nsub = path ? R.nsub : 1;
 
-  // film gathers must run in batch order: batch b waits (on the host) until
-  // batch b-1's gather is enqueued, then (on its stream) for that gather's event
-  std::mutex mu;
-  std::condition_variable cv;
-  int gathers_enqueued = 0;
-  std::string err;
-  int err_code = YK_OK;
-  yk_stats pstats[kPipes] = {};
-
-  auto run_pipe = [&](int pi) {
-    Pipe& P = d->pipe[pi];
-    yk_stats* S = &pstats[pi];
-    try {
-      HIPCHK(hipSetDevice(d->ordinal));
-      Batch B = P.bind(maxc, K, tiles_per_batch);
-      unsigned long long qc[2];
-      auto read_counts = [&]() {
-        HIPCHK(hipMemcpyAsync(qc, P.qcount.p, sizeof qc, hipMemcpyDeviceToHost, P.stream));
-        HIPCHK(hipStreamSynchronize(P.stream));
-      };
-      // shadow rays appended by the launch that filled bounce queue b
-      auto trace_shadow_queue = [&](int b) {
-        read_counts();
-        launch_trace<false>(d, P, B.s_rays, B.s_idx, (long long)(qc[b] & 0xFFFFFFFFull), nullptr, B.s_occl, S);
-      };
-      for (int bi = pi; bi < nbatch; bi += npipes) {
-        {
-          std::lock_guard<std::mutex> lk(mu);
-          if (err_code != YK_OK) return;
-        }
-        const size_t tb0 = (size_t)bi * tiles_per_batch;
-        const size_t tb1 = std::min(owned.size(), tb0 + (size_t)tiles_per_batch);
-        std::vector<int4> tl;
-        std::vector<int> base;
-        long long nc = 0;
-        int rx0 = 1 << 30, ry0 = 1 << 30, rx1 = -(1 << 30), ry1 = -(1 << 30);
-        for (size_t k = tb0; k < tb1; ++k) {
-          const int t = owned[k];
-          const int X = F.cx0 + (t % F.ntx) * F.tile, Y = F.cy0 + (t / F.ntx) * F.tile;
-          const int W = std::min(F.tile, F.cx1 - X), H = std::min(F.tile, F.cy1 - Y);
-          tl.push_back(make_int4(X, Y, W, H));
-          base.push_back((int)nc);
-          nc += (long long)W * H * spp;
-          rx0 = std::min(rx0, X);
-          ry0 = std::min(ry0, Y);
-          rx1 = std::max(rx1, X + W);
-          ry1 = std::max(ry1, Y + H);
-        }
-        base.push_back((int)nc);
-        HIPCHK(hipMemcpyAsync(P.tiles.p, tl.data(), tl.size() * sizeof(int4), hipMemcpyHostToDevice, P.stream));
-        HIPCHK(hipMemcpyAsync(P.tile_base.p, base.data(), base.size() * sizeof(int), hipMemcpyHostToDevice, P.stream));
-        HIPCHK(hipStreamSynchronize(P.stream));  // host vectors die with this iteration
-        TileList TL{P.tiles.p, P.tile_base.p, (int)tl.size()};
-        HIPCHK(hipMemsetAsync(P.qcount.p, 0, 2 * sizeof(unsigned long long), P.stream));
-        hipLaunchKernelGGL(k_camera, dim3(grid_for(nc)), dim3(256), 0, P.stream, TL, B, R, nc);
-        HIPCHK(hipGetLastError());
-        launch_trace<true>(d, P, B.p_rays, nullptr, nc, B.p_hits, nullptr, S);
-        hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, d->S, B, R, nc);
-        HIPCHK(hipGetLastError());
-        trace_shadow_queue(1);
-        hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
-        HIPCHK(hipGetLastError());
-        if (p->integrator == YK_INTEGRATOR_PATH) {
-          // sub-path index outermost: pathCol is shared across sub-paths and
-          // accumulated in the reference's order (pathtracer.cc:164-298)
-          for (int isub = 0; isub < R.nsub; ++isub) {
-            if (isub > 0) {  // sub-path 0's first segment came out of k_shade_primary
-              HIPCHK(hipMemsetAsync(P.qcount.p, 0, 2 * sizeof(unsigned long long), P.stream));
-              hipLaunchKernelGGL(k_path_start, dim3(grid_for(nc)), dim3(256), 0, P.stream, d->S, B, R, nc, isub);
-              HIPCHK(hipGetLastError());
-            }
-            int qin = 1;
-            for (int depth = 1; depth <= R.bounces; ++depth) {
-              read_counts();
-              const unsigned nq = (unsigned)(qc[qin] >> 32);
-              if (nq == 0) break;
-              launch_trace<true>(d, P, B.q_rays[qin], nullptr, nq, B.q_hits[qin], nullptr, S);
-              HIPCHK(hipMemsetAsync(P.qcount.p + (qin ^ 1), 0, sizeof(unsigned long long), P.stream));
-              hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(nq)), dim3(256), 0, P.stream, d->S, B, R,
-                                 (long long)nq, depth, isub, qin);
-              HIPCHK(hipGetLastError());
-              trace_shadow_queue(qin ^ 1);
-              hipLaunchKernelGGL(k_resolve_bounce, dim3(grid_for(nq)), dim3(256), 0, P.stream, B, R, (long long)nq,
-                                 depth, qin);
-              HIPCHK(hipGetLastError());
-              qin ^= 1;
-            }
-          }
-        }
-        hipLaunchKernelGGL(k_finish, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
-        HIPCHK(hipGetLastError());
-        // film: targets = batch rect grown by the filter window, after batch bi-1's gather
-        {
-          std::unique_lock<std::mutex> lk(mu);
-          cv.wait(lk, [&] { return gathers_enqueued == bi || err_code != YK_OK; });
-          if (err_code != YK_OK) return;
-        }
-        if (bi > 0) HIPCHK(hipStreamWaitEvent(P.stream, d->gather_ev[(bi - 1) % kPipes], 0));
-        FilmConst Fb = F;
-        Fb.tb0 = (int)tb0;
-        Fb.tb1 = (int)tb1;
-        const int gx0 = std::max(F.cx0, rx0 + F.olo_x), gy0 = std::max(F.cy0, ry0 + F.olo_y);
-        const int gx1 = std::min(F.cx1, rx1 + F.ohi_x), gy1 = std::min(F.cy1, ry1 + F.ohi_y);
-        const int gw = gx1 - gx0, gh = gy1 - gy0;
-        if (gw > 0 && gh > 0) {
-          hipLaunchKernelGGL(k_film_gather, dim3(grid_for((long long)gw * gh)), dim3(256), 0, P.stream, Fb,
-                             B.samples, B.sxy, P.tile_base.p, d_film, gx0, gy0, gw, gh);
-          HIPCHK(hipGetLastError());
-        }
-        HIPCHK(hipEventRecord(d->gather_ev[bi % kPipes], P.stream));
-        {
-          std::lock_guard<std::mutex> lk(mu);
-          gathers_enqueued = bi + 1;
-        }
-        cv.notify_all();
-        S->camera_samples += (uint64_t)nc;
-        // the pipe's buffers are reused by its next batch: its stream keeps
-        // the order, no host wait needed
-      }
-      HIPCHK(hipStreamSynchronize(P.stream));
-    } catch (const std::exception& e) {
-      std::lock_guard<std::mutex> lk(mu);
-      if (err_code == YK_OK) {
-        err_code = dynamic_cast<const std::invalid_argument*>(&e) ? YK_ERR_ARG : YK_ERR_HIP;
-        err = e.what();
-      }
-      cv.notify_all();
+  // ---- tile lists of all batches, uploaded once
+  std::vector<int4> tiles_all;
+  std::vector<int> base_all((size_t)nbatch * (tiles_per_batch + 1), 0);
+  std::vector<long long> nc_of(nbatch);
+  std::vector<int4> rect_of(nbatch);
+  for (int bi = 0; bi < nbatch; ++bi) {
+    const size_t tb0 = (size_t)bi * tiles_per_batch, tb1 = std::min(owned.size(), tb0 + (size_t)tiles_per_batch);
+    long long nc = 0;
+    int rx0 = 1 << 30, ry0 = 1 << 30, rx1 = -(1 << 30), ry1 = -(1 << 30);
+    for (size_t k = tb0; k < tb1; ++k) {
+      const int t = owned[k];
+      const int X = F.cx0 + (t % F.ntx) * F.tile, Y = F.cy0 + (t / F.ntx) * F.tile;
+      const int W = std::min(F.tile, F.cx1 - X), H = std::min(F.tile, F.cy1 - Y);
+      tiles_all.push_back(make_int4(X, Y, W, H));
+      base_all[(size_t)bi * (tiles_per_batch + 1) + (k - tb0)] = (int)nc;
+      nc += (long long)W * H * spp;
+      rx0 = std::min(rx0, X);
+      ry0 = std::min(ry0, Y);
+      rx1 = std::max(rx1, X + W);
+      ry1 = std::max(ry1, Y + H);
     }
+    base_all[(size_t)bi * (tiles_per_batch + 1) + (tb1 - tb0)] = (int)nc;
+    nc_of[bi] = nc;
+    rect_of[bi] = make_int4(rx0, ry0, rx1, ry1);
+  }
+  DBuf<int4> tiles_dev;
+  DBuf<int> base_dev;
+  tiles_dev.ensure(tiles_all.size());
+  base_dev.ensure(base_all.size());
+  HIPCHK(hipMemcpy(tiles_dev.p, tiles_all.data(), tiles_all.size() * sizeof(int4), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(base_dev.p, base_all.data(), base_all.size() * sizeof(int), hipMemcpyHostToDevice));
+
+  // ---- per-pipe device words: [0,8) accumulators {closest nodes, tris,
+  // errors, rays; any-hit ...}; then per batch: queue-count words
+  // (isub, depth) and one 128-word ray-segment block per trace launch.
+  // All zeroed once; no launch needs a reset or a host round trip.
+  const int qwords_per_batch = nsub * (bounces + 1);
+  const int launches_per_batch = 2 + 2 * nsub * bounces;
+  const long long words_per_batch = qwords_per_batch + 128ll * launches_per_batch;
+  Batch Bp[kPipes];
+  for (int pi = 0; pi < npipes; ++pi) {
+    Pipe& P = d->pipe[pi];
+    const int nb_here = (nbatch - pi + npipes - 1) / npipes;
+    P.words.ensure((size_t)(8 + words_per_batch * nb_here));
+    HIPCHK(hipMemsetAsync(P.words.p, 0, P.words.n * sizeof(unsigned long long), P.stream));
+    Bp[pi] = P.bind(maxc, K, tiles_per_batch);
+  }
+  struct Timed {
+    int pipe;
+    size_t ev;
+    bool closest;
   };
-  std::vector<std::thread> workers;
-  for (int pi = 1; pi < npipes; ++pi) workers.emplace_back(run_pipe, pi);
-  run_pipe(0);
-  for (auto& w : workers) w.join();
-  if (err_code != YK_OK) return set_error(err_code, err);
+  std::vector<Timed> timed;
+  size_t evn[kPipes] = {};
+  long long samples_total = 0;
+
+  for (int bi = 0; bi < nbatch; ++bi) {
+    const int pi = bi % npipes;
+    Pipe& P = d->pipe[pi];
+    const Batch& B = Bp[pi];
+    const long long nc = nc_of[bi];
+    unsigned long long* bw = P.words.p + 8 + words_per_batch * (bi / npipes);
+    auto qw = [&](int isub, int depth) { return bw + isub * (bounces + 1) + depth; };
+    int launch = 0;
+    auto trace = [&](bool closest, const yk_ray* rays, const unsigned* idx, RayCount n, yk_hit* hits,
+                     uint8_t* occ) {
+      unsigned long long* work = bw + qwords_per_batch + 128ll * launch++;
+      const hipEvent_t e0 = P.event(evn[pi]), e1 = P.event(evn[pi] + 1);
+      timed.push_back(Timed{pi, evn[pi], closest});
+      evn[pi] += 2;
+      if (closest) enqueue_trace<true>(d, P, rays, idx, n, hits, occ, work, P.words.p, e0, e1);
+      else enqueue_trace<false>(d, P, rays, idx, n, hits, occ, work, P.words.p + 4, e0, e1);
+    };
+    TileList TL{tiles_dev.p + (size_t)bi * tiles_per_batch, base_dev.p + (size_t)bi * (tiles_per_batch + 1),
+                (int)std::min<size_t>(tiles_per_batch, owned.size() - (size_t)bi * tiles_per_batch)};
+    hipLaunchKernelGGL(k_camera, dim3(grid_for(nc)), dim3(256), 0, P.stream, TL, B, R, nc);
+    HIPCHK(hipGetLastError());
+    trace(true, B.p_rays, nullptr, RayCount{nullptr, 0, nc}, B.p_hits, nullptr);
+    hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, d->S, B, R, nc, qw(0, 0));
+    HIPCHK(hipGetLastError());
+    trace(false, B.s_rays, B.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, B.s_occl);
+    hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
+    HIPCHK(hipGetLastError());
+    // sub-path index outermost: pathCol is shared across sub-paths and
+    // accumulated in the reference's order (pathtracer.cc:164-298)
+    for (int isub = 0; isub < (path ? nsub : 0); ++isub) {
+      if (isub > 0) {  // sub-path 0's first segment came out of k_shade_primary
+        hipLaunchKernelGGL(k_path_start, dim3(grid_for(nc)), dim3(256), 0, P.stream, d->S, B, R, nc, isub,
+                           qw(isub, 0));
+        HIPCHK(hipGetLastError());
+      }
+      int qin = 1;
+      for (int depth = 1; depth <= bounces; ++depth) {
+        const unsigned long long* in_w = qw(isub, depth - 1);
+        unsigned long long* out_w = qw(isub, depth);
+        trace(true, B.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, B.q_hits[qin], nullptr);
+        hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(nc)), dim3(256), 0, P.stream, d->S, B, R, in_w, depth, isub,
+                           qin, out_w);
+        HIPCHK(hipGetLastError());
+        trace(false, B.s_rays, B.s_idx, RayCount{out_w, 0, 0}, nullptr, B.s_occl);
+        hipLaunchKernelGGL(k_resolve_bounce, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, in_w, depth, qin);
+        HIPCHK(hipGetLastError());
+        qin ^= 1;
+      }
+    }
+    hipLaunchKernelGGL(k_finish, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
+    HIPCHK(hipGetLastError());
+    // film: in batch order (tile order), whichever pipe ran the batch
+    if (bi > 0) HIPCHK(hipStreamWaitEvent(P.stream, d->gather_ev[(bi - 1) % kPipes], 0));
+    FilmConst Fb = F;
+    Fb.tb0 = bi * tiles_per_batch;
+    Fb.tb1 = (int)std::min<size_t>(owned.size(), (size_t)(bi + 1) * tiles_per_batch);
+    const int4 rc = rect_of[bi];
+    const int gx0 = std::max(F.cx0, rc.x + F.olo_x), gy0 = std::max(F.cy0, rc.y + F.olo_y);
+    const int gx1 = std::min(F.cx1, rc.z + F.ohi_x), gy1 = std::min(F.cy1, rc.w + F.ohi_y);
+    const int gw = gx1 - gx0, gh = gy1 - gy0;
+    if (gw > 0 && gh > 0) {
+      hipLaunchKernelGGL(k_film_gather, dim3(grid_for((long long)gw * gh)), dim3(256), 0, P.stream, Fb, B.samples,
+                         B.sxy, TL.base, d_film, gx0, gy0, gw, gh);
+      HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(d->gather_ev[bi % kPipes], P.stream));
+    samples_total += nc;
+  }
+  unsigned long long acc[kPipes][8] = {};
+  for (int pi = 0; pi < npipes; ++pi) {
+    Pipe& P = d->pipe[pi];
+    HIPCHK(hipMemcpyAsync(acc[pi], P.words.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, P.stream));
+    HIPCHK(hipStreamSynchronize(P.stream));
+  }
   yk_stats local{};
   yk_stats* S = st ? st : &local;
   for (int pi = 0; pi < npipes; ++pi) {
-    const yk_stats& q = pstats[pi];
-    S->closest_rays += q.closest_rays;
-    S->shadow_rays += q.shadow_rays;
-    S->closest_nodes += q.closest_nodes;
-    S->closest_tris += q.closest_tris;
-    S->shadow_nodes += q.shadow_nodes;
-    S->shadow_tris += q.shadow_tris;
-    S->camera_samples += q.camera_samples;
-    S->ms_closest += q.ms_closest;
-    S->ms_shadow += q.ms_shadow;
-    S->closest_launches += q.closest_launches;
-    S->shadow_launches += q.shadow_launches;
+    if (acc[pi][2] || acc[pi][6])
+      return set_error(YK_ERR_INTERNAL, "kd-tree traversal watchdog fired (corrupt tree or stack)");
+    S->closest_nodes += acc[pi][0];
+    S->closest_tris += acc[pi][1];
+    S->closest_rays += acc[pi][3];
+    S->shadow_nodes += acc[pi][4];
+    S->shadow_tris += acc[pi][5];
+    S->shadow_rays += acc[pi][7];
   }
+  for (const Timed& t : timed) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, d->pipe[t.pipe].evpool[t.ev], d->pipe[t.pipe].evpool[t.ev + 1]));
+    if (t.closest) {
+      S->ms_closest += ms;
+      S->closest_launches++;
+    } else {
+      S->ms_shadow += ms;
+      S->shadow_launches++;
+    }
+  }
+  S->camera_samples += (uint64_t)samples_total;
   S->ms_total += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return YK_OK;
   YK_GUARD_END
