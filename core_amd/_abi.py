@@ -15,6 +15,7 @@ YK_OK = 0
 YK_ERR_ARG, YK_ERR_STATE, YK_ERR_HIP, YK_ERR_UNSUPPORTED, YK_ERR_ALLOC, YK_ERR_INTERNAL = 1, 2, 3, 4, 5, 6
 YK_MAT_SHINYDIFFUSE, YK_MAT_LIGHT = 0, 1
 YK_LIGHT_AREA = 0
+YK_MESH_SMOOTH, YK_MESH_NORMALS_EXPORTED = 1, 2
 YK_INTEGRATOR_DIRECT, YK_INTEGRATOR_PATH = 0, 1
 YK_FILTER_BOX, YK_FILTER_MITCHELL, YK_FILTER_GAUSS, YK_FILTER_LANCZOS = 0, 1, 2, 3
 YK_CAUSTIC_NONE, YK_CAUSTIC_PATH = 0, 1
@@ -104,6 +105,10 @@ SIGNATURES = {
     "yk_scene_destroy": (None, [P]),
     "yk_scene_add_material": (C.c_int, [P, C.POINTER(yk_material), i32p]),
     "yk_scene_add_mesh": (C.c_int, [P, fp, i32, i32p, i32, i32, i32p]),
+    "yk_scene_set_mesh_normals": (C.c_int, [P, i32, fp, i32, i32p, i32]),
+    "yk_scene_set_mesh_base": (C.c_int, [P, i32]),
+    "yk_scene_add_instance": (C.c_int, [P, i32, fp, i32p]),
+    "yk_scene_export_shading": (C.c_int, [P, C.c_void_p, fp]),
     "yk_scene_add_light": (C.c_int, [P, C.POINTER(yk_light)]),
     "yk_scene_set_camera": (C.c_int, [P, C.POINTER(yk_camera)]),
     "yk_scene_build": (C.c_int, [P]),

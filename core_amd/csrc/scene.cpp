@@ -148,31 +148,93 @@ void rec_normal(const float* t, float* n) {
   n[2] = z;
 }
 
+// matrix4x4_t * point3d_t, compiled form of the instance's getVertex
+// (meshtypes.h:140-143): each row as (m0*x + m1*y) + (m2*z + m3)
+static void xform_point(const float* m, const float* p, float* o) {
+  for (int r = 0; r < 3; ++r) {
+    const float* a = m + 4 * r;
+    o[r] = (a[0] * p[0] + a[1] * p[1]) + (a[2] * p[2] + a[3]);
+  }
+}
+// matrix4x4_t * vector3d_t, compiled form of getVertexNormal / getNormal of
+// instances: each row as (m0*x + m2*z) + m1*y
+static void xform_vector(const float* m, const float* v, float* o) {
+  for (int r = 0; r < 3; ++r) {
+    const float* a = m + 4 * r;
+    o[r] = (a[0] * v[0] + a[2] * v[2]) + a[1] * v[1];
+  }
+}
+// vector3d_t::normalize, vector3d.h:249-260
+static void normalize3(float* v) {
+  float len = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+  if (len != 0.f) {
+    len = 1.0f / std::sqrt(len);
+    v[0] *= len;
+    v[1] *= len;
+    v[2] *= len;
+  }
+}
+
 void Scene::finalize() {
-  // scene_t::update, scene.cc:755-782: visible non-base TRIM meshes in object
-  // id order, triangles in insertion order.
+  // scene_t::update, scene.cc:755-782: visible non-base TRIM meshes and
+  // instances in object id order, triangles in insertion order.
   auto t0 = std::chrono::steady_clock::now();
   tri_verts.clear();
   tri_material.clear();
   tri_normal.clear();
-  for (const Mesh& m : meshes) {
-    if (!m.visible) continue;
+  tri_smooth.clear();
+  tri_vnormal.clear();
+  any_smooth = false;
+  for (const Mesh& inst : meshes) {
+    if (!inst.visible || inst.is_base) continue;
+    const bool is_inst = inst.instance_of >= 0;
+    const Mesh& m = is_inst ? meshes[inst.instance_of] : inst;
     const size_t nf = m.faces.size() / 3;
     const int np = (int)(m.points.size() / 3);
+    const int nn = (int)(m.normals.size() / 3);
+    // triangle_t::getSurface smooths with is_smooth; triangleInstance_t with
+    // is_smooth || normals_exported and treats normal index 0 as missing
+    // (triangle.cc:19-26 vs 185-192)
+    const bool smooth = is_inst ? (m.is_smooth || m.normals_exported) : m.is_smooth;
     for (size_t f = 0; f < nf; ++f) {
-      float tv[9];
+      float tv[9], base_tv[9];
       for (int k = 0; k < 3; ++k) {
         int vi = m.faces[3 * f + k];
         if (vi < 0 || vi >= np) throw std::invalid_argument("mesh face references a missing vertex");
-        tv[3 * k + 0] = m.points[3 * vi + 0];
-        tv[3 * k + 1] = m.points[3 * vi + 1];
-        tv[3 * k + 2] = m.points[3 * vi + 2];
+        for (int c = 0; c < 3; ++c) base_tv[3 * k + c] = m.points[3 * vi + c];
+        if (is_inst) xform_point(inst.m, base_tv + 3 * k, tv + 3 * k);
+        else for (int c = 0; c < 3; ++c) tv[3 * k + c] = base_tv[3 * k + c];
       }
       tri_verts.insert(tri_verts.end(), tv, tv + 9);
       tri_material.push_back(m.material);
       float nrm[3];
-      rec_normal(tv, nrm);
+      rec_normal(base_tv, nrm);  // the (base) triangle's recNormal
+      if (is_inst) {  // triangleInstance_t::getNormal: normalize(objToWorld * base normal)
+        float t[3];
+        xform_vector(inst.m, nrm, t);
+        normalize3(t);
+        nrm[0] = t[0];
+        nrm[1] = t[1];
+        nrm[2] = t[2];
+      }
       tri_normal.insert(tri_normal.end(), nrm, nrm + 3);
+      float vn[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+      if (smooth) {
+        for (int k = 0; k < 3; ++k) {
+          const int ni = m.face_normals.empty() ? -1 : m.face_normals[3 * f + k];
+          const bool has = is_inst ? (ni > 0) : (ni >= 0);
+          if (has && ni >= nn) throw std::invalid_argument("face references a missing vertex normal");
+          if (has) {
+            if (is_inst) xform_vector(inst.m, &m.normals[3 * ni], vn + 3 * k);
+            else for (int c = 0; c < 3; ++c) vn[3 * k + c] = m.normals[3 * ni + c];
+          } else {
+            for (int c = 0; c < 3; ++c) vn[3 * k + c] = nrm[c];  // sp.Ng
+          }
+        }
+        any_smooth = true;
+      }
+      tri_smooth.push_back(smooth ? 1 : 0);
+      tri_vnormal.insert(tri_vnormal.end(), vn, vn + 9);
     }
   }
   const int ntris = (int)tri_material.size();

@@ -17,6 +17,14 @@ struct Mesh {
   std::vector<int> faces;     // a,b,c per triangle
   int material = -1;
   bool visible = true;
+  bool is_base = false;       // instancing base: not traced itself
+  // vertex normals (triangleObject_t::normals) and per-face indices (na,nb,nc)
+  std::vector<float> normals;
+  std::vector<int> face_normals;  // 3 per face, -1 = none (empty: all -1)
+  bool is_smooth = false, normals_exported = false;
+  // triangleObjectInstance_t: base mesh index and objToWorld (row-major)
+  int instance_of = -1;
+  float m[16] = {};
 };
 
 struct Scene {
@@ -44,7 +52,10 @@ struct Scene {
   // built by finalize(): flattened prim arrays + kd-tree
   std::vector<float> tri_verts;      // 9 floats per prim
   std::vector<int32_t> tri_material; // material id per prim
-  std::vector<float> tri_normal;     // geometric normal per prim (triangle_t::recNormal)
+  std::vector<float> tri_normal;     // geometric normal per prim (triangle_t::recNormal / instance getNormal)
+  std::vector<uint8_t> tri_smooth;   // getSurface interpolates vertex normals
+  std::vector<float> tri_vnormal;    // 9 floats per prim: va, vb, vc (zero where not smooth)
+  bool any_smooth = false;
   KdTree tree;
   bool built = false;
   double build_seconds = 0.0;

@@ -65,11 +65,13 @@ __constant__ DMat c_mats[kMaxMats];
 __constant__ DLight c_lights[kMaxLights];
 __constant__ DCam c_cam;
 
+constexpr int kSmoothBit = 0x10000;  // prim interpolates vertex normals (mesh is_smooth)
 struct DScene {
   const float4* tris;    // 3 float4 per prim: a, e1=b-a, e2=c-a
   const uint2* nodes;    // kd nodes (kdtree_build.h encoding)
   const uint32_t* leaf;  // leaf primitive lists
-  const float4* ng;      // geometric normal xyz, material id in w (int bits)
+  const float4* ng;      // geometric normal xyz, w = material id | kSmoothBit (int bits)
+  const float* vn;       // 9 floats per prim: getSurface's vertex normals (smooth scenes only)
   float bound[6];
   int nlights;
   unsigned nnodes;  // node count, for the pop-time bounds guard
@@ -457,7 +459,16 @@ __device__ __forceinline__ SurfPt make_surface(const DScene& S, v3 from, v3 dir,
   const float4 g = S.ng[h.prim];
   sp.Ng = V3(g.x, g.y, g.z);
   sp.N = sp.Ng;
-  sp.mat = __float_as_int(g.w);
+  const int mw = __float_as_int(g.w);
+  sp.mat = mw & (kSmoothBit - 1);
+  if (mw & kSmoothBit) {
+    // triangle.cc:19-28 / 185-194: N = normalize(u*va + v*vb + w*vc) with
+    // u = b0 = 1-(b1+b2) (compiled form of intersect's 1-u-v); va..vc resolved
+    // on the host (missing normals -> Ng, instance transform applied)
+    const float* vn = S.vn + 9 * (size_t)h.prim;
+    const float b0 = 1.0f - (h.b1 + h.b2);
+    sp.N = vnormalize(vadd(vadd(vmul(b0, ld3(vn)), vmul(h.b1, ld3(vn + 3))), vmul(h.b2, ld3(vn + 6))));
+  }
   create_cs(sp.N, sp.NU, sp.NV);
   return sp;
 }
@@ -1326,6 +1337,7 @@ struct yk_device {
   bool uploaded = false;
   // scene
   DBuf<float4> tris, ng;
+  DBuf<float> vn;  // smooth-shading vertex normals (9 per prim), only when the scene has smooth meshes
   DBuf<uint2> nodes;
   DBuf<uint32_t> leaf;
   DScene S{};
@@ -1584,7 +1596,7 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
     tris[3 * p + 1] = make_float4(t[3] - t[0], t[4] - t[1], t[5] - t[2], 0.f);
     tris[3 * p + 2] = make_float4(t[6] - t[0], t[7] - t[1], t[8] - t[2], 0.f);
     float nw;
-    int m = S.tri_material[p];
+    int m = S.tri_material[p] | (S.tri_smooth[p] ? kSmoothBit : 0);
     std::memcpy(&nw, &m, 4);
     ng[p] = make_float4(S.tri_normal[3 * p], S.tri_normal[3 * p + 1], S.tri_normal[3 * p + 2], nw);
   }
@@ -1595,6 +1607,10 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   d->leaf.ensure(std::max<size_t>(S.tree.leaf_prims.size(), 1));
   HIPCHK(hipMemcpy(d->tris.p, tris.data(), tris.size() * sizeof(float4), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d->ng.p, ng.data(), ng.size() * sizeof(float4), hipMemcpyHostToDevice));
+  if (S.any_smooth) {
+    d->vn.ensure(S.tri_vnormal.size());
+    HIPCHK(hipMemcpy(d->vn.p, S.tri_vnormal.data(), S.tri_vnormal.size() * sizeof(float), hipMemcpyHostToDevice));
+  }
   HIPCHK(hipMemcpy(d->nodes.p, S.tree.nodes.data(), nn * sizeof(uint2), hipMemcpyHostToDevice));
   if (!S.tree.leaf_prims.empty())
     HIPCHK(hipMemcpy(d->leaf.p, S.tree.leaf_prims.data(), S.tree.leaf_prims.size() * sizeof(uint32_t),
@@ -1619,6 +1635,7 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   d->S.nodes = d->nodes.p;
   d->S.leaf = d->leaf.p;
   d->S.ng = d->ng.p;
+  d->S.vn = S.any_smooth ? d->vn.p : nullptr;
   std::memcpy(d->S.bound, S.tree.bound, sizeof d->S.bound);
   d->S.nlights = (int)S.light_states.size();
   d->S.nnodes = (unsigned)nn;

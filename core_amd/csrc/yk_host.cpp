@@ -91,6 +91,56 @@ int yk_scene_add_mesh(yk_scene* s, const float* points, int32_t npoints, const i
   YK_GUARD_END
 }
 
+int yk_scene_set_mesh_normals(yk_scene* s, int32_t obj_id, const float* normals, int32_t nnormals,
+                              const int32_t* face_normals, int32_t flags) {
+  if (!s || obj_id < 1 || obj_id > (int32_t)s->s.meshes.size() || nnormals < 0 || (nnormals > 0 && !normals))
+    return set_error(YK_ERR_ARG, "yk_scene_set_mesh_normals: bad arguments");
+  if (flags & ~(YK_MESH_SMOOTH | YK_MESH_NORMALS_EXPORTED))
+    return set_error(YK_ERR_ARG, "yk_scene_set_mesh_normals: unknown flags");
+  yk::Mesh& m = s->s.meshes[obj_id - 1];
+  if (m.instance_of >= 0) return set_error(YK_ERR_ARG, "yk_scene_set_mesh_normals: object is an instance");
+  const size_t nf = m.faces.size() / 3;
+  if (face_normals)
+    for (size_t i = 0; i < 3 * nf; ++i)
+      if (face_normals[i] < -1 || face_normals[i] >= nnormals)
+        return set_error(YK_ERR_ARG, "yk_scene_set_mesh_normals: normal index out of range");
+  YK_GUARD_BEGIN
+  m.normals.assign(normals, normals + 3 * (size_t)nnormals);
+  if (face_normals) m.face_normals.assign(face_normals, face_normals + 3 * nf);
+  else m.face_normals.clear();
+  m.is_smooth = (flags & YK_MESH_SMOOTH) != 0;
+  m.normals_exported = (flags & YK_MESH_NORMALS_EXPORTED) != 0;
+  s->s.built = false;
+  return YK_OK;
+  YK_GUARD_END
+}
+
+int yk_scene_set_mesh_base(yk_scene* s, int32_t obj_id) {
+  if (!s || obj_id < 1 || obj_id > (int32_t)s->s.meshes.size())
+    return set_error(YK_ERR_ARG, "yk_scene_set_mesh_base: bad object id");
+  yk::Mesh& m = s->s.meshes[obj_id - 1];
+  if (m.instance_of >= 0) return set_error(YK_ERR_ARG, "yk_scene_set_mesh_base: object is an instance");
+  m.is_base = true;
+  s->s.built = false;
+  return YK_OK;
+}
+
+int yk_scene_add_instance(yk_scene* s, int32_t base_obj_id, const float* obj_to_world, int32_t* obj_id_out) {
+  if (!s || !obj_to_world || base_obj_id < 1 || base_obj_id > (int32_t)s->s.meshes.size())
+    return set_error(YK_ERR_ARG, "yk_scene_add_instance: bad arguments");
+  if (s->s.meshes[base_obj_id - 1].instance_of >= 0)
+    return set_error(YK_ERR_ARG, "yk_scene_add_instance: base object is itself an instance");
+  YK_GUARD_BEGIN
+  yk::Mesh m;
+  m.instance_of = base_obj_id - 1;
+  std::memcpy(m.m, obj_to_world, sizeof m.m);
+  s->s.meshes.push_back(std::move(m));
+  s->s.built = false;
+  if (obj_id_out) *obj_id_out = (int32_t)s->s.meshes.size();
+  return YK_OK;
+  YK_GUARD_END
+}
+
 int yk_scene_add_light(yk_scene* s, const yk_light* l) {
   if (!s || !l) return set_error(YK_ERR_ARG, "yk_scene_add_light: NULL argument");
   if (l->type != YK_LIGHT_AREA) return set_error(YK_ERR_UNSUPPORTED, "light type not supported");
@@ -189,6 +239,15 @@ int yk_scene_export(const yk_scene* s, float* tri_verts, int32_t* tri_material, 
   if (tri_normal) std::memcpy(tri_normal, S.tri_normal.data(), S.tri_normal.size() * sizeof(float));
   if (nodes) std::memcpy(nodes, S.tree.nodes.data(), S.tree.nodes.size() * sizeof(uint32_t));
   if (leaf_prims) std::memcpy(leaf_prims, S.tree.leaf_prims.data(), S.tree.leaf_prims.size() * sizeof(uint32_t));
+  return YK_OK;
+}
+
+int yk_scene_export_shading(const yk_scene* s, uint8_t* smooth, float* vertex_normals) {
+  if (!s) return set_error(YK_ERR_ARG, "yk_scene_export_shading: NULL scene");
+  const yk::Scene& S = s->s;
+  if (!S.built) return set_error(YK_ERR_STATE, "yk_scene_export_shading: scene not built");
+  if (smooth) std::memcpy(smooth, S.tri_smooth.data(), S.tri_smooth.size());
+  if (vertex_normals) std::memcpy(vertex_normals, S.tri_vnormal.data(), S.tri_vnormal.size() * sizeof(float));
   return YK_OK;
 }
 

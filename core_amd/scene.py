@@ -16,6 +16,7 @@ class Scene:
         self._p = C.c_void_p()
         A.check(A.lib().yk_scene_create(C.byref(self._p)))
         self.params = None
+        self.instanced = False
 
     def __del__(self):
         try:
@@ -43,6 +44,27 @@ class Scene:
         oid = C.c_int32()
         A.check(A.lib().yk_scene_add_mesh(self._p, pts.ctypes.data_as(A.fp), len(pts),
                                           fcs.ctypes.data_as(A.i32p), len(fcs), material, C.byref(oid)))
+        return oid.value
+
+    def set_mesh_normals(self, obj_id, normals, face_normals=None, smooth=True, exported=False):
+        """Vertex normals of a mesh (triangleObject_t::normals, triangle_t::na/nb/nc);
+        face_normals: 3 indices per face, -1 = none (None: all missing)."""
+        nrm = np.ascontiguousarray(normals, dtype=np.float32).reshape(-1, 3)
+        fn = None if face_normals is None else np.ascontiguousarray(face_normals, dtype=np.int32).reshape(-1, 3)
+        flags = (A.YK_MESH_SMOOTH if smooth else 0) | (A.YK_MESH_NORMALS_EXPORTED if exported else 0)
+        A.check(A.lib().yk_scene_set_mesh_normals(self._p, obj_id, nrm.ctypes.data_as(A.fp), len(nrm),
+                                                  None if fn is None else fn.ctypes.data_as(A.i32p), flags))
+
+    def set_mesh_base(self, obj_id):
+        """Mark a mesh as an instancing base (not traced itself)."""
+        A.check(A.lib().yk_scene_set_mesh_base(self._p, obj_id))
+
+    def add_instance(self, base_obj_id, obj_to_world):
+        """scene_t::addInstance: obj_to_world is a 4x4 row-major matrix."""
+        m = np.ascontiguousarray(obj_to_world, dtype=np.float32).reshape(16)
+        oid = C.c_int32()
+        A.check(A.lib().yk_scene_add_instance(self._p, base_obj_id, m.ctypes.data_as(A.fp), C.byref(oid)))
+        self.instanced = True
         return oid.value
 
     def add_area_light(self, corner, point1, point2, color=(1, 1, 1), power=1.0, samples=4):
@@ -117,8 +139,11 @@ class Scene:
         A.check(A.lib().yk_scene_export(self._p, tv.ctypes.data_as(A.fp), tm.ctypes.data_as(A.i32p),
                                         tn.ctypes.data_as(A.fp), nodes.ctypes.data_as(A.u32p),
                                         leaf.ctypes.data_as(A.u32p)))
+        sm = np.empty(i.ntris, np.uint8)
+        vn = np.empty((i.ntris, 9), np.float32)
+        A.check(A.lib().yk_scene_export_shading(self._p, sm.ctypes.data, vn.ctypes.data_as(A.fp)))
         return dict(tri_verts=tv, tri_material=tm, tri_normal=tn, nodes=nodes, leaf_prims=leaf,
-                    bound=np.array(i.bound[:], np.float32))
+                    bound=np.array(i.bound[:], np.float32), tri_smooth=sm, tri_vnormal=vn)
 
     def materials(self):
         out = []

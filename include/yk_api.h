@@ -138,6 +138,20 @@ int yk_scene_add_material(yk_scene* s, const yk_material* m, int32_t* id_out);
  * addVertex* + addTriangle* + endTriMesh (scene.cc:265-320,520-625) */
 int yk_scene_add_mesh(yk_scene* s, const float* points, int32_t npoints, const int32_t* faces,
                       int32_t nfaces, int32_t material, int32_t* obj_id_out);
+/* Vertex normals of mesh obj_id (triangle_t::na/nb/nc + triangleObject_t::normals):
+ * normals xyz (nnormals*3), face_normals 3 indices per face (-1 = none),
+ * flags YK_MESH_SMOOTH (triangleObject_t::is_smooth, set by smoothMesh or
+ * exported normals, scene.cc:365-381) and YK_MESH_NORMALS_EXPORTED. */
+enum { YK_MESH_SMOOTH = 1, YK_MESH_NORMALS_EXPORTED = 2 };
+int yk_scene_set_mesh_normals(yk_scene* s, int32_t obj_id, const float* normals, int32_t nnormals,
+                              const int32_t* face_normals, int32_t flags);
+/* mark a mesh as an instancing base: not traced itself (objData_t BASEMESH,
+ * scene_t::update skips isBaseObject(), scene.cc:764) */
+int yk_scene_set_mesh_base(yk_scene* s, int32_t obj_id);
+/* scene_t::addInstance (scene.cc:983-1008): a triangleObjectInstance_t of a
+ * base mesh with objToWorld as 16 floats, row-major (matrix4x4_t). Its prims
+ * are flattened with the reference's vertex / normal transform arithmetic. */
+int yk_scene_add_instance(yk_scene* s, int32_t base_obj_id, const float* obj_to_world, int32_t* obj_id_out);
 int yk_scene_add_light(yk_scene* s, const yk_light* l);
 int yk_scene_set_camera(yk_scene* s, const yk_camera* c);
 /* scene_t::update: gather prims and build the kd-tree (scene.cc:748-785) */
@@ -146,6 +160,9 @@ int yk_scene_info_get(const yk_scene* s, yk_scene_info* out);
 /* copy out flattened prims / tree; any pointer may be NULL */
 int yk_scene_export(const yk_scene* s, float* tri_verts, int32_t* tri_material, float* tri_normal,
                     uint32_t* nodes, uint32_t* leaf_prims);
+/* per-prim shading data: smooth flag (1 byte per prim) and the three vertex
+ * normals getSurface interpolates (9 floats per prim, zero where not smooth) */
+int yk_scene_export_shading(const yk_scene* s, uint8_t* smooth, float* vertex_normals);
 int yk_scene_get_material(const yk_scene* s, int32_t i, yk_material* out);
 int yk_scene_get_light(const yk_scene* s, int32_t i, yk_light* out);
 int yk_scene_get_camera(const yk_scene* s, yk_camera* out);

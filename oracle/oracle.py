@@ -26,6 +26,7 @@ def lib():
         L = C.CDLL(_SO)
         vp = C.c_void_p
         L.orc_load.argtypes = [vp, vp, C.c_int32, vp, vp, vp, vp, C.c_int32, vp, C.c_int32, vp]
+        L.orc_set_shading.argtypes = [vp, vp, vp]
         L.orc_intersect.argtypes = [vp, C.c_int64, vp, vp]
         L.orc_shadow.argtypes = [vp, C.c_int64, vp, vp]
         L.orc_render.argtypes = [vp, vp, vp, vp]
@@ -64,6 +65,7 @@ class Oracle:
         self._lights = (A.yk_light * max(len(lights), 1))(*lights)
         self._cam = scene.camera()
         self._nmats, self._nlights = len(mats), len(lights)
+        self.instanced = bool(getattr(scene, "instanced", False))
         self._activate()
 
     def _activate(self):
@@ -75,6 +77,11 @@ class Oracle:
                        e["nodes"].ctypes.data, e["leaf_prims"].ctypes.data, e["bound"].ctypes.data,
                        C.addressof(self._mats), self._nmats, C.addressof(self._lights), self._nlights,
                        C.addressof(self._cam))
+        # instanced / smooth scenes: the geometric normals and vertex normals
+        # of the host flattening (checked separately by tests/test_instances.py)
+        if e["tri_smooth"].any() or self.instanced:
+            lib().orc_set_shading(e["tri_normal"].ctypes.data, e["tri_smooth"].ctypes.data,
+                                  e["tri_vnormal"].ctypes.data)
         _active = self
 
     def render(self, params):

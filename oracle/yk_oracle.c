@@ -245,7 +245,9 @@ typedef struct {
   int ntris;
   const float* tv;        /* 9 floats / prim                  */
   const int32_t* tmat;
-  v3* ng;                 /* recNormal per prim (computed here) */
+  v3* ng;                 /* recNormal per prim (computed here; orc_set_shading overrides) */
+  const uint8_t* smooth;  /* per prim: getSurface interpolates vertex normals (NULL: none) */
+  const float* vn;        /* 9 floats per prim: va, vb, vc */
   const uint32_t* nodes;  /* 2 words / node                    */
   const uint32_t* leaf;
   float bound[6];
@@ -439,6 +441,14 @@ static int scene_intersect(v3 from, v3 dir, float tmin, float* tmax, surfpt* sp)
   sp->P = vadd(from, vmul(Z, dir));
   sp->Ng = G.ng[prim];
   sp->N = sp->Ng;
+  if (G.smooth && G.smooth[prim]) {
+    /* triangle.cc:19-28 (instances 185-194): u*va + v*vb + w*vc, normalized;
+     * u = data.b0, which intersect computes as 1-(u+v) (compiled form) */
+    const float* n = G.vn + 9 * (size_t)prim;
+    float b0 = 1.0f - (b1 + b2);
+    v3 va = V(n[0], n[1], n[2]), vb = V(n[3], n[4], n[5]), vc = V(n[6], n[7], n[8]);
+    sp->N = vnormalize(vadd(vadd(vmul(b0, va), vmul(b1, vb)), vmul(b2, vc)));
+  }
   createCS(sp->N, &sp->NU, &sp->NV);
   sp->prim = prim;
   sp->mat = G.tmat[prim];
@@ -962,6 +972,21 @@ int orc_load(const float* tri_verts, const int32_t* tri_mat, int32_t ntris, cons
   }
   camera_setup();
   lights_setup();
+  return 0;
+}
+
+/* Shading data of a scene with instances / smooth meshes, taken from the
+ * host's flattening (yk_scene_export / yk_scene_export_shading): the
+ * geometric normal per prim (instances: normalize(M * base recNormal),
+ * triangle.cc triangleInstance_t::getNormal) and the getSurface vertex
+ * normals. The flattening itself is checked against a numpy restatement of
+ * the reference arithmetic in tests/test_instances.py. Arrays must outlive
+ * the loaded scene; call after orc_load. */
+int orc_set_shading(const float* ng, const uint8_t* smooth, const float* vn) {
+  if (ng)
+    for (int p = 0; p < G.ntris; ++p) G.ng[p] = V(ng[3 * p], ng[3 * p + 1], ng[3 * p + 2]);
+  G.smooth = smooth;
+  G.vn = vn;
   return 0;
 }
 

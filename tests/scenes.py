@@ -1,0 +1,86 @@
+"""Test scenes built through the public scene API (no procedural generator):
+Cornell box + an instanced smooth sphere (triangleObjectInstance_t of a base
+mesh, scene.cc:983-1008) + a regular smooth mesh with partly missing vertex
+normals (triangle_t::getSurface na/nb/nc < 0 -> Ng, triangle.cc:19-28).
+"""
+import numpy as np
+
+from core_amd.scene import Scene
+
+
+def uv_sphere(nu, nv, radius=1.0, center=(0.0, 0.0, 0.0)):
+    """Points, faces and unit vertex normals of a UV sphere (float32)."""
+    pts = [(0.0, radius, 0.0)]
+    nrm = [(0.0, 1.0, 0.0)]
+    for j in range(1, nv):
+        th = np.pi * j / nv
+        for i in range(nu):
+            ph = 2 * np.pi * i / nu
+            d = (np.sin(th) * np.cos(ph), np.cos(th), np.sin(th) * np.sin(ph))
+            nrm.append(d)
+            pts.append(tuple(radius * c for c in d))
+    pts.append((0.0, -radius, 0.0))
+    nrm.append((0.0, -1.0, 0.0))
+    south = len(pts) - 1
+    faces = []
+    for i in range(nu):
+        faces.append((0, 1 + (i + 1) % nu, 1 + i))
+    for j in range(nv - 2):
+        r0, r1 = 1 + j * nu, 1 + (j + 1) * nu
+        for i in range(nu):
+            a, b = r0 + i, r0 + (i + 1) % nu
+            c, d = r1 + i, r1 + (i + 1) % nu
+            faces.append((a, b, d))
+            faces.append((a, d, c))
+    r = 1 + (nv - 2) * nu
+    for i in range(nu):
+        faces.append((south, r + i, r + (i + 1) % nu))
+    p = np.asarray(pts, np.float64) + np.asarray(center, np.float64)
+    return p.astype(np.float32), np.asarray(faces, np.int32), np.asarray(nrm, np.float32)
+
+
+def rot_y(deg):
+    c, s = np.cos(np.radians(deg)), np.sin(np.radians(deg))
+    return np.array([[c, 0, s, 0], [0, 1, 0, 0], [-s, 0, c, 0], [0, 0, 0, 1]])
+
+
+def rot_x(deg):
+    c, s = np.cos(np.radians(deg)), np.sin(np.radians(deg))
+    return np.array([[1, 0, 0, 0], [0, c, -s, 0], [0, s, c, 0], [0, 0, 0, 1]])
+
+
+def translate_scale(t, sc):
+    m = np.diag([sc[0], sc[1], sc[2], 1.0])
+    m[:3, 3] = t
+    return m
+
+
+# instance transforms (objToWorld, row-major), rounded to float32 like the
+# matrix4x4_t the reference parses from XML
+INSTANCES = [
+    (translate_scale((0.45, 0.95, -0.25), (0.22, 0.22, 0.22)) @ rot_y(30)).astype(np.float32),
+    (translate_scale((-0.5, 1.55, -0.35), (0.2, 0.15, 0.24)) @ rot_x(-40) @ rot_y(75)).astype(np.float32),
+]
+
+
+def smooth_instanced(resx, resy, integrator="cornell_pt", nu=14, nv=9, smooth=True):
+    """Returns (scene, params, parts) with parts describing the object ids."""
+    s = Scene()
+    p = s.generate(integrator, resx, resy)
+    # base mesh: a smooth unit sphere with exported normals (normals_exported:
+    # face normal index = vertex index, so index 0 -- the north pole -- falls
+    # back to Ng in instances, triangle.cc:185-192)
+    pts, faces, nrm = uv_sphere(nu, nv)
+    base = s.add_mesh(pts, faces, 1)  # red
+    s.set_mesh_normals(base, nrm, faces, smooth=smooth, exported=smooth)
+    s.set_mesh_base(base)
+    inst = [s.add_instance(base, m) for m in INSTANCES]
+    # a regular smooth mesh, every 5th vertex-normal reference missing
+    pts2, faces2, nrm2 = uv_sphere(nu, nv, 0.2, (0.05, 0.35, -0.6))
+    fn2 = faces2.copy().reshape(-1)
+    fn2[::5] = -1
+    reg = s.add_mesh(pts2, faces2, 2)  # green
+    s.set_mesh_normals(reg, nrm2, fn2.reshape(-1, 3), smooth=smooth)
+    s.build()
+    parts = dict(base=base, instances=inst, regular=reg, sphere=(pts, faces, nrm), sphere2=(pts2, faces2, nrm2, fn2))
+    return s, p, parts

@@ -13,6 +13,7 @@ from core_amd import _abi as A
 from core_amd.scene import probe_scene
 from oracle.oracle import Oracle
 from tests.raygen import edge_rays, random_rays
+from tests.scenes import smooth_instanced
 
 pytestmark = pytest.mark.gpu
 
@@ -22,12 +23,17 @@ _SCENES = {}
 def scene(name, resx, resy, nu=0, nv=0):
     key = (name, resx, resy, nu, nv)
     if key not in _SCENES:
-        s, p = probe_scene(name, resx, resy, nu, nv)
+        if name.startswith("smooth_inst"):  # instances + smooth normals (§8 a6/a7), tests/scenes.py
+            gen = "cornell_dl" if name.endswith("_dl") else "cornell_pt"
+            s, p, _ = smooth_instanced(resx, resy, gen)
+        else:
+            s, p = probe_scene(name, resx, resy, nu, nv)
         _SCENES[key] = (s, p, Oracle(s))
     return _SCENES[key]
 
 
-SCENE_CASES = [("cornell_pt", 64, 64, 0, 0), ("bumpy", 64, 64, 120, 61), ("bumpy", 64, 64, 1000, 501)]
+SCENE_CASES = [("cornell_pt", 64, 64, 0, 0), ("bumpy", 64, 64, 120, 61), ("bumpy", 64, 64, 1000, 501),
+               ("smooth_inst", 64, 64, 0, 0)]
 
 
 def _ray_batch(s, seed):
@@ -103,6 +109,9 @@ RENDER_CASES = [
     ("pt_cornell_2sub", ("cornell_pt", 48, 48, 0, 0), (0, 0, 48, 48), {"path_samples": 2, "aa_samples": 3}),
     ("pt_bumpy", ("bumpy", 96, 54, 120, 61), (0, 0, 96, 54), {}),
     ("pt_bumpy_tile16", ("bumpy", 96, 54, 120, 61), (10, 5, 70, 40), {"tile_size": 16, "bounces": 5}),
+    # instances + smooth vertex normals (§8 a6/a7): oracle restatement, parity unpinned vs reference outputs
+    ("pt_smooth_inst", ("smooth_inst", 80, 80, 0, 0), (0, 0, 80, 80), {}),
+    ("dl_smooth_inst", ("smooth_inst_dl", 80, 80, 0, 0), (0, 0, 80, 80), {}),
 ]
 
 
