@@ -59,7 +59,15 @@ YK_MEMBER(SceneMeshes, scene_t, std::map<objID_t YK_COMMA objData_t>, meshes)
 YK_MEMBER(TriPa, triangle_t, int, pa)
 YK_MEMBER(TriPb, triangle_t, int, pb)
 YK_MEMBER(TriPc, triangle_t, int, pc)
+YK_MEMBER(TriNa, triangle_t, int, na)
+YK_MEMBER(TriNb, triangle_t, int, nb)
+YK_MEMBER(TriNc, triangle_t, int, nc)
 YK_MEMBER(MeshPoints, triangleObject_t, std::vector<point3d_t>, points)
+YK_MEMBER(MeshNormals, triangleObject_t, std::vector<normal_t>, normals)
+YK_MEMBER(MeshSmooth, triangleObject_t, bool, is_smooth)
+YK_MEMBER(MeshNormalsExported, triangleObject_t, bool, normals_exported)
+YK_MEMBER(InstToWorld, triangleObjectInstance_t, matrix4x4_t, objToWorld)
+YK_MEMBER(InstBase, triangleObjectInstance_t, triangleObject_t*, mBase)
 YK_MEMBER(SdColor, shinyDiffuseMat_t, color_t, mDiffuseColor)
 YK_MEMBER(SdStrength, shinyDiffuseMat_t, float, mDiffuseStrength)
 YK_MEMBER(SdEmit, shinyDiffuseMat_t, color_t, mEmitColor)
@@ -100,31 +108,59 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     // materials: object state of the materials the prims reference
     std::map<const material_t*, int32_t> mat_ids;
     std::map<objID_t, objData_t>& meshes = GET(*scene, SceneMeshes);
+    // yk object ids of each reference mesh (one per material run), so that
+    // instances (scene_t::addInstance, scene.cc:983-1008) can name their base
+    std::map<const triangleObject_t*, std::vector<int32_t>> yk_ids;
     for (auto& kv : meshes) {
       objData_t& dat = kv.second;
-      if (!dat.obj->isVisible() || dat.obj->isBaseObject() || dat.type != TRIM) continue;
+      if (!dat.obj->isVisible() || dat.type != TRIM) continue;
+      if (triangleObjectInstance_t* inst = dynamic_cast<triangleObjectInstance_t*>(dat.obj)) {
+        // prims of an instance = the base's prims in order: instance each run
+        const matrix4x4_t& M = GET(*inst, InstToWorld);
+        float m16[16];
+        for (int r = 0; r < 4; ++r)
+          for (int c = 0; c < 4; ++c) m16[4 * r + c] = M[r][c];
+        auto it = yk_ids.find(GET(*inst, InstBase));
+        if (it == yk_ids.end()) return unsupported("instance of a mesh the GPU path did not load");
+        for (int32_t base_id : it->second)
+          if (yk_scene_add_instance(ys, base_id, m16, nullptr) != YK_OK) return fail();
+        continue;
+      }
+      // base meshes are loaded too (marked base: not traced, scene.cc:765)
       const int n = dat.obj->numPrimitives();
       std::vector<const triangle_t*> prims(n);
       dat.obj->getPrimitives(prims.data());
       const std::vector<point3d_t>& pts = GET(*dat.obj, MeshPoints);
       std::vector<float> xyz(3 * pts.size());
       for (size_t i = 0; i < pts.size(); ++i) put3(&xyz[3 * i], pts[i].x, pts[i].y, pts[i].z);
+      const std::vector<normal_t>& nrm = GET(*dat.obj, MeshNormals);
+      std::vector<float> nxyz(3 * nrm.size());
+      for (size_t i = 0; i < nrm.size(); ++i) put3(&nxyz[3 * i], nrm[i].x, nrm[i].y, nrm[i].z);
+      const int32_t flags = (GET(*dat.obj, MeshSmooth) ? YK_MESH_SMOOTH : 0) |
+                            (GET(*dat.obj, MeshNormalsExported) ? YK_MESH_NORMALS_EXPORTED : 0);
+      std::vector<int32_t>& ids = yk_ids[dat.obj];
       // one yk mesh per run of prims with the same material, prim order kept
       for (int a = 0; a < n;) {
         const material_t* m = prims[a]->getMaterial();
         int b = a;
-        std::vector<int32_t> faces;
+        std::vector<int32_t> faces, fnrm;
         while (b < n && prims[b]->getMaterial() == m) {
           faces.push_back(GET(*prims[b], TriPa));
           faces.push_back(GET(*prims[b], TriPb));
           faces.push_back(GET(*prims[b], TriPc));
+          for (int k : {GET(*prims[b], TriNa), GET(*prims[b], TriNb), GET(*prims[b], TriNc)})
+            fnrm.push_back(k >= 0 && k < (int)nrm.size() ? k : -1);
           ++b;
         }
-        int32_t mid;
+        int32_t mid, oid;
         if (!material_id(m, mat_ids, mid)) return false;
         if (yk_scene_add_mesh(ys, xyz.data(), (int32_t)pts.size(), faces.data(), (int32_t)(faces.size() / 3),
-                              mid, nullptr) != YK_OK)
+                              mid, &oid) != YK_OK)
           return fail();
+        if (flags && yk_scene_set_mesh_normals(ys, oid, nxyz.data(), (int32_t)nrm.size(), fnrm.data(), flags) != YK_OK)
+          return fail();
+        if (dat.obj->isBaseObject() && yk_scene_set_mesh_base(ys, oid) != YK_OK) return fail();
+        ids.push_back(oid);
         a = b;
       }
     }
