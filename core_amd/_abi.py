@@ -107,6 +107,7 @@ SIGNATURES = {
     "yk_scene_add_mesh": (C.c_int, [P, fp, i32, i32p, i32, i32, i32p]),
     "yk_scene_set_mesh_normals": (C.c_int, [P, i32, fp, i32, i32p, i32]),
     "yk_scene_set_mesh_base": (C.c_int, [P, i32]),
+    "yk_scene_add_curve": (C.c_int, [P, fp, i32, i32, C.c_float, C.c_float, C.c_float, i32p]),
     "yk_scene_add_instance": (C.c_int, [P, i32, fp, i32p]),
     "yk_scene_export_shading": (C.c_int, [P, C.c_void_p, fp]),
     "yk_scene_add_light": (C.c_int, [P, C.POINTER(yk_light)]),

@@ -1,6 +1,7 @@
 // Host scene assembly, kd-tree build trigger and the procedural probe scenes.
 #include "scene.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -244,6 +245,75 @@ void Scene::finalize() {
   build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// scene_t::endCurveMesh (scene.cc:138-264): a strand polyline extruded to a
+// triangular prism, in the compiled operation order of the survey build
+// (-O3 -ffast-math, read from its disassembly):
+//   (float)i/(n-1)       -> i * (1.0f/(n-1))
+//   r                    -> start + pow(t, 1+shape)*(end-start)         (shape < 0)
+//                           start + (1 - pow(t', 1-shape))*(end-start)  (else)
+//   1.5*r/sqrt(3.f)      -> (float)((double)r * (1.5/(double)sqrtf(3)))
+//   a, b                 -> (o - (0.5r)*v) -/+ c*u per component; u.z == 0
+// Points: the n centre points, then a_i, b_i per point; faces: bottom cap,
+// 6 per segment, top cap (2 + 6(n-1) triangles).
+Mesh curve_mesh(const float* pts, int n, int material, float strand_start, float strand_end, float strand_shape) {
+  if (n < 2) throw std::invalid_argument("a curve needs at least 2 points");
+  Mesh m;
+  m.material = material;
+  m.points.assign(pts, pts + 3 * (size_t)n);
+  m.points.reserve(9 * (size_t)n);
+  const float inv_nm1 = 1.0f / (float)(n - 1);
+  const float span = strand_end - strand_start;
+  const double k_half_w = 1.5 / (double)std::sqrt(3.0f);
+  float ux = 0, uy = 0, vx = 0, vy = 0, vz = 0;
+  for (int i = 0; i < n; ++i) {
+    const float* o = pts + 3 * i;
+    float r;
+    if (strand_shape < 0)
+      r = std::pow((float)i * inv_nm1, 1.0f + strand_shape) * span + strand_start;
+    else
+      r = (1.0f - std::pow((float)(n - i - 1) * inv_nm1, 1.0f - strand_shape)) * span + strand_start;
+    if (i < n - 1) {  // the last point keeps the previous tangent frame
+      float N[3] = {o[3] - o[0], o[4] - o[1], o[5] - o[2]};
+      const float len = (N[0] * N[0] + N[1] * N[1]) + N[2] * N[2];
+      if (len != 0.f) {
+        const float inv = 1.0f / std::sqrt(len);
+        N[0] *= inv;
+        N[1] *= inv;
+        N[2] *= inv;
+      }
+      if (N[0] == 0.f && N[1] == 0.f) {  // createCS, vector3d.h:316-334
+        ux = N[2] < 0.f ? -1.f : 1.f;
+        uy = 0.f;
+        vx = 0.f;
+        vy = 1.f;
+        vz = 0.f;
+      } else {
+        const float d = 1.0f / std::sqrt(N[1] * N[1] + N[0] * N[0]);
+        ux = N[1] * d;
+        uy = -(N[0] * d);
+        vx = -(N[2] * uy);
+        vy = N[2] * ux;
+        vz = N[0] * uy - N[1] * ux;
+      }
+    }
+    const float h = r * 0.5f;
+    const float c = (float)((double)r * k_half_w);
+    const float px = o[0] - h * vx, py = o[1] - h * vy, pz = o[2] - h * vz;
+    const float a[3] = {px - c * ux, py - c * uy, pz}, b[3] = {px + c * ux, py + c * uy, pz};
+    m.points.insert(m.points.end(), a, a + 3);
+    m.points.insert(m.points.end(), b, b + 3);
+  }
+  m.faces.reserve(3 * (size_t)(6 * (n - 1) + 2));
+  int i = 0;
+  for (; i < n - 1; ++i) {
+    const int a1 = i, a2 = 2 * i + n, a3 = a2 + 1, b1 = i + 1, b2 = a2 + 2, b3 = b2 + 1;
+    if (i == 0) m.faces.insert(m.faces.end(), {a1, a3, a2});
+    m.faces.insert(m.faces.end(), {a1, b2, b1, a1, a2, b2, a2, b3, b2, a2, a3, b3, b3, a3, a1, b3, a1, b1});
+  }
+  m.faces.insert(m.faces.end(), {i, 2 * i + n, 2 * i + n + 1});
+  return m;
+}
+
 namespace {
 
 inline float atof_f(double v) { return (float)v; }  // xmlparser.cc:237-239: atof -> float
@@ -412,6 +482,52 @@ void gen_bumpy(Scene& s, int nu, int nv, int resx, int resy) {
   cam.near_clip = 0.f;
   cam.far_clip = -1.f;
   s.set_camera(cam);
+}
+
+// C5 probe: hair. A flat-shaded head sphere (200x101
+// grid) at (0,1.2,0) over the 6x6 floor, with `nstrands` <curve> strands of
+// `npoints` points (6(n-1)+2 triangles each, scene.cc:138-264) rooted on a
+// Fibonacci spiral over the upper 80 % of the sphere and drooping under a
+// fixed bend; strand thickness 0.012 -> 0.004, shape alternating -0.3 / 0.3
+// (both branches of the radius law). 200,000 strands x 9 points = 10.0M
+// strand triangles. Coordinates go through "%.6f" text like the XML.
+void gen_hair(Scene& s, int nstrands, int npoints, int resx, int resy) {
+  gen_bumpy(s, 200, 101, resx, resy);
+  s.meshes[1].material = 0;
+  const int hair_a = add_mat(s, YK_MAT_SHINYDIFFUSE, 0.45f, 0.3f, 0.15f, 1.f);
+  const int hair_b = add_mat(s, YK_MAT_SHINYDIFFUSE, 0.3f, 0.2f, 0.1f, 1.f);
+  const double pi = 3.141592653589793, golden = pi * (3.0 - std::sqrt(5.0));
+  {  // key light in front of the head (the top light is mostly blocked by the hair)
+    yk_light l = s.lights[0];
+    const float c[3] = {-1.f, 1.5f, -3.f}, p1[3] = {1.f, 1.5f, -3.f}, p2[3] = {-1.f, 2.5f, -3.f};
+    for (int k = 0; k < 3; ++k) {
+      l.corner[k] = c[k];
+      l.point1[k] = p1[k];
+      l.point2[k] = p2[k];
+    }
+    l.power = 3.f;
+    s.add_light(l);
+  }
+  const double len = 0.7;
+  std::vector<float> pts(3 * (size_t)npoints);
+  s.meshes.reserve(s.meshes.size() + nstrands);
+  for (int k = 0; k < nstrands; ++k) {
+    const double y = 1.0 - 1.8 * (k + 0.5) / nstrands;  // root height on the unit sphere
+    const double rr = std::sqrt(std::max(0.0, 1.0 - y * y)), ph = golden * k;
+    const double n[3] = {rr * std::cos(ph), y, rr * std::sin(ph)};
+    double p[3] = {n[0], 1.2 + n[1], n[2]};
+    const double seg = len / (npoints - 1);
+    for (int j = 0; j < npoints; ++j) {
+      for (int c = 0; c < 3; ++c) pts[3 * j + c] = fmt6(p[c]);
+      const double t = (double)(j + 1) / (npoints - 1);
+      const double curl = 0.15 * std::sin(3.0 * t + 0.7 * k);
+      double d[3] = {n[0] * (1.0 - t) + curl * n[2], n[1] * (1.0 - t) - 0.9 * t, n[2] * (1.0 - t) - curl * n[0]};
+      const double dl = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+      for (int c = 0; c < 3; ++c) p[c] += seg * d[c] / (dl > 0 ? dl : 1.0);
+    }
+    s.meshes.push_back(curve_mesh(pts.data(), npoints, (k & 1) ? hair_b : hair_a, 0.012f, 0.004f,
+                                  (k & 1) ? 0.3f : -0.3f));
+  }
 }
 
 }  // namespace yk

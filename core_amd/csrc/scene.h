@@ -64,7 +64,9 @@ struct Scene {
 };
 
 // Procedural fixtures (deterministic, no RNG): the probe scenes of BASELINE.md.
+Mesh curve_mesh(const float* pts, int n, int material, float strand_start, float strand_end, float strand_shape);
 void gen_cornell(Scene& s, int resx, int resy);
+void gen_hair(Scene& s, int nstrands, int npoints, int resx, int resy);
 void gen_bumpy(Scene& s, int nu, int nv, int resx, int resy);
 
 // Reference constructor arithmetic (IEEE, no contraction):

@@ -141,6 +141,19 @@ int yk_scene_add_instance(yk_scene* s, int32_t base_obj_id, const float* obj_to_
   YK_GUARD_END
 }
 
+int yk_scene_add_curve(yk_scene* s, const float* points, int32_t npoints, int32_t material, float strand_start,
+                       float strand_end, float strand_shape, int32_t* obj_id_out) {
+  if (!s || !points || npoints < 2) return set_error(YK_ERR_ARG, "yk_scene_add_curve: need >= 2 points");
+  if (material < 0 || material >= (int32_t)s->s.material_states.size())
+    return set_error(YK_ERR_ARG, "yk_scene_add_curve: unknown material id");
+  YK_GUARD_BEGIN
+  s->s.meshes.push_back(yk::curve_mesh(points, npoints, material, strand_start, strand_end, strand_shape));
+  s->s.built = false;
+  if (obj_id_out) *obj_id_out = (int32_t)s->s.meshes.size();
+  return YK_OK;
+  YK_GUARD_END
+}
+
 int yk_scene_add_light(yk_scene* s, const yk_light* l) {
   if (!s || !l) return set_error(YK_ERR_ARG, "yk_scene_add_light: NULL argument");
   if (l->type != YK_LIGHT_AREA) return set_error(YK_ERR_UNSUPPORTED, "light type not supported");
@@ -328,6 +341,13 @@ int yk_scene_generate(yk_scene* s, const char* name, int32_t p0, int32_t p1, int
     yk::gen_bumpy(s->s, nu, nv, resx, resy);
     p.integrator = YK_INTEGRATOR_PATH;
     p.bounces = 3;
+    p.aa_samples = 4;
+  } else if (n == "hair") {
+    const int ns = p0 > 0 ? p0 : 200000, np = p1 > 0 ? p1 : 9;
+    if (np < 2) return set_error(YK_ERR_ARG, "hair: strands need >= 2 points");
+    yk::gen_hair(s->s, ns, np, resx, resy);
+    p.integrator = YK_INTEGRATOR_PATH;
+    p.bounces = 8;
     p.aa_samples = 4;
   } else {
     return set_error(YK_ERR_ARG, "unknown procedural scene '" + n + "'");

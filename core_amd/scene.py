@@ -55,6 +55,14 @@ class Scene:
         A.check(A.lib().yk_scene_set_mesh_normals(self._p, obj_id, nrm.ctypes.data_as(A.fp), len(nrm),
                                                   None if fn is None else fn.ctypes.data_as(A.i32p), flags))
 
+    def add_curve(self, points, material, strand_start=0.01, strand_end=0.01, strand_shape=0.0):
+        """scene_t curve mesh (hair strand): points (n,3), n >= 2."""
+        pts = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)
+        oid = C.c_int32()
+        A.check(A.lib().yk_scene_add_curve(self._p, pts.ctypes.data_as(A.fp), len(pts), material, strand_start,
+                                           strand_end, strand_shape, C.byref(oid)))
+        return oid.value
+
     def set_mesh_base(self, obj_id):
         """Mark a mesh as an instancing base (not traced itself)."""
         A.check(A.lib().yk_scene_set_mesh_base(self._p, obj_id))

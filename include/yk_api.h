@@ -145,6 +145,12 @@ int yk_scene_add_mesh(yk_scene* s, const float* points, int32_t npoints, const i
 enum { YK_MESH_SMOOTH = 1, YK_MESH_NORMALS_EXPORTED = 2 };
 int yk_scene_set_mesh_normals(yk_scene* s, int32_t obj_id, const float* normals, int32_t nnormals,
                               const int32_t* face_normals, int32_t flags);
+/* scene_t::startCurveMesh/addVertex/endCurveMesh (scene.cc:110-264): a hair
+ * strand through npoints points, extruded to a triangular prism of
+ * 6*(npoints-1)+2 triangles with the reference's radius law
+ * (strand_start/end/shape) and vertex arithmetic. */
+int yk_scene_add_curve(yk_scene* s, const float* points, int32_t npoints, int32_t material, float strand_start,
+                       float strand_end, float strand_shape, int32_t* obj_id_out);
 /* mark a mesh as an instancing base: not traced itself (objData_t BASEMESH,
  * scene_t::update skips isBaseObject(), scene.cc:764) */
 int yk_scene_set_mesh_base(yk_scene* s, int32_t obj_id);

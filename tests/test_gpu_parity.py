@@ -33,7 +33,7 @@ def scene(name, resx, resy, nu=0, nv=0):
 
 
 SCENE_CASES = [("cornell_pt", 64, 64, 0, 0), ("bumpy", 64, 64, 120, 61), ("bumpy", 64, 64, 1000, 501),
-               ("smooth_inst", 64, 64, 0, 0)]
+               ("smooth_inst", 64, 64, 0, 0), ("hair", 64, 64, 3000, 9)]
 
 
 def _ray_batch(s, seed):
@@ -112,6 +112,8 @@ RENDER_CASES = [
     # instances + smooth vertex normals (§8 a6/a7): oracle restatement, parity unpinned vs reference outputs
     ("pt_smooth_inst", ("smooth_inst", 80, 80, 0, 0), (0, 0, 80, 80), {}),
     ("dl_smooth_inst", ("smooth_inst_dl", 80, 80, 0, 0), (0, 0, 80, 80), {}),
+    # C5 shape: hair strands (curve meshes), 8 bounces, two area lights
+    ("pt_hair", ("hair", 64, 64, 3000, 9), (0, 0, 64, 64), {}),
 ]
 
 
