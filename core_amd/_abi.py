@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("YK_LIB") or os.path.join(_HERE, "libyk.so")  # YK_LIB
 YK_OK = 0
 YK_ERR_ARG, YK_ERR_STATE, YK_ERR_HIP, YK_ERR_UNSUPPORTED, YK_ERR_ALLOC, YK_ERR_INTERNAL = 1, 2, 3, 4, 5, 6
 YK_MAT_SHINYDIFFUSE, YK_MAT_LIGHT = 0, 1
-YK_LIGHT_AREA = 0
+YK_LIGHT_AREA, YK_LIGHT_POINT, YK_LIGHT_DIRECTIONAL = 0, 1, 2
 YK_MESH_SMOOTH, YK_MESH_NORMALS_EXPORTED = 1, 2
 YK_INTEGRATOR_DIRECT, YK_INTEGRATOR_PATH = 0, 1
 YK_FILTER_BOX, YK_FILTER_MITCHELL, YK_FILTER_GAUSS, YK_FILTER_LANCZOS = 0, 1, 2, 3
@@ -30,7 +30,8 @@ class yk_material(C.Structure):
 
 class yk_light(C.Structure):
     _fields_ = [("type", C.c_int32), ("corner", f3), ("point1", f3), ("point2", f3),
-                ("color", f3), ("power", C.c_float), ("samples", C.c_int32)]
+                ("color", f3), ("power", C.c_float), ("samples", C.c_int32),
+                ("from_", f3), ("direction", f3), ("radius", C.c_float), ("infinite", C.c_int32)]
 
 
 class yk_camera(C.Structure):
@@ -46,6 +47,11 @@ class yk_material_state(C.Structure):
 
 class yk_area_light_state(C.Structure):
     _fields_ = [("corner", f3), ("to_x", f3), ("to_y", f3), ("color", f3), ("samples", C.c_int32)]
+
+
+class yk_dirac_light_state(C.Structure):
+    _fields_ = [("type", C.c_int32), ("position", f3), ("direction", f3), ("color", f3),
+                ("radius", C.c_float), ("infinite", C.c_int32)]
 
 
 class yk_camera_state(C.Structure):
@@ -123,6 +129,10 @@ SIGNATURES = {
     "yk_scene_set_camera_state": (C.c_int, [P, C.POINTER(yk_camera_state)]),
     "yk_scene_get_material_state": (C.c_int, [P, i32, C.POINTER(yk_material_state)]),
     "yk_scene_get_area_light_state": (C.c_int, [P, i32, C.POINTER(yk_area_light_state)]),
+    "yk_scene_add_dirac_light_state": (C.c_int, [P, C.POINTER(yk_dirac_light_state)]),
+    "yk_scene_get_dirac_light_state": (C.c_int, [P, i32, C.POINTER(yk_dirac_light_state)]),
+    "yk_scene_set_background": (C.c_int, [P, fp, C.c_float]),
+    "yk_scene_get_background": (C.c_int, [P, fp, i32p]),
     "yk_scene_get_camera_state": (C.c_int, [P, C.POINTER(yk_camera_state)]),
     "yk_scene_generate": (C.c_int, [P, C.c_char_p, i32, i32, i32, i32, C.POINTER(yk_render_params)]),
     "yk_render_params_default": (None, [C.POINTER(yk_render_params)]),

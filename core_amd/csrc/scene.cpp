@@ -69,6 +69,29 @@ yk_area_light_state light_state(const yk_light& l) {  // areaLight_t::factory + 
   return o;
 }
 
+// pointLight_t::pointLight_t (pointlight.cc:53-58) / directionalLight_t::
+// directionalLight_t (directional.cc:50-58): color*power, direction.normalize()
+yk_dirac_light_state dirac_state(const yk_light& l) {
+  yk_dirac_light_state o{};
+  o.type = l.type;
+  for (int k = 0; k < 3; ++k) {
+    o.position[k] = l.from[k];
+    o.color[k] = l.color[k] * l.power;
+  }
+  if (l.type == YK_LIGHT_DIRECTIONAL) {
+    float d[3] = {l.direction[0], l.direction[1], l.direction[2]};
+    const float len = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
+    if (len != 0.f) {
+      const float inv = 1.0f / std::sqrt(len);
+      for (float& x : d) x *= inv;
+    }
+    for (int k = 0; k < 3; ++k) o.direction[k] = d[k];
+    o.radius = l.radius;
+    o.infinite = l.infinite;
+  }
+  return o;
+}
+
 yk_camera_state camera_state(const yk_camera& c) {  // camera_t ctor + setAxis
   yk_camera_state o{};
   const hv3 pos = H(c.from), look = H(c.to), up = H(c.up);
@@ -110,12 +133,32 @@ int Scene::add_material_state(const yk_material_state& m) {
 void Scene::add_light(const yk_light& l) {
   lights.push_back(l);
   light_has_params.push_back(true);
-  light_states.push_back(light_state(l));
+  light_kind.push_back(l.type);
+  if (l.type == YK_LIGHT_AREA) {
+    light_states.push_back(light_state(l));
+    dirac_states.push_back(yk_dirac_light_state{});
+  } else {
+    yk_area_light_state a{};
+    a.samples = 1;
+    light_states.push_back(a);
+    dirac_states.push_back(dirac_state(l));
+  }
+}
+void Scene::add_dirac_light_state(const yk_dirac_light_state& l) {
+  lights.push_back(yk_light{});
+  light_has_params.push_back(false);
+  light_kind.push_back(l.type);
+  yk_area_light_state a{};
+  a.samples = 1;
+  light_states.push_back(a);
+  dirac_states.push_back(l);
 }
 void Scene::add_light_state(const yk_area_light_state& l) {
   lights.push_back(yk_light{});
   light_has_params.push_back(false);
+  light_kind.push_back(YK_LIGHT_AREA);
   light_states.push_back(l);
+  dirac_states.push_back(yk_dirac_light_state{});
 }
 void Scene::set_camera(const yk_camera& c) {
   camera = c;

@@ -38,7 +38,11 @@ struct Scene {
   bool camera_has_params = false;
   // ... and the reference object state the kernels consume
   std::vector<yk_material_state> material_states;
-  std::vector<yk_area_light_state> light_states;
+  std::vector<int> light_kind;                      // YK_LIGHT_*, scene light order
+  std::vector<yk_area_light_state> light_states;    // area lights (zero entry for Dirac lights)
+  std::vector<yk_dirac_light_state> dirac_states;   // point / directional (zero entry for area lights)
+  bool has_background = false;
+  float background[3] = {0.f, 0.f, 0.f};            // constBackground_t::color (color*power)
   yk_camera_state camera_state{};
   bool has_camera = false;
 
@@ -46,6 +50,7 @@ struct Scene {
   int add_material_state(const yk_material_state& m);
   void add_light(const yk_light& l);
   void add_light_state(const yk_area_light_state& l);
+  void add_dirac_light_state(const yk_dirac_light_state& l);
   void set_camera(const yk_camera& c);
   void set_camera_state(const yk_camera_state& c);
 
@@ -74,6 +79,7 @@ void gen_bumpy(Scene& s, int nu, int nv, int resx, int resy);
 // camera_t ctor + perspectiveCam_t::setAxis (camera.h:41-60, perspectiveCamera.cc:28-71).
 yk_material_state material_state(const yk_material& m);
 yk_area_light_state light_state(const yk_light& l);
+yk_dirac_light_state dirac_state(const yk_light& l);
 yk_camera_state camera_state(const yk_camera& c);
 
 // recNormal: ((b-a)^(c-a)).normalize() with the reference's float op order

@@ -53,6 +53,10 @@ struct DLight {  // areaLight_t members after its constructor (arealight.cc:30-4
   float corner[3], toX[3], toY[3], fnormal[3], c2[3], c3[3], c4[3], color[3];
   float area;
   int samples;
+  int type;    // YK_LIGHT_*; point / directional are Dirac lights (mcintegrator.cc:85-100)
+  int nslots;  // shadow slots per doLightEstimation: 2*samples (area + MIS half), 1 (Dirac)
+  float pos[3], dir[3], radius;  // pointLight_t / directionalLight_t members
+  int infinite;
 };
 
 struct DCam {  // perspectiveCam_t after camera_t ctor + setAxis
@@ -582,6 +586,38 @@ __device__ __forceinline__ bool light_hit(const DLight& L, v3 from, v3 dir, floa
   return true;
 }
 
+// pointLight_t::illuminate (pointlight.cc:60-75) / directionalLight_t::
+// illuminate (directional.cc:77-96), compiled forms: |v|^2 as (x*x + y*y) + z*z,
+// 1/dist and 1/dist^2 as separate divisions; col = color * (1/dist^2).
+__device__ __forceinline__ bool dirac_illum(const DLight& L, v3 P, v3& ldir, float& tmax, c3& col) {
+  if (L.type == YK_LIGHT_POINT) {
+    const v3 l = vsub(ld3(L.pos), P);
+    const float dist_sqr = l.x * l.x + l.y * l.y + l.z * l.z;
+    const float dist = sqrtf(dist_sqr);
+    if (dist == 0.f) return false;
+    const float idist_sqr = 1.f / dist_sqr;
+    const float inv = 1.f / dist;
+    ldir = V3(l.x * inv, l.y * inv, l.z * inv);
+    tmax = dist;
+    col = C3(L.color[0] * idist_sqr, L.color[1] * idist_sqr, L.color[2] * idist_sqr);
+    return true;
+  }
+  const v3 d = ld3(L.dir);
+  if (!L.infinite) {  // outside the illuminated cylinder?
+    const v3 vec = vsub(ld3(L.pos), P);
+    const v3 cr = vcross(d, vec);
+    const float dist = sqrtf(cr.x * cr.x + cr.y * cr.y + cr.z * cr.z);
+    if (dist > L.radius) return false;
+    tmax = vdot(vec, d);
+    if (tmax <= 0.f) return false;
+  } else {
+    tmax = -1.f;
+  }
+  ldir = d;
+  col = C3(L.color[0], L.color[1], L.color[2]);
+  return true;
+}
+
 // ------------------------------------------------------------ queues
 
 // Reserves m_s shadow-queue and m_b bounce-queue entries with ONE returning
@@ -651,6 +687,8 @@ struct RenderConst {
   int integrator;
   int transp_bg;
   int nlights;
+  int has_bg;     // constant background color for camera-ray misses
+  float bg[3];
   float d1;       // 1/spp as renderTile computes it
 };
 
@@ -731,10 +769,29 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
                                          unsigned long long& traced) {
   const DLight& L = c_lights[li];
   const DMat& M = c_mats[sp.mat];
+  const c3 black = C3(0.f, 0.f, 0.f);
+  if (L.type != YK_LIGHT_AREA) {  // Dirac branch, mcintegrator.cc:85-100: one shadow ray
+    const long long slot = c * B.K + k0;
+    v3 ldir;
+    float ltmax;
+    c3 lc;
+    if (!dirac_illum(L, sp.P, ldir, ltmax, lc)) {
+      put_slot(B, slot, 0, black);
+      return 0;
+    }
+    put_ray(B.s_rays[slot], sp.P, ldir, YK_SHADOW_BIAS, ltmax);
+    if (k0 < 64) traced |= 1ull << k0;
+    const c3 surf = mat_eval(M, sp, wo, ldir);
+    const float f = fabsf(vdot(sp.N, ldir));
+    // compiled form of surfCol*lcol*|N.l|*transmitCol (transmitCol = 1):
+    // R,G (lcol*surf)*f, B surf*(lcol*f)
+    put_slot(B, slot, SL_TRACED | SL_ADDS,
+             C3((lc.r * surf.r) * f, (lc.g * surf.g) * f, surf.b * (lc.b * f)));
+    return 1;
+  }
   const int n = L.samples;
   const unsigned offs = (unsigned)(n * (int)pixelSample) + soffs + loffs * 4567u;
   const c3 lcol = C3(L.color[0], L.color[1], L.color[2]);
-  const c3 black = C3(0.f, 0.f, 0.f);
   int nr = 0;
   Halton h2, h3;
   hal_start(h2, 2u, offs - 1u);
@@ -869,7 +926,7 @@ __global__ void __launch_bounds__(256) k_shade_primary(DScene S, Batch B, Render
         int k0 = 0;
         for (int l = 0; l < R.nlights; ++l) {
           nr += gen_light(B, c, k0, l, sp, wo, s, B.soffs[c], (unsigned)l, traced);
-          k0 += 2 * c_lights[l].samples;
+          k0 += c_lights[l].nslots;
         }
         kend = k0;
         if (R.integrator == YK_INTEGRATOR_PATH) {
@@ -879,6 +936,8 @@ __global__ void __launch_bounds__(256) k_shade_primary(DScene S, Batch B, Render
         }
       }
       alpha = 1.0f;
+    } else if (R.has_bg) {  // nothing hit: col += (*background)(ray), constant color
+      col = cadd(col, C3(R.bg[0], R.bg[1], R.bg[2]));
     }
     B.prim_hit[c] = ph;
     B.col[3 * c] = col.r;
@@ -900,8 +959,16 @@ __global__ void __launch_bounds__(256) k_shade_primary(DScene S, Batch B, Render
 }
 
 // Sums light li's unoccluded slot contributions in reference order:
-// (0 + invNS*ccol) + invNS*ccol2 (mcintegrator.cc:116-191).
-__device__ __forceinline__ c3 resolve_light(const Batch& B, long long c, int k0, int n) {
+// (0 + invNS*ccol) + invNS*ccol2 (mcintegrator.cc:116-191); Dirac: 0 + v.
+__device__ __forceinline__ c3 resolve_light(const Batch& B, long long c, int k0, int li) {
+  if (c_lights[li].type != YK_LIGHT_AREA) {
+    const long long slot = c * B.K + k0;
+    c3 col = C3(0.f, 0.f, 0.f);
+    if ((B.sl_flags[slot] & SL_ADDS) && !B.s_occl[slot])
+      col = cadd(col, C3(B.sl_contrib[3 * slot], B.sl_contrib[3 * slot + 1], B.sl_contrib[3 * slot + 2]));
+    return col;
+  }
+  const int n = c_lights[li].samples;
   const float invNS = 1.f / (float)n;
   c3 ccol = C3(0.f, 0.f, 0.f), ccol2 = C3(0.f, 0.f, 0.f);
   for (int i = 0; i < 2 * n; ++i) {
@@ -925,9 +992,8 @@ __global__ void __launch_bounds__(256) k_resolve_primary(Batch B, RenderConst R,
   c3 dl = C3(0.f, 0.f, 0.f);
   int k0 = 0;
   for (int l = 0; l < R.nlights; ++l) {
-    const int n = c_lights[l].samples;
-    dl = cadd(dl, resolve_light(B, c, k0, n));
-    k0 += 2 * n;
+    dl = cadd(dl, resolve_light(B, c, k0, l));
+    k0 += c_lights[l].nslots;
   }
   B.col[3 * c] = B.col[3 * c] + dl.r;
   B.col[3 * c + 1] = B.col[3 * c + 1] + dl.g;
@@ -995,7 +1061,7 @@ __global__ void __launch_bounds__(256) k_shade_bounce(DScene S, Batch B, RenderC
         int lnum = (int)(hal_next(h2) * (float)R.nlights);
         if (lnum > R.nlights - 1) lnum = R.nlights - 1;
         nr = gen_light(B, c, 0, lnum, sp, pwo, s, B.soffs[c], (unsigned)lnum, traced);
-        kend = 2 * c_lights[lnum].samples;
+        kend = c_lights[lnum].nslots;
         B.lsel[c] = lnum;
         ps |= PS_EST;
       }
@@ -1048,7 +1114,7 @@ __global__ void __launch_bounds__(256) k_resolve_bounce(Batch B, RenderConst R,
   c3 lcol = C3(0.f, 0.f, 0.f);
   if (ps & PS_EST) {
     const int lnum = B.lsel[c];
-    lcol = cscale((float)R.nlights, resolve_light(B, c, 0, c_lights[lnum].samples));
+    lcol = cscale((float)R.nlights, resolve_light(B, c, 0, lnum));
   }
   if (depth == 1) lcol = cadd(lcol, C3(B.emit_b[3 * c], B.emit_b[3 * c + 1], B.emit_b[3 * c + 2]));
   const c3 thr = C3(B.thr[3 * c], B.thr[3 * c + 1], B.thr[3 * c + 2]);
@@ -1341,7 +1407,9 @@ struct yk_device {
   DBuf<uint2> nodes;
   DBuf<uint32_t> leaf;
   DScene S{};
-  int ntris = 0, max_depth = 0, nlights = 0, sum_light_samples = 0;
+  int ntris = 0, max_depth = 0, nlights = 0, sum_light_slots = 0;
+  bool has_bg = false;
+  float bg[3] = {0.f, 0.f, 0.f};
   Pipe pipe[kPipes];
   hipEvent_t gather_ev[kPipes] = {};
   ~yk_device() {
@@ -1403,6 +1471,23 @@ DLight make_light(const yk_area_light_state& L) {
   }
   D.area = vl;
   D.samples = L.samples;
+  D.type = YK_LIGHT_AREA;
+  D.nslots = 2 * L.samples;
+  return D;
+}
+
+DLight make_dirac_light(const yk_dirac_light_state& L) {
+  DLight D{};
+  D.type = L.type;
+  D.nslots = 1;
+  D.samples = 1;
+  for (int k = 0; k < 3; ++k) {
+    D.pos[k] = L.position[k];
+    D.dir[k] = L.direction[k];
+    D.color[k] = L.color[k];
+  }
+  D.radius = L.radius;
+  D.infinite = L.infinite;
   return D;
 }
 
@@ -1619,14 +1704,20 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   for (const auto& m : S.material_states) mats.push_back(make_mat(m));
   if (!mats.empty()) HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_mats), mats.data(), mats.size() * sizeof(DMat)));
   std::vector<DLight> lights;
-  int sum_samples = 0;
-  for (const auto& l : S.light_states) {
-    if (l.samples < 1) return set_error(YK_ERR_ARG, "light samples must be >= 1");
-    lights.push_back(make_light(l));
-    sum_samples += l.samples;
+  int sum_slots = 0;
+  for (size_t i = 0; i < S.light_states.size(); ++i) {
+    if (S.light_kind[i] == YK_LIGHT_AREA) {
+      if (S.light_states[i].samples < 1) return set_error(YK_ERR_ARG, "light samples must be >= 1");
+      lights.push_back(make_light(S.light_states[i]));
+    } else {
+      lights.push_back(make_dirac_light(S.dirac_states[i]));
+    }
+    sum_slots += lights.back().nslots;
   }
-  if (sum_samples > 4096) return set_error(YK_ERR_UNSUPPORTED, "too many light samples per shading point");
-  d->sum_light_samples = sum_samples;
+  if (sum_slots > 8192) return set_error(YK_ERR_UNSUPPORTED, "too many light samples per shading point");
+  d->sum_light_slots = sum_slots;
+  d->has_bg = S.has_background;
+  for (int k = 0; k < 3; ++k) d->bg[k] = S.background[k];
   if (!lights.empty())
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_lights), lights.data(), lights.size() * sizeof(DLight)));
   const DCam cam = make_cam(S.camera_state);
@@ -1743,8 +1834,10 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   R.integrator = p->integrator;
   R.transp_bg = p->transp_background;
   R.nlights = d->nlights;
+  R.has_bg = d->has_bg ? 1 : 0;
+  for (int k = 0; k < 3; ++k) R.bg[k] = d->bg[k];
   R.d1 = F.d1;
-  const int K = std::max(1, 2 * d->sum_light_samples);
+  const int K = std::max(1, d->sum_light_slots);
   // batch = whole tiles, about YK_BATCH_SAMPLES camera samples (default 32M:
   // each trace launch ends in a tail of long rays, which large batches
   // amortise), capped so the buffers of all pipes stay within ~64 GB of HBM

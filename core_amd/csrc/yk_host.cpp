@@ -156,8 +156,9 @@ int yk_scene_add_curve(yk_scene* s, const float* points, int32_t npoints, int32_
 
 int yk_scene_add_light(yk_scene* s, const yk_light* l) {
   if (!s || !l) return set_error(YK_ERR_ARG, "yk_scene_add_light: NULL argument");
-  if (l->type != YK_LIGHT_AREA) return set_error(YK_ERR_UNSUPPORTED, "light type not supported");
-  if (l->samples < 1) return set_error(YK_ERR_ARG, "area light needs samples >= 1");
+  if (l->type != YK_LIGHT_AREA && l->type != YK_LIGHT_POINT && l->type != YK_LIGHT_DIRECTIONAL)
+    return set_error(YK_ERR_UNSUPPORTED, "light type not supported");
+  if (l->type == YK_LIGHT_AREA && l->samples < 1) return set_error(YK_ERR_ARG, "area light needs samples >= 1");
   YK_GUARD_BEGIN
   s->s.add_light(*l);
   return YK_OK;
@@ -171,6 +172,39 @@ int yk_scene_add_area_light_state(yk_scene* s, const yk_area_light_state* l) {
   s->s.add_light_state(*l);
   return YK_OK;
   YK_GUARD_END
+}
+
+int yk_scene_add_dirac_light_state(yk_scene* s, const yk_dirac_light_state* l) {
+  if (!s || !l) return set_error(YK_ERR_ARG, "yk_scene_add_dirac_light_state: NULL argument");
+  if (l->type != YK_LIGHT_POINT && l->type != YK_LIGHT_DIRECTIONAL)
+    return set_error(YK_ERR_ARG, "yk_scene_add_dirac_light_state: type must be point or directional");
+  YK_GUARD_BEGIN
+  s->s.add_dirac_light_state(*l);
+  return YK_OK;
+  YK_GUARD_END
+}
+
+int yk_scene_get_dirac_light_state(const yk_scene* s, int32_t i, yk_dirac_light_state* out) {
+  if (!s || !out || i < 0 || i >= (int32_t)s->s.dirac_states.size())
+    return set_error(YK_ERR_ARG, "yk_scene_get_dirac_light_state: bad arguments");
+  if (s->s.light_kind[i] == YK_LIGHT_AREA) return set_error(YK_ERR_STATE, "light is an area light");
+  *out = s->s.dirac_states[i];
+  return YK_OK;
+}
+
+int yk_scene_set_background(yk_scene* s, const float* rgb, float power) {
+  if (!s) return set_error(YK_ERR_ARG, "yk_scene_set_background: NULL scene");
+  s->s.has_background = rgb != nullptr;
+  for (int k = 0; k < 3; ++k) s->s.background[k] = rgb ? rgb[k] * power : 0.f;  // col*power, textureback.cc:218
+  return YK_OK;
+}
+
+int yk_scene_get_background(const yk_scene* s, float* rgb_out, int32_t* has_out) {
+  if (!s) return set_error(YK_ERR_ARG, "yk_scene_get_background: NULL scene");
+  if (rgb_out)
+    for (int k = 0; k < 3; ++k) rgb_out[k] = s->s.background[k];
+  if (has_out) *has_out = s->s.has_background ? 1 : 0;
+  return YK_OK;
 }
 
 int yk_scene_set_camera(yk_scene* s, const yk_camera* c) {
@@ -199,6 +233,7 @@ int yk_scene_get_material_state(const yk_scene* s, int32_t i, yk_material_state*
 int yk_scene_get_area_light_state(const yk_scene* s, int32_t i, yk_area_light_state* out) {
   if (!s || !out || i < 0 || i >= (int32_t)s->s.light_states.size())
     return set_error(YK_ERR_ARG, "yk_scene_get_area_light_state: bad arguments");
+  if (s->s.light_kind[i] != YK_LIGHT_AREA) return set_error(YK_ERR_STATE, "light is not an area light");
   *out = s->s.light_states[i];
   return YK_OK;
 }

@@ -80,6 +80,32 @@ class Scene:
                        power, samples)
         A.check(A.lib().yk_scene_add_light(self._p, C.byref(l)))
 
+    def add_point_light(self, from_, color=(1, 1, 1), power=1.0):
+        """pointlight (pointlight.cc:129-139)"""
+        l = A.yk_light(type=A.YK_LIGHT_POINT, color=A.f3(*color), power=power, from_=A.f3(*from_))
+        A.check(A.lib().yk_scene_add_light(self._p, C.byref(l)))
+
+    def add_directional_light(self, direction, color=(1, 1, 1), power=1.0, infinite=True, from_=(0, 0, 0),
+                              radius=1.0):
+        """directional (directional.cc:139-165)"""
+        l = A.yk_light(type=A.YK_LIGHT_DIRECTIONAL, color=A.f3(*color), power=power, from_=A.f3(*from_),
+                       direction=A.f3(*direction), radius=radius, infinite=int(infinite))
+        A.check(A.lib().yk_scene_add_light(self._p, C.byref(l)))
+
+    def set_background(self, color, power=1.0):
+        """constant background (textureback.cc:206-218, ibl off); None removes it"""
+        if color is None:
+            A.check(A.lib().yk_scene_set_background(self._p, None, 0.0))
+        else:
+            rgb = (C.c_float * 3)(*color)
+            A.check(A.lib().yk_scene_set_background(self._p, rgb, power))
+
+    def background(self):
+        rgb = (C.c_float * 3)()
+        has = C.c_int32()
+        A.check(A.lib().yk_scene_get_background(self._p, rgb, C.byref(has)))
+        return tuple(rgb) if has.value else None
+
     def set_camera(self, from_, to, up, resx, resy, focal=1.0, aspect_ratio=1.0, near_clip=0.0,
                    far_clip=-1.0):
         c = A.yk_camera(A.f3(*from_), A.f3(*to), A.f3(*up), resx, resy, focal, aspect_ratio, near_clip,
@@ -113,11 +139,17 @@ class Scene:
             out.append(m)
         return out
 
+    def add_dirac_light_state(self, st):
+        A.check(A.lib().yk_scene_add_dirac_light_state(self._p, C.byref(st)))
+
     def light_states(self):
+        """Per light: yk_area_light_state or yk_dirac_light_state."""
         out = []
         for k in range(self.info().nlights):
             m = A.yk_area_light_state()
-            A.check(A.lib().yk_scene_get_area_light_state(self._p, k, C.byref(m)))
+            if A.lib().yk_scene_get_area_light_state(self._p, k, C.byref(m)) == A.YK_ERR_STATE:
+                m = A.yk_dirac_light_state()
+                A.check(A.lib().yk_scene_get_dirac_light_state(self._p, k, C.byref(m)))
             out.append(m)
         return out
 

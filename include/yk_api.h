@@ -50,13 +50,21 @@ typedef struct yk_material {
   int32_t double_sided;   /* "double_sided" (light_mat, default 0)                  */
 } yk_material;
 
-enum { YK_LIGHT_AREA = 0 };
-typedef struct yk_light { /* areaLight_t::factory, arealight.cc:171-192 */
+enum { YK_LIGHT_AREA = 0, YK_LIGHT_POINT = 1, YK_LIGHT_DIRECTIONAL = 2 };
+typedef struct yk_light {
   int32_t type;
+  /* area: areaLight_t::factory, arealight.cc:171-192 */
   float corner[3], point1[3], point2[3];
   float color[3];
   float power;
   int32_t samples;
+  /* point: pointLight_t::factory (pointlight.cc:129-139), position = from;
+   * directional: directionalLight_t::factory (directional.cc:139-165):
+   * direction, and from/radius when infinite == 0 */
+  float from[3];
+  float direction[3];
+  float radius;
+  int32_t infinite;
 } yk_light;
 
 typedef struct yk_camera { /* perspectiveCam_t::factory, perspectiveCamera.cc:191-232 */
@@ -198,6 +206,15 @@ typedef struct yk_area_light_state { /* areaLight_t members (arealight.h:45-53) 
   int32_t samples;
 } yk_area_light_state;
 
+typedef struct yk_dirac_light_state { /* pointLight_t / directionalLight_t members after their ctors */
+  int32_t type;          /* YK_LIGHT_POINT or YK_LIGHT_DIRECTIONAL                                  */
+  float position[3];     /* pointLight_t::position / directionalLight_t::position                  */
+  float direction[3];    /* directional: normalized (directional.cc:53)                             */
+  float color[3];        /* color * power (pointlight.cc:55, directional.cc:51)                     */
+  float radius;          /* directional, non-infinite                                              */
+  int32_t infinite;
+} yk_dirac_light_state;
+
 typedef struct yk_camera_state { /* perspectiveCam_t after setAxis (perspectiveCamera.cc:57-71) */
   float position[3], vright[3], vup[3], vto[3], cam_z[3];
   float near_p[3], far_p[3]; /* near_plane.p / far_plane.p (camera.h:54-57)            */
@@ -206,6 +223,15 @@ typedef struct yk_camera_state { /* perspectiveCam_t after setAxis (perspectiveC
 
 int yk_scene_add_material_state(yk_scene* s, const yk_material_state* m, int32_t* id_out);
 int yk_scene_add_area_light_state(yk_scene* s, const yk_area_light_state* l);
+/* point / directional light (light_t::diracLight() == true): one shadow ray
+ * per estimate, mcintegrator.cc:85-100 */
+int yk_scene_add_dirac_light_state(yk_scene* s, const yk_dirac_light_state* l);
+int yk_scene_get_dirac_light_state(const yk_scene* s, int32_t i, yk_dirac_light_state* out);
+/* constBackground_t (textureback.cc:187-218, "constant", ibl off): camera
+ * rays that miss add color*power. rgb NULL removes the background. */
+int yk_scene_set_background(yk_scene* s, const float* rgb, float power);
+/* has_out = 0 when the scene has no background */
+int yk_scene_get_background(const yk_scene* s, float* rgb_out, int32_t* has_out);
 int yk_scene_set_camera_state(yk_scene* s, const yk_camera_state* c);
 int yk_scene_get_material_state(const yk_scene* s, int32_t i, yk_material_state* out);
 int yk_scene_get_area_light_state(const yk_scene* s, int32_t i, yk_area_light_state* out);

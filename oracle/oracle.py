@@ -27,6 +27,7 @@ def lib():
         vp = C.c_void_p
         L.orc_load.argtypes = [vp, vp, C.c_int32, vp, vp, vp, vp, C.c_int32, vp, C.c_int32, vp]
         L.orc_set_shading.argtypes = [vp, vp, vp]
+        L.orc_set_background.argtypes = [vp]
         L.orc_intersect.argtypes = [vp, C.c_int64, vp, vp]
         L.orc_shadow.argtypes = [vp, C.c_int64, vp, vp]
         L.orc_render.argtypes = [vp, vp, vp, vp]
@@ -66,6 +67,8 @@ class Oracle:
         self._cam = scene.camera()
         self._nmats, self._nlights = len(mats), len(lights)
         self.instanced = bool(getattr(scene, "instanced", False))
+        bg = scene.background()
+        self._bg = None if bg is None else (C.c_float * 3)(*bg)
         self._activate()
 
     def _activate(self):
@@ -79,6 +82,7 @@ class Oracle:
                        C.addressof(self._cam))
         # instanced / smooth scenes: the geometric normals and vertex normals
         # of the host flattening (checked separately by tests/test_instances.py)
+        lib().orc_set_background(None if self._bg is None else C.addressof(self._bg))
         if e["tri_smooth"].any() or self.instanced:
             lib().orc_set_shading(e["tri_normal"].ctypes.data, e["tri_smooth"].ctypes.data,
                                   e["tri_vnormal"].ctypes.data)

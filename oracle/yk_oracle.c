@@ -262,7 +262,14 @@ typedef struct {
     col3 color;
     float area, inv_area;
     int samples;
+    /* point / directional lights (pointlight.cc:53-58, directional.cc:50-58) */
+    int type;
+    v3 pos, dir;
+    float radius;
+    int infinite;
   } * al;
+  int has_bg;  /* constBackground_t, textureback.cc:187-218 */
+  col3 bg;
   /* derived camera data, camera.h:41-60 + perspectiveCamera.cc:28-71 */
   v3 cam_pos, vright, vup, vto, camZ;
   v3 near_p, far_p;
@@ -622,6 +629,17 @@ static void lights_setup(void) {
   for (int i = 0; i < G.nlights; ++i) {
     const yk_light* L = &G.lights[i];
     struct arealight* A = &G.al[i];
+    A->type = L->type;
+    if (L->type != YK_LIGHT_AREA) {
+      /* color = col * inte; directional: direction.normalize() */
+      A->color = C(L->color[0] * L->power, L->color[1] * L->power, L->color[2] * L->power);
+      A->pos = V(L->from[0], L->from[1], L->from[2]);
+      A->dir = vnormalize(V(L->direction[0], L->direction[1], L->direction[2]));
+      A->radius = L->radius;
+      A->infinite = L->infinite;
+      A->samples = 1;
+      continue;
+    }
     v3 corner = V(L->corner[0], L->corner[1], L->corner[2]);
     v3 p1 = V(L->point1[0], L->point1[1], L->point1[2]);
     v3 p2 = V(L->point2[0], L->point2[1], L->point2[2]);
@@ -685,6 +703,37 @@ static int al_intersect(const struct arealight* A, v3 from, v3 dir, float* t, co
   return 1;
 }
 
+/* pointLight_t::illuminate, pointlight.cc:60-75 */
+static int point_illuminate(const struct arealight* A, v3 P, col3* col, v3* dir, float* tmax) {
+  v3 ldir = vsub(A->pos, P);
+  float dist_sqr = ldir.x * ldir.x + ldir.y * ldir.y + ldir.z * ldir.z;
+  float dist = sqrtf(dist_sqr);
+  if (dist == 0.0f) return 0;
+  float idist_sqr = 1.f / dist_sqr;
+  float inv = 1.f / dist;
+  *dir = V(ldir.x * inv, ldir.y * inv, ldir.z * inv);
+  *tmax = dist;
+  *col = C(A->color.r * idist_sqr, A->color.g * idist_sqr, A->color.b * idist_sqr);
+  return 1;
+}
+
+/* directionalLight_t::illuminate, directional.cc:77-96 */
+static int dir_illuminate(const struct arealight* A, v3 P, col3* col, v3* dir, float* tmax) {
+  if (!A->infinite) {
+    v3 vec = vsub(A->pos, P);
+    v3 cr = vcross(A->dir, vec);
+    float dist = sqrtf(vdot(cr, cr));
+    if (dist > A->radius) return 0;
+    *tmax = vdot(vec, A->dir);
+    if (*tmax <= 0.0f) return 0;
+  } else {
+    *tmax = -1.0f;
+  }
+  *dir = A->dir;
+  *col = A->color;
+  return 1;
+}
+
 /* ------------------------------------------------------ integrators -- */
 
 typedef struct {
@@ -698,6 +747,21 @@ static col3 do_light_estimation(rstate* st, int li, const surfpt* sp, v3 wo, uns
   col3 col = C(0, 0, 0);
   const struct arealight* A = &G.al[li];
   const yk_material* M = mat_of(sp->mat);
+  if (A->type != YK_LIGHT_AREA) { /* diracLight(): mcintegrator.cc:85-100 */
+    col3 lcol;
+    v3 ldir;
+    float ltmax;
+    int ok = A->type == YK_LIGHT_POINT ? point_illuminate(A, sp->P, &lcol, &ldir, &ltmax)
+                                       : dir_illuminate(A, sp->P, &lcol, &ldir, &ltmax);
+    if (ok && !scene_shadowed(sp->P, ldir, SHADOW_BIAS, ltmax)) {
+      col3 surf = sd_eval(M, sp, wo, ldir, BSDF_ALL);
+      float f = fabsf(vdot(sp->N, ldir));
+      /* compiled form of surfCol*lcol*|N.l|*transmitCol, transmitCol = 1:
+       * R,G (lcol*surf)*f; B surf*(lcol*f) (SLP pair + scalar lane) */
+      col = cadd(col, C((lcol.r * surf.r) * f, (lcol.g * surf.g) * f, surf.b * (lcol.b * f)));
+    }
+    return col;
+  }
   unsigned l_offs = loffs * 4567u;
   int n = A->samples;
   float invNS = 1.f / (float)n;
@@ -853,6 +917,8 @@ static rgba pt_integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir,
       col = cadd(col, C(pathCol.r / ns, pathCol.g / ns, pathCol.b / ns));
     }
     alpha = 1.0f; /* getAlpha of opaque shinydiffuse/light_mat = 1 */
+  } else if (G.has_bg) { /* nothing hit, return background (pathtracer.cc:318-324) */
+    col = cadd(col, G.bg);
   }
   rgba r = {col.r, col.g, col.b, alpha};
   return r;
@@ -871,6 +937,8 @@ static rgba dl_integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir,
     if (bsdfs & BSDF_EMIT) col = cadd(col, mat_emit(M, &sp, wo, st->includeLights));
     if (bsdfs & BSDF_DIFFUSE) col = cadd(col, estimate_all_direct(st, &sp, wo));
     alpha = 1.0f;
+  } else if (G.has_bg) { /* directlight.cc:163-166 */
+    col = cadd(col, G.bg);
   }
   rgba r = {col.r, col.g, col.b, alpha};
   return r;
@@ -972,6 +1040,13 @@ int orc_load(const float* tri_verts, const int32_t* tri_mat, int32_t ntris, cons
   }
   camera_setup();
   lights_setup();
+  return 0;
+}
+
+/* constant background color (already color*power); NULL = none */
+int orc_set_background(const float* rgb) {
+  G.has_bg = rgb != NULL;
+  G.bg = rgb ? C(rgb[0], rgb[1], rgb[2]) : C(0, 0, 0);
   return 0;
 }
 

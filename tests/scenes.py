@@ -84,3 +84,23 @@ def smooth_instanced(resx, resy, integrator="cornell_pt", nu=14, nv=9, smooth=Tr
     s.build()
     parts = dict(base=base, instances=inst, regular=reg, sphere=(pts, faces, nrm), sphere2=(pts2, faces2, nrm2, fn2))
     return s, p, parts
+
+
+BACKGROUND = ((0.2, 0.3, 0.45), 0.8)
+
+
+def dirac_lights(resx, resy, integrator="cornell_pt", with_dirac=True):
+    """Cornell box + a point light, an infinite and a finite directional light
+    (mcintegrator.cc:85-100 Dirac branch) and a constant background
+    (textureback.cc:187-218) seen around the box."""
+    s = Scene()
+    p = s.generate(integrator, resx, resy)
+    s.set_camera((0, 1, -5.4), (0, 1, 0), (0, 2, -5.4), resx, resy, focal=1.3)  # box + background around it
+    if with_dirac:
+        s.add_point_light((0.35, 1.55, -0.3), (1.0, 0.9, 0.7), 0.5)
+        s.add_directional_light((0.35, 0.45, -1.0), (0.6, 0.7, 1.0), 0.3)  # through the open front
+        s.add_directional_light((0.0, 0.1, -1.0), (1.0, 1.0, 1.0), 0.5, infinite=False,
+                                from_=(-0.3, 0.9, -3.0), radius=0.45)
+    s.set_background(*BACKGROUND)
+    s.build()
+    return s, p

@@ -13,7 +13,7 @@ from core_amd import _abi as A
 from core_amd.scene import probe_scene
 from oracle.oracle import Oracle
 from tests.raygen import edge_rays, random_rays
-from tests.scenes import smooth_instanced
+from tests.scenes import dirac_lights, smooth_instanced
 
 pytestmark = pytest.mark.gpu
 
@@ -23,9 +23,11 @@ _SCENES = {}
 def scene(name, resx, resy, nu=0, nv=0):
     key = (name, resx, resy, nu, nv)
     if key not in _SCENES:
+        gen = "cornell_dl" if name.endswith("_dl") else "cornell_pt"
         if name.startswith("smooth_inst"):  # instances + smooth normals (§8 a6/a7), tests/scenes.py
-            gen = "cornell_dl" if name.endswith("_dl") else "cornell_pt"
             s, p, _ = smooth_instanced(resx, resy, gen)
+        elif name.startswith("dirac"):  # point + directional lights, constant background (§8 f1)
+            s, p = dirac_lights(resx, resy, gen)
         else:
             s, p = probe_scene(name, resx, resy, nu, nv)
         _SCENES[key] = (s, p, Oracle(s))
@@ -114,6 +116,10 @@ RENDER_CASES = [
     ("dl_smooth_inst", ("smooth_inst_dl", 80, 80, 0, 0), (0, 0, 80, 80), {}),
     # C5 shape: hair strands (curve meshes), 8 bounces, two area lights
     ("pt_hair", ("hair", 64, 64, 3000, 9), (0, 0, 64, 64), {}),
+    # Dirac lights + constant background (§8 f1): oracle restatement, parity unpinned vs reference outputs
+    ("pt_dirac_bg", ("dirac", 72, 72, 0, 0), (0, 0, 72, 72), {}),
+    ("dl_dirac_bg", ("dirac_dl", 72, 72, 0, 0), (0, 0, 72, 72), {}),
+    ("pt_dirac_bg_opaque", ("dirac", 72, 72, 0, 0), (4, 4, 60, 60), {"transp_background": 0, "path_samples": 2}),
 ]
 
 
