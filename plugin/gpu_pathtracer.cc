@@ -27,6 +27,8 @@
 
 #include <cstring>
 #include <map>
+#include <string>
+#include <typeinfo>
 #include <vector>
 
 #include "yk_api.h"
@@ -90,6 +92,32 @@ YK_MEMBER(FilmFilterW, imageFilm_t, float, filterw)
 YK_MEMBER(FilmTable, imageFilm_t, float*, filterTable)
 YK_MEMBER(FilmTileSize, imageFilm_t, int, tileSize)
 #define GET(obj, Tag) ((obj).*member_of<Tag>::ptr)
+
+// pointLight_t, directionalLight_t and constBackground_t are defined inside
+// their plugins' .cc files (pointlight.cc:27-45, directional.cc:27-50,
+// textureback.cc:59-69), so no header declares them. These mirror their
+// member layout (same compiler and ABI as the reference build, SURVEY.md
+// §8(b)); the object is identified by its typeid name before the cast.
+// The integrator never constructs them.
+struct PointLightLayout : public light_t {
+  point3d_t position;
+  color_t color;
+  float intensity;
+};
+struct DirectionalLightLayout : public light_t {
+  point3d_t position;
+  color_t color;
+  vector3d_t direction, du, dv;
+  float intensity;
+  PFLOAT radius;
+  float areaPdf;
+  PFLOAT worldRadius;
+  bool infinite;
+  int majorAxis;
+};
+struct ConstBackgroundLayout : public background_t {
+  color_t color;
+};
 
 static void put3(float* d, float x, float y, float z) { d[0] = x; d[1] = y; d[2] = z; }
 
@@ -165,8 +193,30 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
       }
     }
     for (light_t* l : scene->lights) {
+      const std::string tn = typeid(*l).name();
+      if (tn == "N7yafaray12pointLight_tE") {
+        const PointLightLayout* pl = static_cast<const PointLightLayout*>(l);
+        yk_dirac_light_state d{};
+        d.type = YK_LIGHT_POINT;
+        put3(d.position, pl->position.x, pl->position.y, pl->position.z);
+        put3(d.color, pl->color.R, pl->color.G, pl->color.B);
+        if (yk_scene_add_dirac_light_state(ys, &d) != YK_OK) return fail();
+        continue;
+      }
+      if (tn == "N7yafaray18directionalLight_tE") {
+        const DirectionalLightLayout* dl = static_cast<const DirectionalLightLayout*>(l);
+        yk_dirac_light_state d{};
+        d.type = YK_LIGHT_DIRECTIONAL;
+        put3(d.position, dl->position.x, dl->position.y, dl->position.z);
+        put3(d.direction, dl->direction.x, dl->direction.y, dl->direction.z);
+        put3(d.color, dl->color.R, dl->color.G, dl->color.B);
+        d.radius = dl->radius;
+        d.infinite = dl->infinite ? 1 : 0;
+        if (yk_scene_add_dirac_light_state(ys, &d) != YK_OK) return fail();
+        continue;
+      }
       areaLight_t* al = dynamic_cast<areaLight_t*>(l);
-      if (!al) return unsupported("only area lights run on the GPU path");
+      if (!al) return unsupported("only area, point and directional lights run on the GPU path");
       yk_area_light_state s{};
       const point3d_t& c = GET(*al, AlCorner);
       const vector3d_t &x = GET(*al, AlToX), &y = GET(*al, AlToY);
@@ -177,6 +227,13 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
       put3(s.color, col.R, col.G, col.B);
       s.samples = GET(*al, AlSamples);
       if (yk_scene_add_area_light_state(ys, &s) != YK_OK) return fail();
+    }
+    if (const background_t* bg = scene->getBackground()) {
+      if (std::string(typeid(*bg).name()) != "N7yafaray17constBackground_tE")
+        return unsupported("only the constant background runs on the GPU path");
+      const color_t& c = static_cast<const ConstBackgroundLayout*>(bg)->color;
+      const float rgb[3] = {c.R, c.G, c.B};
+      if (yk_scene_set_background(ys, rgb, 1.0f) != YK_OK) return fail();  // color already * power
     }
     const perspectiveCam_t* cam = dynamic_cast<const perspectiveCam_t*>(scene->getCamera());
     if (!cam) return unsupported("only the perspective camera runs on the GPU path");
