@@ -35,7 +35,8 @@ void put(float* d, hv3 v) {
   d[1] = v.y;
   d[2] = v.z;
 }
-constexpr unsigned kDiffuse = 0x4u, kReflect = 0x10u, kEmit = 0x80u;  // material.h:49-66
+constexpr unsigned kSpecular = 0x1u, kDiffuse = 0x4u, kReflect = 0x10u, kTransmit = 0x20u, kFilter = 0x40u,
+                   kEmit = 0x80u;  // material.h:49-66
 }  // namespace
 
 yk_material_state material_state(const yk_material& m) {
@@ -45,14 +46,42 @@ yk_material_state material_state(const yk_material& m) {
     o.bsdf_flags = kEmit;
     for (int k = 0; k < 3; ++k) o.color[k] = m.color[k] * m.power;
     o.double_sided = m.double_sided;
-  } else {  // shinyDiffuseMat_t ctor, shinydiffuse.cc:9-60
+  } else {  // shinyDiffuseMat_t ctor + factory + config(), shinydiffuse.cc:9-80,474-562
     if (m.emit > 0.f) o.bsdf_flags |= kEmit;
-    if (m.diffuse_reflect > 0.00001f) o.bsdf_flags |= kDiffuse | kReflect;
     for (int k = 0; k < 3; ++k) {
       o.color[k] = m.color[k];
       o.emit_color[k] = m.emit * m.color[k];
+      o.mirror_color[k] = m.mirror_color[k];
     }
     o.diffuse_strength = m.diffuse_reflect;
+    o.transmit_filter = m.transmit_filter;
+    if (m.fresnel_effect) {
+      o.has_fresnel = 1;
+      o.ior_squared = (float)(m.ior * m.ior);
+    }
+    float acc = 1.f;
+    int n = 0;
+    auto add = [&](unsigned flags, int index, float strength) {
+      o.bsdf_flags |= flags;
+      o.comp_flags[n] = flags;
+      o.comp_index[n] = index;
+      o.component[index] = strength;
+      ++n;
+    };
+    if (m.specular_reflect > 0.00001f) {
+      if (!o.has_fresnel) acc = 1.f - m.specular_reflect;
+      add(kSpecular | kReflect, 0, m.specular_reflect);
+    }
+    if (m.transparency * acc > 0.00001f) {
+      acc *= 1.f - m.transparency;
+      add(kTransmit | kFilter, 1, m.transparency);
+    }
+    if (m.translucency * acc > 0.00001f) {
+      acc *= 1.f - m.transparency;  // sic, shinydiffuse.cc:59
+      add(kDiffuse | kTransmit, 2, m.translucency);
+    }
+    if (m.diffuse_reflect * acc > 0.00001f) add(kDiffuse | kReflect, 3, m.diffuse_reflect);
+    o.ncomp = n;
   }
   return o;
 }
@@ -395,6 +424,9 @@ int add_mat(Scene& s, int type, float r, float g, float b, float power) {
   m.emit = 0.f;
   m.power = power;
   m.double_sided = 0;
+  m.mirror_color[0] = m.mirror_color[1] = m.mirror_color[2] = 1.f;  // factory defaults
+  m.transmit_filter = 1.f;
+  m.ior = 1.33;
   return s.add_material(m);
 }
 

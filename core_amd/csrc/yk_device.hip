@@ -44,9 +44,18 @@ struct DMat {
   int type;
   unsigned flags;
   float col[3];       // diffuse colour (shinydiffuse) / lightCol = col*power (light_mat)
-  float diffuse;      // component[3] = diffuse strength (shinydiffuse.cc:98-101)
   float emit_col[3];  // mEmitColor = emit * color (shinydiffuse.cc:12)
   int double_sided;
+  // shinyDiffuseMat_t after config() (shinydiffuse.cc:27-80)
+  float comp[4];      // getComponents: mirror, transparency, translucency, diffuse
+  float mirror[3];    // mMirrorColor
+  int ncomp;          // nBSDF
+  unsigned cflags[4]; // cFlags
+  int cindex[4];      // cIndex
+  float tfilter;      // mTransmitFilterStrength
+  int fresnel;        // mHasFresnelEffect
+  float ior2;         // mIOR_Squared
+  int translucent;    // mIsTranslucent
 };
 
 struct DLight {  // areaLight_t members after its constructor (arealight.cc:30-49)
@@ -477,23 +486,53 @@ __device__ __forceinline__ SurfPt make_surface(const DScene& S, v3 from, v3 dir,
   return sp;
 }
 
-// shinyDiffuseMat_t::eval (diffuse subset), shinydiffuse.cc:223-249 (compiled
-// order of mD: ((1-c2)*c3)*mT)
+// getFresnel, shinydiffuse.cc:100-122. Compiled form: c = |N.wo| (the
+// face-forward sign folded into fabs), g tested as ior2 + c*c < 1,
+// 0.5*(g-c)^2 as ((g-c)*(g-c))*0.5, aux = (g+c)*c.
+__device__ __forceinline__ float mat_fresnel(const DMat& M, v3 wo, v3 N) {
+  if (!M.fresnel) return 1.f;
+  const float c = fabsf(N.x * wo.x + N.y * wo.y + N.z * wo.z);
+  const float t = M.ior2 + c * c;
+  const float g = (t < 1.f) ? 0.f : sqrtf(t - 1.f);
+  const float gc = g + c, aux = gc * c;
+  const float a = (((g - c) * (g - c)) * 0.5f) / (gc * gc);
+  const float b = ((aux - 1.f) * (aux - 1.f)) / ((aux + 1.f) * (aux + 1.f)) + 1.f;
+  return b * a;
+}
+
+// accumulate(), shinydiffuse.cc:124-133; compiled: accum3 = ((1-c2)*c3)*acc
+__device__ __forceinline__ void mat_accum(const DMat& M, float Kr, float* a) {
+  a[0] = Kr * M.comp[0];
+  const float t = 1.f - a[0];
+  a[1] = t * M.comp[1];
+  const float acc2 = (1.f - M.comp[1]) * t;
+  a[2] = acc2 * M.comp[2];
+  a[3] = ((1.f - M.comp[2]) * M.comp[3]) * acc2;
+}
+
+// shinyDiffuseMat_t::eval, shinydiffuse.cc:223-249 (compiled: cos_Ng_wl as
+// (y + z) + x; mD = ((1-c2)*c3)*mT)
 __device__ __forceinline__ c3 mat_eval(const DMat& M, const SurfPt& sp, v3 wo, v3 wl) {
   if (M.type == YK_MAT_LIGHT) return C3(0.f, 0.f, 0.f);
-  v3 N = (vdot(sp.Ng, wo) < 0.f) ? vneg(sp.N) : sp.N;
+  const float cos_Ng_wo = vdot(sp.Ng, wo);
+  const float cos_Ng_wl = (sp.Ng.y * wl.y + sp.Ng.z * wl.z) + sp.Ng.x * wl.x;
+  const v3 N = (cos_Ng_wo < 0.f) ? vneg(sp.N) : sp.N;
   if (!(M.flags & BSDF_DIFFUSE)) return C3(0.f, 0.f, 0.f);
-  const float mT = (1.f - 0.f) * (1.f - 0.f);
-  if (vdot(N, wl) < 0.0f) return C3(0.f, 0.f, 0.f);
-  const float mD = ((1.f - 0.f) * M.diffuse) * mT;
+  const float Kr = mat_fresnel(M, wo, N);
+  const float mT = (1.f - Kr * M.comp[0]) * (1.f - M.comp[1]);
+  if (cos_Ng_wo * cos_Ng_wl < 0.f && M.translucent) return cscale(mT * M.comp[2], C3(M.col[0], M.col[1], M.col[2]));
+  if (vdot(wl, N) < 0.0f) return C3(0.f, 0.f, 0.f);
+  const float mD = ((1.f - M.comp[2]) * M.comp[3]) * mT;
   return cscale(mD, C3(M.col[0], M.col[1], M.col[2]));
 }
 
-// shinyDiffuseMat_t::sample, diffuse-reflect component (shinydiffuse.cc:259-336);
-// lightMat_t::sample (simple.cc:47-52). ok=false: early return, W untouched.
+// shinyDiffuseMat_t::sample, shinydiffuse.cc:259-336; lightMat_t::sample
+// (simple.cc:55-60). ok=false: early return with W and wi untouched.
+// sflags = s.sampledFlags.
 __device__ __forceinline__ c3 mat_sample(const DMat& M, const SurfPt& sp, v3 wo, v3& wi, float s1in, float s2in,
-                                         unsigned flags, float& pdf, float& W, bool& ok) {
+                                         unsigned flags, float& pdf, float& W, bool& ok, unsigned& sflags) {
   ok = true;
+  sflags = 0u;
   if (M.type == YK_MAT_LIGHT) {
     pdf = 0.f;
     W = 0.f;
@@ -501,41 +540,139 @@ __device__ __forceinline__ c3 mat_sample(const DMat& M, const SurfPt& sp, v3 wo,
   }
   const float cos_Ng_wo = vdot(sp.Ng, wo);
   const v3 N = (cos_Ng_wo < 0.f) ? vneg(sp.N) : sp.N;
-  const float accum3 = M.diffuse * (((1.f - 0.f * 1.f) * (1.f - 0.f)) * (1.f - 0.f));
-  const unsigned cf = BSDF_DIFFUSE | BSDF_REFLECT;
-  if (!(M.flags & BSDF_DIFFUSE) || (flags & cf) != cf) {
-    pdf = 0.f;
-    ok = false;
-    return C3(1.f, 1.f, 1.f);
+  const float Kr = mat_fresnel(M, wo, N);
+  float a[4];
+  mat_accum(M, Kr, a);
+  float sum = 0.f, val[4], width[4];
+  unsigned choice[4];
+  int nMatch = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i < M.ncomp && (flags & M.cflags[i]) == M.cflags[i]) {
+      const int ci = M.cindex[i];
+      const float w = ci == 0 ? a[0] : (ci == 1 ? a[1] : (ci == 2 ? a[2] : a[3]));
+      width[nMatch] = w;
+      sum += w;
+      choice[nMatch] = M.cflags[i];
+      val[nMatch] = sum;
+      ++nMatch;
+    }
   }
-  float width = accum3;
-  const float sum = 0.f + width;
-  if (sum < 0.00001f) {
+  if (!nMatch || (double)sum < 0.00001) {
     pdf = 0.f;
     ok = false;
     return C3(1.f, 1.f, 1.f);
   }
   const float inv_sum = 1.f / sum;
-  width *= inv_sum;
-  const float s1 = s1in / width;
-  wi = sample_cos_hemisphere(N, sp.NU, sp.NV, s1, s2in);
-  const float cos_Ng_wi = vdot(sp.Ng, wi);
+  int pick = -1;
+  for (int i = 0; i < nMatch; ++i) {
+    val[i] *= inv_sum;
+    width[i] *= inv_sum;
+    if ((s1in <= val[i]) && (pick < 0)) pick = i;
+  }
+  if (pick < 0) pick = nMatch - 1;
+  const float wp = width[pick];
+  const float s1 = (pick > 0) ? (s1in - val[pick - 1]) / wp : s1in / wp;
+  const c3 dcol = C3(M.col[0], M.col[1], M.col[2]);
   c3 sc = C3(0.f, 0.f, 0.f);
-  if (cos_Ng_wo * cos_Ng_wi > 0.f) sc = cscale(accum3, C3(M.col[0], M.col[1], M.col[2]));
-  pdf = fabsf(vdot(wi, N)) * width;
-  W = fabsf(vdot(wi, sp.N)) / (pdf * 0.99f + 0.01f);
+  v3 w;
+  const unsigned ch = choice[pick];
+  if (ch == (BSDF_SPECULAR | BSDF_REFLECT)) {  // reflect_dir(N, wo), compiled vn = (x + z) + y
+    const float vn = (wo.x * N.x + wo.z * N.z) + N.y * wo.y;
+    if (vn < 0.f) {
+      w = vneg(wo);
+    } else {
+      const float v2 = vn + vn;
+      w = V3(v2 * N.x - wo.x, v2 * N.y - wo.y, v2 * N.z - wo.z);
+    }
+    pdf = wp;
+    sc = C3(M.mirror[0] * a[0], M.mirror[1] * a[0], M.mirror[2] * a[0]);
+    const float k = 1.f / fabsf(vdot(w, sp.N));
+    sc = C3(sc.r * k, sc.g * k, sc.b * k);
+  } else if (ch == (BSDF_TRANSMIT | BSDF_FILTER)) {
+    w = vneg(wo);
+    const float t = 1.f - M.tfilter;
+    sc = C3((dcol.r * M.tfilter + t) * a[1], (dcol.g * M.tfilter + t) * a[1], (dcol.b * M.tfilter + t) * a[1]);
+    const float cosN = fabsf(vdot(N, w));
+    pdf = ((double)cosN < 1e-6) ? 0.f : wp;
+  } else if (ch == (BSDF_DIFFUSE | BSDF_TRANSMIT)) {
+    w = sample_cos_hemisphere(vneg(N), sp.NU, sp.NV, s1, s2in);
+    if (cos_Ng_wo * vdot(sp.Ng, w) < 0.f) sc = cscale(a[2], dcol);
+    pdf = fabsf(vdot(N, w)) * wp;
+  } else {
+    w = sample_cos_hemisphere(N, sp.NU, sp.NV, s1, s2in);
+    if (cos_Ng_wo * vdot(sp.Ng, w) > 0.f) sc = cscale(a[3], dcol);
+    pdf = fabsf(vdot(N, w)) * wp;
+  }
+  wi = w;
+  sflags = ch;
+  W = fabsf(vdot(w, sp.N)) / (pdf * 0.99f + 0.01f);
   return sc;
 }
+__device__ __forceinline__ c3 mat_sample(const DMat& M, const SurfPt& sp, v3 wo, v3& wi, float s1in, float s2in,
+                                         unsigned flags, float& pdf, float& W, bool& ok) {
+  unsigned sf;
+  return mat_sample(M, sp, wo, wi, s1in, s2in, flags, pdf, W, ok, sf);
+}
 
-// shinyDiffuseMat_t::pdf, shinydiffuse.cc:338-377
+// shinyDiffuseMat_t::pdf, shinydiffuse.cc:338-377: every component sharing a
+// bit with bsdfs adds its width to the sum; only diffuse ones add pdf.
+// Called with bsdfs = GLOSSY|DIFFUSE|DISPERSIVE|REFLECT|TRANSMIT, which
+// overlaps every shinydiffuse component.
 __device__ __forceinline__ float mat_pdf(const DMat& M, const SurfPt& sp, v3 wo, v3 wi) {
-  if (M.type == YK_MAT_LIGHT || !(M.flags & BSDF_DIFFUSE)) return 0.f;
-  const v3 N = (vdot(sp.Ng, wo) < 0.f) ? vneg(sp.N) : sp.N;
-  const float width = M.diffuse * (((1.f - 0.f * 1.f) * (1.f - 0.f)) * (1.f - 0.f));
-  const float sum = 0.f + width;
-  const float pdf = 0.f + fabsf(vdot(wi, N)) * width;
-  if (sum < 0.00001f) return 0.f;
+  if (M.type == YK_MAT_LIGHT) return 0.f;
+  const float cos_Ng_wo = vdot(sp.Ng, wo);
+  const v3 N = (cos_Ng_wo < 0.f) ? vneg(sp.N) : sp.N;
+  const float Kr = mat_fresnel(M, wo, N);
+  float a[4];
+  mat_accum(M, Kr, a);
+  float sum = 0.f, pdf = 0.f;
+  for (int i = 0; i < M.ncomp; ++i) {
+    const int ci = M.cindex[i];
+    const float width = ci == 0 ? a[0] : (ci == 1 ? a[1] : (ci == 2 ? a[2] : a[3]));
+    sum += width;
+    if (M.cflags[i] == (BSDF_DIFFUSE | BSDF_TRANSMIT)) {
+      if (cos_Ng_wo * vdot(sp.Ng, wi) < 0.f) pdf += fabsf(vdot(wi, N)) * width;
+    } else if (M.cflags[i] == (BSDF_DIFFUSE | BSDF_REFLECT)) {
+      pdf += fabsf(vdot(wi, N)) * width;
+    }
+  }
+  if (M.ncomp == 0 || (double)sum < 0.00001) return 0.f;
   return pdf / sum;
+}
+
+// shinyDiffuseMat_t::getSpecular, shinydiffuse.cc:379-433 (compiled: the
+// backface test as (x + z) + y; reflect() without a sign test; the 0.01
+// grazing correction in double)
+__device__ __forceinline__ void mat_specular(const DMat& M, const SurfPt& sp, v3 wo, bool& refl, bool& refr,
+                                             v3* dir, c3* col) {
+  refl = refr = false;
+  if (M.type == YK_MAT_LIGHT) return;
+  const bool backface = ((sp.Ng.x * wo.x + sp.Ng.z * wo.z) + sp.Ng.y * wo.y) < 0.f;
+  const v3 N = backface ? vneg(sp.N) : sp.N;
+  const v3 Ng = backface ? vneg(sp.Ng) : sp.Ng;
+  const float Kr = mat_fresnel(M, wo, N);
+  if (M.flags & BSDF_FILTER) {  // mIsTransparent
+    refr = true;
+    dir[1] = vneg(wo);
+    const float t = 1.f - M.tfilter;
+    const float k = M.comp[1] * (1.f - M.comp[0] * Kr);
+    col[1] = C3((M.col[0] * M.tfilter + t) * k, (M.col[1] * M.tfilter + t) * k, (M.col[2] * M.tfilter + t) * k);
+  }
+  if (M.flags & BSDF_SPECULAR) {  // mIsMirror
+    refl = true;
+    const float vn = vdot(wo, N);
+    const float v2 = vn + vn;
+    v3 w = V3(v2 * N.x - wo.x, v2 * N.y - wo.y, v2 * N.z - wo.z);
+    const float cos_wi_Ng = vdot(w, Ng);
+    if ((double)cos_wi_Ng < 0.01) {
+      const float f = (float)(0.01 - (double)cos_wi_Ng);
+      w = vnormalize(V3(f * Ng.x + w.x, f * Ng.y + w.y, f * Ng.z + w.z));
+    }
+    dir[0] = w;
+    const float k = Kr * M.comp[0];
+    col[0] = C3(M.mirror[0] * k, M.mirror[1] * k, M.mirror[2] * k);
+  }
 }
 
 // emit: shinyDiffuseMat_t::emit (shinydiffuse.cc:251-257), lightMat_t::emit (simple.cc:54-61)
@@ -644,7 +781,7 @@ __device__ __forceinline__ void wave_append2(unsigned long long* counter, unsign
 // Shadow-ray slot flags
 enum : uint8_t { SL_TRACED = 1, SL_ADDS = 2 };
 // prim_hit flags
-enum : int { PH_HIT = 1, PH_DIFFUSE = 2 };
+enum : int { PH_HIT = 1, PH_DIFFUSE = 2, PH_LIGHT = 4 };
 // path state bits
 enum : int { PS_ALIVE = 1, PS_RESOLVE = 2, PS_CONT = 4, PS_EST = 8 };
 
@@ -678,9 +815,18 @@ struct Batch {
   float4* samples;      // final RGBA per camera sample
   float2* sxy;          // (dx, dy) of the sample inside its pixel
   int K;
+  // specular recursion (recursiveRaytrace) only, see k_spawn / k_fold
+  unsigned* psample;    // pixel sample index of each entry (state.pixelSample)
+  uint8_t* incl;        // state.includeLights after the entry's path loop
+  uint8_t* caus;        // caustic flag of the current path segment
+  float* emit0;         // 3 floats: emission at the entry's hit, added at the fold
 };
 
 struct RenderConst {
+  int spec;       // specular recursion pipeline (scene has SPECULAR|FILTER materials)
+  int trace_caustics;  // caustic_type path: traceCaustics (pathtracer.cc:389-397)
+  int rdepth;     // raydepth
+  int level;      // state.raylevel of the entries being shaded
   int spp;
   int nsub;       // path_samples
   int bounces;    // maxBounces
@@ -718,6 +864,7 @@ __global__ void __launch_bounds__(256) k_camera(TileList TL, Batch B, RenderCons
   const int j = T.x + pl % T.z, i = T.y + pl / T.z;
   const unsigned so = fnv32a((unsigned)i * fnv32a((unsigned)j));
   B.soffs[c] = so;
+  if (R.spec) B.psample[c] = (unsigned)s;
   float dx = 0.5f, dy = 0.5f;
   if (R.spp > 1) {
     dx = (0.5f + (float)s) * R.d1;
@@ -878,7 +1025,7 @@ __device__ __forceinline__ void flush_shadow(const Batch& B, long long c, int ke
 // primary BSDF (pathtracer.cc:169-187). Returns the segment's ray.
 __device__ __forceinline__ yk_ray path_first_segment(const Batch& B, const RenderConst& R, long long c,
                                                      const SurfPt& sp, const DMat& M, v3 dir, int isub) {
-  const unsigned s = (unsigned)(c % R.spp);
+  const unsigned s = R.spec ? B.psample[c] : (unsigned)(c % R.spp);
   const unsigned offs = (unsigned)(R.nsub * (int)s) + B.soffs[c] + (unsigned)isub;
   const float s1 = ri_vdc(offs, 0u);
   const float s2 = (float)scr_halton(2, offs);
@@ -909,7 +1056,7 @@ __global__ void __launch_bounds__(256) k_shade_primary(DScene S, Batch B, Render
   yk_ray seg;
   if (valid) {
     const yk_hit h = B.p_hits[c];
-    c3 col = C3(0.f, 0.f, 0.f);
+    c3 col = C3(0.f, 0.f, 0.f), em = C3(0.f, 0.f, 0.f);
     float alpha = R.transp_bg ? 0.f : 1.f;
     int ph = 0;
     if (h.prim >= 0) {
@@ -919,10 +1066,17 @@ __global__ void __launch_bounds__(256) k_shade_primary(DScene S, Batch B, Render
       const DMat& M = c_mats[sp.mat];
       const v3 wo = vneg(dir);
       ph = PH_HIT;
-      if (M.flags & BSDF_EMIT) col = cadd(col, mat_emit(M, sp, wo, true));
+      if (M.flags & BSDF_EMIT) {
+        // spec mode: emission is added at the fold, where state.includeLights
+        // of this recursion level is known (lightMat_t::emit depends on it)
+        const c3 e = mat_emit(M, sp, wo, true);
+        if (R.spec) em = e;
+        else col = cadd(col, e);
+        if (M.type == YK_MAT_LIGHT) ph |= PH_LIGHT;
+      }
       if (M.flags & BSDF_DIFFUSE) {
         ph |= PH_DIFFUSE;
-        const unsigned s = (unsigned)(c % R.spp);
+        const unsigned s = R.spec ? B.psample[c] : (unsigned)(c % R.spp);
         int k0 = 0;
         for (int l = 0; l < R.nlights; ++l) {
           nr += gen_light(B, c, k0, l, sp, wo, s, B.soffs[c], (unsigned)l, traced);
@@ -933,6 +1087,10 @@ __global__ void __launch_bounds__(256) k_shade_primary(DScene S, Batch B, Render
           B.wlast[c] = 0.f;
           seg = path_first_segment(B, R, c, sp, M, dir, 0);
           emit = true;
+          if (R.spec) {  // state.includeLights = false before the first segment's intersect
+            B.incl[c] = 0;
+            B.caus[c] = 0;
+          }
         }
       }
       alpha = 1.0f;
@@ -944,6 +1102,11 @@ __global__ void __launch_bounds__(256) k_shade_primary(DScene S, Batch B, Render
     B.col[3 * c + 1] = col.g;
     B.col[3 * c + 2] = col.b;
     B.alpha[c] = alpha;
+    if (R.spec) {
+      B.emit0[3 * c] = em.r;
+      B.emit0[3 * c + 1] = em.g;
+      B.emit0[3 * c + 2] = em.b;
+    }
     B.pathcol[3 * c] = 0.f;
     B.pathcol[3 * c + 1] = 0.f;
     B.pathcol[3 * c + 2] = 0.f;
@@ -1015,6 +1178,10 @@ __global__ void __launch_bounds__(256) k_path_start(DScene S, Batch B, RenderCon
     const SurfPt sp = make_surface(S, from, dir, h);
     r = path_first_segment(B, R, c, sp, c_mats[sp.mat], dir, isub);
     emit = true;
+    if (R.spec) {
+      B.incl[c] = 0;
+      B.caus[c] = 0;
+    }
   }
   unsigned sbase, q;
   wave_append2(qword, 0u, emit ? 1u : 0u, sbase, q);
@@ -1043,14 +1210,21 @@ __global__ void __launch_bounds__(256) k_shade_bounce(DScene S, Batch B, RenderC
   if (valid) {
     const yk_hit h = B.q_hits[qin][qi];
     if (h.prim < 0) {
-      B.pstate[c] = 0;  // background: "continue" at depth 1, "break" later
+      // background: "continue" at depth 1, "break" later; a caustic segment
+      // adds the background first (pathtracer.cc:279-286)
+      if (R.spec && depth >= 2 && B.caus[c] && R.has_bg) {
+        B.pathcol[3 * c] = B.pathcol[3 * c] + B.thr[3 * c] * R.bg[0];
+        B.pathcol[3 * c + 1] = B.pathcol[3 * c + 1] + B.thr[3 * c + 1] * R.bg[1];
+        B.pathcol[3 * c + 2] = B.pathcol[3 * c + 2] + B.thr[3 * c + 2] * R.bg[2];
+      }
+      B.pstate[c] = 0;
     } else {
       const yk_ray pr = B.q_rays[qin][qi];
       const v3 from = V3(pr.from[0], pr.from[1], pr.from[2]), dir = V3(pr.dir[0], pr.dir[1], pr.dir[2]);
       const SurfPt sp = make_surface(S, from, dir, h);
       const DMat& M = c_mats[sp.mat];
       const v3 pwo = vneg(dir);
-      const unsigned s = (unsigned)(c % R.spp);
+      const unsigned s = R.spec ? B.psample[c] : (unsigned)(c % R.spp);
       const unsigned offs = (unsigned)(R.nsub * (int)s) + B.soffs[c] + (unsigned)isub;
       int ps = PS_RESOLVE;
       // estimateOneDirectLight(state, hit, pwo, offs): always at the first
@@ -1067,6 +1241,9 @@ __global__ void __launch_bounds__(256) k_shade_bounce(DScene S, Batch B, RenderC
       }
       c3 em = C3(0.f, 0.f, 0.f);
       if (depth == 1 && (M.flags & BSDF_EMIT)) em = mat_emit(M, sp, pwo, false);
+      // "matBSDFs & (BSDF_EMIT && caustic)" is matBSDFs & BSDF_SPECULAR when
+      // the segment was caustic (pathtracer.cc:295); includeLights = caustic
+      if (R.spec && depth >= 2 && B.caus[c] && (M.flags & BSDF_SPECULAR)) em = mat_emit(M, sp, pwo, true);
       B.emit_b[3 * c] = em.r;
       B.emit_b[3 * c + 1] = em.g;
       B.emit_b[3 * c + 2] = em.b;
@@ -1075,11 +1252,18 @@ __global__ void __launch_bounds__(256) k_shade_bounce(DScene S, Batch B, RenderC
         const float s2 = (float)scr_halton(4 * depth + 4, offs);
         float pdf, W = B.wlast[c];
         bool ok;
-        v3 ndir = V3(0.f, 0.f, 0.f);
-        c3 sc = mat_sample(M, sp, pwo, ndir, s1, s2, BSDF_ALL, pdf, W, ok);
+        v3 ndir = dir;  // pRay.dir keeps the previous direction if sample() returns early
+        unsigned sfl;
+        c3 sc = mat_sample(M, sp, pwo, ndir, s1, s2, BSDF_ALL, pdf, W, ok, sfl);
         B.wlast[c] = W;
         sc = cscale(W, sc);
         if (!cblack(sc)) {
+          if (R.spec) {  // caustic = traceCaustics && sampledFlags & (SPECULAR|GLOSSY|FILTER)
+            const uint8_t caustic =
+                (R.trace_caustics && (sfl & (BSDF_SPECULAR | BSDF_GLOSSY | BSDF_FILTER))) ? 1 : 0;
+            B.caus[c] = caustic;
+            B.incl[c] = caustic;
+          }
           put_ray(nxt, sp.P, ndir, YK_MIN_RAYDIST, -1.0f);
           emit_next = true;
           B.scol_next[3 * c] = sc.r;
@@ -1116,7 +1300,7 @@ __global__ void __launch_bounds__(256) k_resolve_bounce(Batch B, RenderConst R,
     const int lnum = B.lsel[c];
     lcol = cscale((float)R.nlights, resolve_light(B, c, 0, lnum));
   }
-  if (depth == 1) lcol = cadd(lcol, C3(B.emit_b[3 * c], B.emit_b[3 * c + 1], B.emit_b[3 * c + 2]));
+  if (depth == 1 || R.spec) lcol = cadd(lcol, C3(B.emit_b[3 * c], B.emit_b[3 * c + 1], B.emit_b[3 * c + 2]));
   const c3 thr = C3(B.thr[3 * c], B.thr[3 * c + 1], B.thr[3 * c + 2]);
   B.pathcol[3 * c] = B.pathcol[3 * c] + lcol.r * thr.r;
   B.pathcol[3 * c + 1] = B.pathcol[3 * c + 1] + lcol.g * thr.g;
@@ -1141,6 +1325,171 @@ __global__ void __launch_bounds__(256) k_finish(Batch B, RenderConst R, long lon
     col = cadd(col, C3(B.pathcol[3 * c] / ns, B.pathcol[3 * c + 1] / ns, B.pathcol[3 * c + 2] / ns));
   }
   B.samples[c] = make_float4(col.r, col.g, col.b, B.alpha[c]);
+}
+
+// ------------------------------------------------------------ specular recursion
+//
+// mcIntegrator_t::recursiveRaytrace (mcintegrator.cc:421-627) calls the
+// integrator again for the mirror and refraction rays of a specular hit, up
+// to raydepth levels. Here every such call is an entry ("node") of a later
+// generation: generation g holds the rays of recursion level g, shaded by the
+// same kernels as camera rays. Each node keeps its own terms (emission,
+// direct light, path estimate) and its children; k_fold then sums every
+// camera sample's tree in the reference's order. state.includeLights is
+// shared by the recursive calls, and lightMat_t::emit reads it, so a node's
+// emission is only added at the fold, where the value left by the previous
+// sibling's subtree is known (pathtracer.cc:149-152,220,264; directlight.cc
+// restores it on return).
+
+enum : int { NF_HIT = 1, NF_LIGHT = 2, NF_LOOP = 4, NF_LOOPT = 8, NF_SPEC = 16 };
+
+struct NodeStore {
+  float* E;      // 3 per node: emission at the node's hit (includeLights = true)
+  float* D;      // 3 per node: direct light (or background on a miss)
+  float* P;      // 3 per node: pathCol / nSamples (path tracer)
+  int* flags;    // NF_*
+  int* child;    // 2 per node: reflect, refract (-1 none)
+  float* rcol;   // 6 per node: getSpecular colours of the two children
+  float* alpha;  // camera nodes
+  yk_ray* ray;   // rays of nodes of generation >= 1 (by node id)
+  unsigned* soffs;
+  unsigned* psample;
+  unsigned long long* count;  // allocated node ids
+  long long cap;
+  int* overflow;
+};
+
+// Terms of the n entries of one chunk (node ids base..base+n-1).
+__global__ void __launch_bounds__(256) k_finish_spec(Batch B, RenderConst R, NodeStore NS, long long base,
+                                                     long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const long long node = base + i;
+  const int ph = B.prim_hit[i];
+  const bool loop = R.integrator == YK_INTEGRATOR_PATH && (ph & PH_DIFFUSE);
+  c3 P = C3(0.f, 0.f, 0.f);
+  if (loop) {
+    const float ns = (float)R.nsub;
+    P = C3(B.pathcol[3 * i] / ns, B.pathcol[3 * i + 1] / ns, B.pathcol[3 * i + 2] / ns);
+  }
+  int f = 0;
+  if (ph & PH_HIT) f |= NF_HIT;
+  if (ph & PH_LIGHT) f |= NF_LIGHT;
+  if (loop) f |= NF_LOOP | (B.incl[i] ? NF_LOOPT : 0);
+  NS.flags[node] = f;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    NS.E[3 * node + k] = (ph & PH_HIT) ? B.emit0[3 * i + k] : 0.f;
+    NS.D[3 * node + k] = B.col[3 * i + k];
+  }
+  NS.P[3 * node] = P.r;
+  NS.P[3 * node + 1] = P.g;
+  NS.P[3 * node + 2] = P.b;
+  NS.child[2 * node] = -1;
+  NS.child[2 * node + 1] = -1;
+  if (R.level == 0) NS.alpha[node] = B.alpha[i];
+}
+
+// recursiveRaytrace's specular block for the hits of one chunk: allocate the
+// reflect / refract children (rays from sp.P, tmin MIN_RAYDIST, unbounded).
+__global__ void __launch_bounds__(256) k_spawn(DScene S, Batch B, RenderConst R, NodeStore NS, long long base,
+                                               long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !(B.prim_hit[i] & PH_HIT)) return;
+  const int lv = R.level + 1;  // state.raylevel++
+  if (lv > R.rdepth || lv >= 20) return;
+  const yk_hit h = B.p_hits[i];
+  const yk_ray r = B.p_rays[i];
+  const v3 from = V3(r.from[0], r.from[1], r.from[2]), dir = V3(r.dir[0], r.dir[1], r.dir[2]);
+  const SurfPt sp = make_surface(S, from, dir, h);
+  const DMat& M = c_mats[sp.mat];
+  if (!(M.flags & (BSDF_SPECULAR | BSDF_FILTER))) return;
+  const long long node = base + i;
+  NS.flags[node] |= NF_SPEC;
+  bool refl, refr;
+  v3 d[2];
+  c3 col[2];
+  mat_specular(M, sp, vneg(dir), refl, refr, d, col);
+  const bool want[2] = {refl, refr};
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    if (!want[k]) continue;
+    const unsigned long long id = atomicAdd(NS.count, 1ull);
+    if ((long long)id >= NS.cap) {
+      *NS.overflow = 1;
+      continue;
+    }
+    NS.child[2 * node + k] = (int)id;
+    NS.rcol[6 * node + 3 * k] = col[k].r;
+    NS.rcol[6 * node + 3 * k + 1] = col[k].g;
+    NS.rcol[6 * node + 3 * k + 2] = col[k].b;
+    put_ray(NS.ray[id], sp.P, d[k], YK_MIN_RAYDIST, -1.0f);
+    NS.soffs[id] = B.soffs[i];
+    NS.psample[id] = B.psample[i];
+  }
+}
+
+// Sums each camera sample's node tree depth first, in the reference's order:
+// col = (emit + direct) + path; col += child_r * rcol0; col += child_t * rcol1.
+__global__ void __launch_bounds__(256) k_fold(Batch B, RenderConst R, NodeStore NS, long long nc) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  constexpr int kMaxLevel = 22;
+  int nodes[kMaxLevel], stage[kMaxLevel];
+  c3 acc[kMaxLevel];
+  const bool pt = R.integrator == YK_INTEGRATOR_PATH;
+  bool e = true;  // state.includeLights
+  int dd = 0;
+  nodes[0] = (int)c;
+  stage[0] = 0;
+  c3 result = C3(0.f, 0.f, 0.f);
+  for (;;) {
+    const int n = nodes[dd];
+    const int F = NS.flags[n];
+    if (stage[dd] == 0) {
+      c3 col = C3(NS.D[3 * n], NS.D[3 * n + 1], NS.D[3 * n + 2]);
+      if (F & NF_HIT) {
+        if (dd == 0) e = true;  // raylevel 0: includeLights = true
+        const bool incl = pt ? e : true;
+        const c3 E = ((F & NF_LIGHT) && !incl) ? C3(0.f, 0.f, 0.f)
+                                               : C3(NS.E[3 * n], NS.E[3 * n + 1], NS.E[3 * n + 2]);
+        col = cadd(E, col);
+        col = cadd(col, C3(NS.P[3 * n], NS.P[3 * n + 1], NS.P[3 * n + 2]));
+        if (pt && (F & NF_LOOP)) e = (F & NF_LOOPT) != 0;
+        if (F & NF_SPEC) e = true;
+      }
+      acc[dd] = col;
+      stage[dd] = 1;
+      const int ch = (F & NF_HIT) ? NS.child[2 * n] : -1;
+      if (ch >= 0 && dd + 1 < kMaxLevel) {
+        ++dd;
+        nodes[dd] = ch;
+        stage[dd] = 0;
+        continue;
+      }
+    }
+    if (stage[dd] == 1) {
+      stage[dd] = 2;
+      const int ch = (F & NF_HIT) ? NS.child[2 * n + 1] : -1;
+      if (ch >= 0 && dd + 1 < kMaxLevel) {
+        ++dd;
+        nodes[dd] = ch;
+        stage[dd] = 0;
+        continue;
+      }
+    }
+    const c3 v = acc[dd];
+    if (dd == 0) {
+      result = v;
+      break;
+    }
+    --dd;
+    const int pn = nodes[dd];
+    const int k = stage[dd] - 1;
+    const float* rc = NS.rcol + 6 * pn + 3 * k;
+    acc[dd] = cadd(acc[dd], C3(v.r * rc[0], v.g * rc[1], v.b * rc[2]));
+  }
+  B.samples[c] = make_float4(result.r, result.g, result.b, NS.alpha[c]);
 }
 
 // ------------------------------------------------------------ film
@@ -1309,6 +1658,9 @@ struct Pipe {
   DBuf<uint8_t> sl_flags, s_occl;
   DBuf<float4> samples;
   DBuf<float2> sxy;
+  DBuf<unsigned> psample;
+  DBuf<uint8_t> incl, caus;
+  DBuf<float> emit0;
   void create() {
     HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&ev0));
@@ -1329,7 +1681,7 @@ struct Pipe {
     if (ev1) (void)hipEventDestroy(ev1);
     if (stream) (void)hipStreamDestroy(stream);
   }
-  Batch bind(long long maxc, int K, int tiles_per_batch) {
+  Batch bind(long long maxc, int K, int tiles_per_batch, bool spec = false) {
     soffs.ensure(maxc);
     col.ensure(3 * maxc);
     alpha.ensure(maxc);
@@ -1386,6 +1738,16 @@ struct Pipe {
     B.samples = samples.p;
     B.sxy = sxy.p;
     B.K = K;
+    if (spec) {
+      psample.ensure(maxc);
+      incl.ensure(maxc);
+      caus.ensure(maxc);
+      emit0.ensure(3 * maxc);
+      B.psample = psample.p;
+      B.incl = incl.p;
+      B.caus = caus.p;
+      B.emit0 = emit0.p;
+    }
     return B;
   }
 };
@@ -1408,6 +1770,13 @@ struct yk_device {
   DBuf<uint32_t> leaf;
   DScene S{};
   int ntris = 0, max_depth = 0, nlights = 0, sum_light_slots = 0;
+  bool spec = false;  // some material has SPECULAR|FILTER components: recursion pipeline
+  // node store of the specular recursion (k_finish_spec / k_spawn / k_fold)
+  DBuf<float> nE, nD, nP, nrcol, nalpha;
+  DBuf<int> nflags, nchild, noverflow;
+  DBuf<yk_ray> nray;
+  DBuf<unsigned> nsoffs, npsample;
+  DBuf<unsigned long long> ncount, spec_words;
   bool has_bg = false;
   float bg[3] = {0.f, 0.f, 0.f};
   Pipe pipe[kPipes];
@@ -1499,8 +1868,18 @@ DMat make_mat(const yk_material_state& m) {
     M.col[k] = m.color[k];
     M.emit_col[k] = m.emit_color[k];
   }
-  M.diffuse = m.diffuse_strength;
   M.double_sided = m.double_sided;
+  for (int k = 0; k < 3; ++k) M.mirror[k] = m.mirror_color[k];
+  M.ncomp = std::max(0, std::min(4, (int)m.ncomp));
+  for (int i = 0; i < 4; ++i) {
+    M.comp[i] = m.component[i];
+    M.cflags[i] = m.comp_flags[i];
+    M.cindex[i] = std::max(0, std::min(3, (int)m.comp_index[i]));
+    if (i < M.ncomp && m.comp_flags[i] == (BSDF_DIFFUSE | BSDF_TRANSMIT)) M.translucent = 1;
+  }
+  M.tfilter = m.transmit_filter;
+  M.fresnel = m.has_fresnel;
+  M.ior2 = m.ior_squared;
   return M;
 }
 
@@ -1701,7 +2080,11 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
     HIPCHK(hipMemcpy(d->leaf.p, S.tree.leaf_prims.data(), S.tree.leaf_prims.size() * sizeof(uint32_t),
                      hipMemcpyHostToDevice));
   std::vector<DMat> mats;
-  for (const auto& m : S.material_states) mats.push_back(make_mat(m));
+  d->spec = false;
+  for (const auto& m : S.material_states) {
+    mats.push_back(make_mat(m));
+    if (m.bsdf_flags & (BSDF_SPECULAR | BSDF_FILTER)) d->spec = true;
+  }
   if (!mats.empty()) HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_mats), mats.data(), mats.size() * sizeof(DMat)));
   std::vector<DLight> lights;
   int sum_slots = 0;
@@ -1809,8 +2192,9 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
     return set_error(YK_ERR_UNSUPPORTED, "filter not supported (box, mitchell)");
   if (p->integrator != YK_INTEGRATOR_PATH && p->integrator != YK_INTEGRATOR_DIRECT)
     return set_error(YK_ERR_ARG, "unknown integrator");
-  if (p->integrator == YK_INTEGRATOR_PATH && p->caustic_type != YK_CAUSTIC_NONE)
-    return set_error(YK_ERR_UNSUPPORTED, "pathtracing needs caustic_type none");
+  if (p->integrator == YK_INTEGRATOR_PATH && p->caustic_type != YK_CAUSTIC_NONE &&
+      p->caustic_type != YK_CAUSTIC_PATH)
+    return set_error(YK_ERR_UNSUPPORTED, "pathtracing needs caustic_type none or path");
   if (p->integrator == YK_INTEGRATOR_PATH && (p->bounces < 1 || 4 * p->bounces + 4 >= 50))
     return set_error(YK_ERR_UNSUPPORTED, "bounces must be in [1, 11]");
   if (p->width <= 0 || p->height <= 0) return set_error(YK_ERR_ARG, "empty render area");
@@ -1837,7 +2221,17 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   R.has_bg = d->has_bg ? 1 : 0;
   for (int k = 0; k < 3; ++k) R.bg[k] = d->bg[k];
   R.d1 = F.d1;
+  R.spec = d->spec ? 1 : 0;
+  R.trace_caustics = (p->integrator == YK_INTEGRATOR_PATH && p->caustic_type == YK_CAUSTIC_PATH) ? 1 : 0;
+  R.rdepth = p->raydepth;
+  R.level = 0;
   const int K = std::max(1, d->sum_light_slots);
+  // specular recursion: generation g holds recursion level g; every node has
+  // at most two children, so a batch of nc camera samples needs at most
+  // nc * (2^(L+1) - 1) nodes, L = min(raydepth, 19)
+  const int spec_levels = d->spec ? std::max(0, std::min(p->raydepth, 19)) : 0;
+  const long long spec_worst = (2ll << spec_levels) - 1;
+  constexpr long long kNodeBytes = 116;
   // batch = whole tiles, about YK_BATCH_SAMPLES camera samples (default 32M:
   // each trace launch ends in a tail of long rays, which large batches
   // amortise), capped so the buffers of all pipes stay within ~64 GB of HBM
@@ -1849,10 +2243,13 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   const long long bytes_per_sample = 400 + 52ll * K;
   const long long target = std::max(1ll << 20, std::min(target_env, (64ll << 30) / kPipes / bytes_per_sample));
   const long long tile_samples = (long long)F.tile * F.tile * spp;
-  const int tiles_per_batch = (int)std::max<long long>(1, target / tile_samples);
+  if (d->spec && spec_worst * tile_samples * kNodeBytes > (48ll << 30))
+    return set_error(YK_ERR_UNSUPPORTED, "raydepth too large for the tile size / spp (node store > 48 GB)");
+  const long long target_spec = d->spec ? std::min(target, (12ll << 30) / (kNodeBytes * spec_worst)) : target;
+  const int tiles_per_batch = (int)std::max<long long>(1, target_spec / tile_samples);
   const long long maxc = (long long)tiles_per_batch * tile_samples;
   const int nbatch = (int)((owned.size() + tiles_per_batch - 1) / tiles_per_batch);
-  const int npipes = std::min(kPipes, std::max(1, nbatch));
+  const int npipes = d->spec ? 1 : std::min(kPipes, std::max(1, nbatch));
   const bool path = p->integrator == YK_INTEGRATOR_PATH;
   const int bounces = path ? R.bounces : 0;
   const int nsub = path ? R.nsub : 1;
@@ -1900,9 +2297,29 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   for (int pi = 0; pi < npipes; ++pi) {
     Pipe& P = d->pipe[pi];
     const int nb_here = (nbatch - pi + npipes - 1) / npipes;
-    P.words.ensure((size_t)(8 + words_per_batch * nb_here));
+    P.words.ensure((size_t)(8 + (d->spec ? 0 : words_per_batch * nb_here)));
     HIPCHK(hipMemsetAsync(P.words.p, 0, P.words.n * sizeof(unsigned long long), P.stream));
-    Bp[pi] = P.bind(maxc, K, tiles_per_batch);
+    Bp[pi] = P.bind(maxc, K, tiles_per_batch, d->spec);
+  }
+  NodeStore NS{};
+  if (d->spec) {
+    const long long cap = maxc * spec_worst;
+    d->nE.ensure(3 * cap);
+    d->nD.ensure(3 * cap);
+    d->nP.ensure(3 * cap);
+    d->nrcol.ensure(6 * cap);
+    d->nalpha.ensure(maxc);
+    d->nflags.ensure(cap);
+    d->nchild.ensure(2 * cap);
+    d->nray.ensure(cap);
+    d->nsoffs.ensure(cap);
+    d->npsample.ensure(cap);
+    d->ncount.ensure(1);
+    d->noverflow.ensure(1);
+    d->spec_words.ensure((size_t)words_per_batch);
+    NS = NodeStore{d->nE.p,   d->nD.p,     d->nP.p,       d->nflags.p, d->nchild.p,  d->nrcol.p,    d->nalpha.p,
+                   d->nray.p, d->nsoffs.p, d->npsample.p, d->ncount.p, (long long)cap, d->noverflow.p};
+    HIPCHK(hipMemsetAsync(d->noverflow.p, 0, sizeof(int), d->pipe[0].stream));
   }
   struct Timed {
     int pipe;
@@ -1918,7 +2335,7 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
     Pipe& P = d->pipe[pi];
     const Batch& B = Bp[pi];
     const long long nc = nc_of[bi];
-    unsigned long long* bw = P.words.p + 8 + words_per_batch * (bi / npipes);
+    unsigned long long* bw = d->spec ? d->spec_words.p : P.words.p + 8 + words_per_batch * (bi / npipes);
     auto qw = [&](int isub, int depth) { return bw + isub * (bounces + 1) + depth; };
     int launch = 0;
     auto trace = [&](bool closest, const yk_ray* rays, const unsigned* idx, RayCount n, yk_hit* hits,
@@ -1934,6 +2351,70 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
                 (int)std::min<size_t>(tiles_per_batch, owned.size() - (size_t)bi * tiles_per_batch)};
     hipLaunchKernelGGL(k_camera, dim3(grid_for(nc)), dim3(256), 0, P.stream, TL, B, R, nc);
     HIPCHK(hipGetLastError());
+    if (d->spec) {
+      // ---- specular recursion: generations of nodes, host-synchronised
+      auto shade_entries = [&](const Batch& Bc, const RenderConst& Rc, long long n, long long node_base) {
+        HIPCHK(hipMemsetAsync(d->spec_words.p, 0, d->spec_words.n * sizeof(unsigned long long), P.stream));
+        launch = 0;
+        trace(true, Bc.p_rays, nullptr, RayCount{nullptr, 0, n}, Bc.p_hits, nullptr);
+        hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(n)), dim3(256), 0, P.stream, d->S, Bc, Rc, n, qw(0, 0));
+        HIPCHK(hipGetLastError());
+        trace(false, Bc.s_rays, Bc.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, Bc.s_occl);
+        hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(n)), dim3(256), 0, P.stream, Bc, Rc, n);
+        HIPCHK(hipGetLastError());
+        for (int isub = 0; isub < (path ? nsub : 0); ++isub) {
+          if (isub > 0) {
+            hipLaunchKernelGGL(k_path_start, dim3(grid_for(n)), dim3(256), 0, P.stream, d->S, Bc, Rc, n, isub,
+                               qw(isub, 0));
+            HIPCHK(hipGetLastError());
+          }
+          int qin = 1;
+          for (int depth = 1; depth <= bounces; ++depth) {
+            const unsigned long long* in_w = qw(isub, depth - 1);
+            unsigned long long* out_w = qw(isub, depth);
+            trace(true, Bc.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, Bc.q_hits[qin], nullptr);
+            hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(n)), dim3(256), 0, P.stream, d->S, Bc, Rc, in_w, depth,
+                               isub, qin, out_w);
+            HIPCHK(hipGetLastError());
+            trace(false, Bc.s_rays, Bc.s_idx, RayCount{out_w, 0, 0}, nullptr, Bc.s_occl);
+            hipLaunchKernelGGL(k_resolve_bounce, dim3(grid_for(n)), dim3(256), 0, P.stream, Bc, Rc, in_w, depth,
+                               qin);
+            HIPCHK(hipGetLastError());
+            qin ^= 1;
+          }
+        }
+        hipLaunchKernelGGL(k_finish_spec, dim3(grid_for(n)), dim3(256), 0, P.stream, Bc, Rc, NS, node_base, n);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_spawn, dim3(grid_for(n)), dim3(256), 0, P.stream, d->S, Bc, Rc, NS, node_base, n);
+        HIPCHK(hipGetLastError());
+      };
+      const unsigned long long start = (unsigned long long)nc;
+      HIPCHK(hipMemcpyAsync(NS.count, &start, sizeof start, hipMemcpyHostToDevice, P.stream));
+      shade_entries(B, R, nc, 0);
+      long long g0 = 0, g1 = nc;
+      for (int level = 1; level <= spec_levels; ++level) {
+        unsigned long long cnt = 0;
+        HIPCHK(hipMemcpyAsync(&cnt, NS.count, sizeof cnt, hipMemcpyDeviceToHost, P.stream));
+        HIPCHK(hipStreamSynchronize(P.stream));
+        if ((long long)cnt > NS.cap) return set_error(YK_ERR_INTERNAL, "specular node store overflow");
+        g0 = g1;
+        g1 = (long long)cnt;
+        if (g1 <= g0) break;
+        RenderConst Rl = R;
+        Rl.level = level;
+        for (long long off = g0; off < g1; off += maxc) {
+          const long long n = std::min<long long>(maxc, g1 - off);
+          Batch Bc = B;
+          Bc.p_rays = NS.ray + off;
+          Bc.soffs = NS.soffs + off;
+          Bc.psample = NS.psample + off;
+          shade_entries(Bc, Rl, n, off);
+        }
+      }
+      hipLaunchKernelGGL(k_fold, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, NS, nc);
+      HIPCHK(hipGetLastError());
+    }
+    if (!d->spec) {
     trace(true, B.p_rays, nullptr, RayCount{nullptr, 0, nc}, B.p_hits, nullptr);
     hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, d->S, B, R, nc, qw(0, 0));
     HIPCHK(hipGetLastError());
@@ -1964,6 +2445,7 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
     }
     hipLaunchKernelGGL(k_finish, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
     HIPCHK(hipGetLastError());
+    }  // !d->spec
     // film: in batch order (tile order), whichever pipe ran the batch
     if (bi > 0) HIPCHK(hipStreamWaitEvent(P.stream, d->gather_ev[(bi - 1) % kPipes], 0));
     FilmConst Fb = F;

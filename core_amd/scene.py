@@ -32,8 +32,13 @@ class Scene:
 
     # -- assembly ------------------------------------------------------
     def add_material(self, type_=A.YK_MAT_SHINYDIFFUSE, color=(1, 1, 1), diffuse_reflect=1.0, emit=0.0,
-                     power=1.0, double_sided=False):
-        m = A.yk_material(type_, A.f3(*color), diffuse_reflect, emit, power, int(double_sided))
+                     power=1.0, double_sided=False, mirror_color=(1, 1, 1), specular_reflect=0.0,
+                     transparency=0.0, translucency=0.0, transmit_filter=1.0, fresnel_effect=False, ior=1.33):
+        """shinydiffusemat / light_mat parameters with the reference factory defaults
+        (shinydiffuse.cc:474-503, simple.cc:80-90)."""
+        m = A.yk_material(type_, A.f3(*color), diffuse_reflect, emit, power, int(double_sided),
+                          A.f3(*mirror_color), specular_reflect, transparency, translucency, transmit_filter,
+                          int(fresnel_effect), ior)
         mid = C.c_int32()
         A.check(A.lib().yk_scene_add_material(self._p, C.byref(m), C.byref(mid)))
         return mid.value

@@ -48,6 +48,15 @@ typedef struct yk_material {
   float emit;             /* "emit" (shinydiffusemat, default 0)                    */
   float power;            /* "power" (light_mat, default 1)                         */
   int32_t double_sided;   /* "double_sided" (light_mat, default 0)                  */
+  /* shinydiffusemat specular / transmissive parameters (shinydiffuse.cc:474-503;
+   * reference defaults in brackets -- a zero-initialised struct must set them) */
+  float mirror_color[3];  /* "mirror_color" [1,1,1]                                 */
+  float specular_reflect; /* "specular_reflect" [0]: mirror strength                */
+  float transparency;     /* "transparency" [0]                                     */
+  float translucency;     /* "translucency" [0]                                     */
+  float transmit_filter;  /* "transmit_filter" [1]                                  */
+  int32_t fresnel_effect; /* "fresnel_effect" [0]                                   */
+  double ior;             /* "IOR" [1.33] (parsed as double; mIOR_Squared = IOR*IOR) */
 } yk_material;
 
 enum { YK_LIGHT_AREA = 0, YK_LIGHT_POINT = 1, YK_LIGHT_DIRECTIONAL = 2 };
@@ -198,6 +207,16 @@ typedef struct yk_material_state {
   float diffuse_strength;   /* shinyDiffuseMat_t::mDiffuseStrength                      */
   float emit_color[3];      /* shinyDiffuseMat_t::mEmitColor (= emit strength * color)  */
   int32_t double_sided;     /* lightMat_t::doubleSided                                  */
+  /* shinyDiffuseMat_t after config() (shinydiffuse.cc:27-80) */
+  float mirror_color[3];    /* mMirrorColor                                              */
+  float component[4];       /* getComponents: mirror, transparency, translucency,
+                               diffuse strength; 0 where config() left it off           */
+  int32_t ncomp;            /* nBSDF                                                     */
+  uint32_t comp_flags[4];   /* cFlags                                                    */
+  int32_t comp_index[4];    /* cIndex                                                    */
+  float transmit_filter;    /* mTransmitFilterStrength                                   */
+  int32_t has_fresnel;      /* mHasFresnelEffect                                         */
+  float ior_squared;        /* mIOR_Squared                                              */
 } yk_material_state;
 
 typedef struct yk_area_light_state { /* areaLight_t members (arealight.h:45-53) */

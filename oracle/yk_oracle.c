@@ -513,26 +513,123 @@ static void camera_ray(float px, float py, v3* from, v3* dir, float* tmin, float
 
 /* --------------------------------------------------------- materials -- */
 
-static const yk_material* mat_of(int m) { return &G.mats[m]; }
+/* shinyDiffuseMat_t after its ctor + config() (shinydiffuse.cc:9-80) or
+ * lightMat_t (simple.cc:50-53), derived from the factory parameters. */
+typedef struct {
+  int type;
+  unsigned flags; /* bsdfFlags */
+  col3 diff, mirror, emit_col, light_col;
+  float comp[4];  /* getComponents: mirror, transparency, translucency, diffuse */
+  int ncomp;
+  unsigned cflags[4];
+  int cindex[4];
+  int is_mirror, is_transparent, is_translucent;
+  float tfilter;
+  int fresnel;
+  float ior2;
+  int double_sided;
+} sdmat;
+static sdmat* g_sd;
 
-static unsigned mat_flags(int m) {
-  const yk_material* M = mat_of(m);
-  if (M->type == YK_MAT_LIGHT) return BSDF_EMIT;
-  unsigned f = 0;
-  if (M->emit > 0.f) f |= BSDF_EMIT;
-  if (M->diffuse_reflect > 0.00001f) f |= BSDF_DIFFUSE | BSDF_REFLECT;
-  return f;
+static void mats_setup(void) {
+  free(g_sd);
+  g_sd = (sdmat*)calloc(G.nmats > 0 ? G.nmats : 1, sizeof *g_sd);
+  for (int m = 0; m < G.nmats; ++m) {
+    const yk_material* M = &G.mats[m];
+    sdmat* D = &g_sd[m];
+    D->type = M->type;
+    if (M->type == YK_MAT_LIGHT) {
+      D->flags = BSDF_EMIT;
+      D->light_col = C(M->color[0] * M->power, M->color[1] * M->power, M->color[2] * M->power);
+      D->double_sided = M->double_sided;
+      continue;
+    }
+    D->diff = C(M->color[0], M->color[1], M->color[2]);
+    D->mirror = C(M->mirror_color[0], M->mirror_color[1], M->mirror_color[2]);
+    D->emit_col = cscale(M->emit, D->diff); /* mEmitColor = emitStrength * diffuseColor */
+    if (M->emit > 0.f) D->flags |= BSDF_EMIT;
+    D->tfilter = M->transmit_filter;
+    if (M->fresnel_effect) {
+      D->fresnel = 1;
+      D->ior2 = (float)(M->ior * M->ior);
+    }
+    float acc = 1.f;
+    int n = 0;
+    if (M->specular_reflect > 0.00001f) {
+      D->is_mirror = 1;
+      if (!D->fresnel) acc = 1.f - M->specular_reflect;
+      D->flags |= BSDF_SPECULAR | BSDF_REFLECT;
+      D->cflags[n] = BSDF_SPECULAR | BSDF_REFLECT;
+      D->cindex[n++] = 0;
+      D->comp[0] = M->specular_reflect;
+    }
+    if (M->transparency * acc > 0.00001f) {
+      D->is_transparent = 1;
+      acc *= 1.f - M->transparency;
+      D->flags |= BSDF_TRANSMIT | BSDF_FILTER;
+      D->cflags[n] = BSDF_TRANSMIT | BSDF_FILTER;
+      D->cindex[n++] = 1;
+      D->comp[1] = M->transparency;
+    }
+    if (M->translucency * acc > 0.00001f) {
+      D->is_translucent = 1;
+      acc *= 1.f - M->transparency; /* sic: shinydiffuse.cc:59 uses the transparency strength */
+      D->flags |= BSDF_DIFFUSE | BSDF_TRANSMIT;
+      D->cflags[n] = BSDF_DIFFUSE | BSDF_TRANSMIT;
+      D->cindex[n++] = 2;
+      D->comp[2] = M->translucency;
+    }
+    if (M->diffuse_reflect * acc > 0.00001f) {
+      D->flags |= BSDF_DIFFUSE | BSDF_REFLECT;
+      D->cflags[n] = BSDF_DIFFUSE | BSDF_REFLECT;
+      D->cindex[n++] = 3;
+      D->comp[3] = M->diffuse_reflect;
+    }
+    D->ncomp = n;
+  }
 }
 
-/* shinyDiffuseMat_t::eval (diffuse subset), shinydiffuse.cc:223-249 */
-static col3 sd_eval(const yk_material* M, const surfpt* sp, v3 wo, v3 wl, unsigned bsdfs) {
+static const sdmat* mat_of(int m) { return &g_sd[m]; }
+static unsigned mat_flags(int m) { return g_sd[m].flags; }
+
+/* getFresnel, shinydiffuse.cc:100-122. Compiled form: c = |N.wo| (the
+ * face-forward sign folded into fabs), g tested as ior2 + c*c < 1,
+ * 0.5*(g-c)^2 as ((g-c)*(g-c))*0.5, aux = (g+c)*c. */
+static float sd_fresnel(const sdmat* M, v3 wo, v3 N) {
+  if (!M->fresnel) return 1.f;
+  float c = fabsf(N.x * wo.x + N.y * wo.y + N.z * wo.z);
+  float t = M->ior2 + c * c;
+  float g = (t < 1.f) ? 0.f : sqrtf(t - 1.f);
+  float gc = g + c, aux = gc * c;
+  float a = (((g - c) * (g - c)) * 0.5f) / (gc * gc);
+  float b = ((aux - 1.f) * (aux - 1.f)) / ((aux + 1.f) * (aux + 1.f)) + 1.f;
+  return b * a;
+}
+
+/* accumulate(), shinydiffuse.cc:124-133; compiled: accum3 = ((1-c2)*c3)*acc */
+static void sd_accum(const sdmat* M, float Kr, float* a) {
+  a[0] = Kr * M->comp[0];
+  float t = 1.f - a[0];
+  a[1] = t * M->comp[1];
+  float acc2 = (1.f - M->comp[1]) * t;
+  a[2] = acc2 * M->comp[2];
+  a[3] = ((1.f - M->comp[2]) * M->comp[3]) * acc2;
+}
+
+/* shinyDiffuseMat_t::eval, shinydiffuse.cc:223-249 (compiled: cos_Ng_wl as
+ * (y + z) + x; mD = ((1-c2)*c3)*mT) */
+static col3 sd_eval(const sdmat* M, const surfpt* sp, v3 wo, v3 wl, unsigned bsdfs) {
   if (M->type == YK_MAT_LIGHT) return C(0, 0, 0);
-  v3 N = (vdot(sp->Ng, wo) < 0) ? vneg(sp->N) : sp->N;
-  if (!(bsdfs & BSDF_DIFFUSE) || M->diffuse_reflect <= 0.00001f) return C(0, 0, 0);
-  float mT = (1.f - 1.f * 0.f) * (1.f - 0.f);
-  if (vdot(N, wl) < 0.0f) return C(0, 0, 0);
-  float mD = mT * (1.f - 0.f) * M->diffuse_reflect;
-  return cscale(mD, C(M->color[0], M->color[1], M->color[2]));
+  float cos_Ng_wo = vdot(sp->Ng, wo);
+  float cos_Ng_wl = (sp->Ng.y * wl.y + sp->Ng.z * wl.z) + sp->Ng.x * wl.x;
+  v3 N = (cos_Ng_wo < 0) ? vneg(sp->N) : sp->N;
+  if (!(bsdfs & M->flags & BSDF_DIFFUSE)) return C(0, 0, 0);
+  float Kr = sd_fresnel(M, wo, N);
+  float mT = (1.f - Kr * M->comp[0]) * (1.f - M->comp[1]);
+  if (cos_Ng_wo * cos_Ng_wl < 0.f && M->is_translucent) return cscale(mT * M->comp[2], M->diff);
+  if (vdot(wl, N) < 0.0f) return C(0, 0, 0);
+  float mD = ((1.f - M->comp[2]) * M->comp[3]) * mT;
+  return cscale(mD, M->diff);
 }
 
 /* SampleCosHemisphere, sample_utils.h:41-49 */
@@ -545,64 +642,162 @@ static v3 sample_cos_hemisphere(v3 N, v3 Ru, v3 Rv, float s1, float s2) {
   return vadd(vmul(sq1, vadd(vmul(c, Ru), vmul(s, Rv))), vmul(sqz, N));
 }
 
-/* shinyDiffuseMat_t::sample (diffuse-reflect component), shinydiffuse.cc:259-336 */
-static col3 sd_sample(const yk_material* M, const surfpt* sp, v3 wo, v3* wi, float s1in, float s2in,
-                      unsigned flags, float* pdf, float* W, int* ok) {
+/* shinyDiffuseMat_t::sample, shinydiffuse.cc:259-336; lightMat_t::sample
+ * (simple.cc:55-60). *ok = 0: early return with W and wi untouched.
+ * *sflags = s.sampledFlags. */
+static col3 sd_sample(const sdmat* M, const surfpt* sp, v3 wo, v3* wi, float s1in, float s2in, unsigned flags,
+                      float* pdf, float* W, int* ok, unsigned* sflags) {
   *ok = 1;
-  if (M->type == YK_MAT_LIGHT) { /* lightMat_t::sample, simple.cc:47-52 */
+  if (sflags) *sflags = 0;
+  if (M->type == YK_MAT_LIGHT) {
     *pdf = 0.f;
     *W = 0.f;
     return C(0, 0, 0);
   }
   float cos_Ng_wo = vdot(sp->Ng, wo);
   v3 N = (cos_Ng_wo < 0) ? vneg(sp->N) : sp->N;
-  float accum3 = M->diffuse_reflect * (((1.f - 0.f * 1.f) * (1.f - 0.f)) * (1.f - 0.f));
-  const unsigned cf = BSDF_DIFFUSE | BSDF_REFLECT;
-  if (M->diffuse_reflect <= 0.00001f || (flags & cf) != cf) {
+  float Kr = sd_fresnel(M, wo, N);
+  float a[4];
+  sd_accum(M, Kr, a);
+  float sum = 0.f, val[4], width[4];
+  unsigned choice[4];
+  int nMatch = 0, pick = -1;
+  for (int i = 0; i < M->ncomp; ++i) {
+    if ((flags & M->cflags[i]) == M->cflags[i]) {
+      width[nMatch] = a[M->cindex[i]];
+      sum += width[nMatch];
+      choice[nMatch] = M->cflags[i];
+      val[nMatch] = sum;
+      ++nMatch;
+    }
+  }
+  if (!nMatch || (double)sum < 0.00001) {
     *pdf = 0.f;
-    *ok = 0; /* W untouched, as the reference */
+    *ok = 0;
     return C(1.f, 1.f, 1.f);
   }
-  float width = accum3, sum = 0.f + width, val = sum;
-  if (sum < 0.00001f) { *pdf = 0.f; *ok = 0; return C(1.f, 1.f, 1.f); }
   float inv_sum = 1.f / sum;
-  val *= inv_sum;
-  width *= inv_sum;
-  (void)val;
-  float s1 = s1in / width;
-  *wi = sample_cos_hemisphere(N, sp->NU, sp->NV, s1, s2in);
-  float cos_Ng_wi = vdot(sp->Ng, *wi);
+  for (int i = 0; i < nMatch; ++i) {
+    val[i] *= inv_sum;
+    width[i] *= inv_sum;
+    if ((s1in <= val[i]) && (pick < 0)) pick = i;
+  }
+  if (pick < 0) pick = nMatch - 1;
+  float s1 = (pick > 0) ? (s1in - val[pick - 1]) / width[pick] : s1in / width[pick];
   col3 sc = C(0, 0, 0);
-  if (cos_Ng_wo * cos_Ng_wi > 0) sc = cscale(accum3, C(M->color[0], M->color[1], M->color[2]));
-  *pdf = fabsf(vdot(*wi, N)) * width;
-  *W = fabsf(vdot(*wi, sp->N)) / (*pdf * 0.99f + 0.01f);
+  v3 w;
+  switch (choice[pick]) {
+    case BSDF_SPECULAR | BSDF_REFLECT: { /* reflect_dir(N, wo), compiled vn = (x + z) + y */
+      float vn = (wo.x * N.x + wo.z * N.z) + N.y * wo.y;
+      if (vn < 0) w = vneg(wo);
+      else {
+        float v2 = vn + vn;
+        w = V(v2 * N.x - wo.x, v2 * N.y - wo.y, v2 * N.z - wo.z);
+      }
+      *pdf = width[pick];
+      sc = C(M->mirror.r * a[0], M->mirror.g * a[0], M->mirror.b * a[0]);
+      float k = 1.f / fabsf(vdot(w, sp->N));
+      sc = C(sc.r * k, sc.g * k, sc.b * k);
+      break;
+    }
+    case BSDF_TRANSMIT | BSDF_FILTER: {
+      w = vneg(wo);
+      float t = 1.f - M->tfilter;
+      sc = C((M->diff.r * M->tfilter + t) * a[1], (M->diff.g * M->tfilter + t) * a[1],
+             (M->diff.b * M->tfilter + t) * a[1]);
+      float cosN = fabsf(vdot(N, w));
+      *pdf = ((double)cosN < 1e-6) ? 0.f : width[pick];
+      break;
+    }
+    case BSDF_DIFFUSE | BSDF_TRANSMIT:
+      w = sample_cos_hemisphere(vneg(N), sp->NU, sp->NV, s1, s2in);
+      if (cos_Ng_wo * vdot(sp->Ng, w) < 0) sc = cscale(a[2], M->diff);
+      *pdf = fabsf(vdot(N, w)) * width[pick];
+      break;
+    default:
+      w = sample_cos_hemisphere(N, sp->NU, sp->NV, s1, s2in);
+      if (cos_Ng_wo * vdot(sp->Ng, w) > 0) sc = cscale(a[3], M->diff);
+      *pdf = fabsf(vdot(N, w)) * width[pick];
+      break;
+  }
+  *wi = w;
+  if (sflags) *sflags = choice[pick];
+  *W = fabsf(vdot(w, sp->N)) / (*pdf * 0.99f + 0.01f);
   return sc;
 }
 
-/* shinyDiffuseMat_t::pdf, shinydiffuse.cc:338-377 */
-static float sd_pdf(const yk_material* M, const surfpt* sp, v3 wo, v3 wi, unsigned bsdfs) {
+/* shinyDiffuseMat_t::pdf, shinydiffuse.cc:338-377: every component sharing a
+ * bit with bsdfs adds its width to the sum; only diffuse ones add pdf. */
+static float sd_pdf(const sdmat* M, const surfpt* sp, v3 wo, v3 wi, unsigned bsdfs) {
   if (M->type == YK_MAT_LIGHT) return 0.f;
   if (!(bsdfs & BSDF_DIFFUSE)) return 0.f;
-  v3 N = (vdot(sp->Ng, wo) < 0) ? vneg(sp->N) : sp->N;
-  if (M->diffuse_reflect <= 0.00001f) return 0.f;
-  float width = M->diffuse_reflect * (((1.f - 0.f * 1.f) * (1.f - 0.f)) * (1.f - 0.f));
-  float sum = 0.f + width;
-  float pdf = 0.f + fabsf(vdot(wi, N)) * width;
-  if (sum < 0.00001f) return 0.f;
+  float cos_Ng_wo = vdot(sp->Ng, wo);
+  v3 N = (cos_Ng_wo < 0) ? vneg(sp->N) : sp->N;
+  float Kr = sd_fresnel(M, wo, N);
+  float a[4];
+  sd_accum(M, Kr, a);
+  float sum = 0.f, pdf = 0.f;
+  int nMatch = 0;
+  for (int i = 0; i < M->ncomp; ++i) {
+    if (bsdfs & M->cflags[i]) {
+      float width = a[M->cindex[i]];
+      sum += width;
+      if (M->cflags[i] == (BSDF_DIFFUSE | BSDF_TRANSMIT)) {
+        if (cos_Ng_wo * vdot(sp->Ng, wi) < 0) pdf += fabsf(vdot(wi, N)) * width;
+      } else if (M->cflags[i] == (BSDF_DIFFUSE | BSDF_REFLECT)) {
+        pdf += fabsf(vdot(wi, N)) * width;
+      }
+      ++nMatch;
+    }
+  }
+  if (!nMatch || (double)sum < 0.00001) return 0.f;
   return pdf / sum;
+}
+
+/* shinyDiffuseMat_t::getSpecular, shinydiffuse.cc:379-433 (compiled: the
+ * backface test as (x + z) + y; reflect() without a sign test; the 0.01
+ * grazing correction in double) */
+static void sd_get_specular(const sdmat* M, const surfpt* sp, v3 wo, int* refl, int* refr, v3* dir, col3* col) {
+  *refl = *refr = 0;
+  if (M->type == YK_MAT_LIGHT) return; /* material_t::getSpecular default: none */
+  int backface = ((sp->Ng.x * wo.x + sp->Ng.z * wo.z) + sp->Ng.y * wo.y) < 0.f;
+  v3 N = backface ? vneg(sp->N) : sp->N;
+  v3 Ng = backface ? vneg(sp->Ng) : sp->Ng;
+  float Kr = sd_fresnel(M, wo, N);
+  if (M->is_transparent) {
+    *refr = 1;
+    dir[1] = vneg(wo);
+    float t = 1.f - M->tfilter;
+    float k = M->comp[1] * (1.f - M->comp[0] * Kr);
+    col[1] = C((M->diff.r * M->tfilter + t) * k, (M->diff.g * M->tfilter + t) * k, (M->diff.b * M->tfilter + t) * k);
+  }
+  if (M->is_mirror) {
+    *refl = 1;
+    float vn = vdot(wo, N);
+    float v2 = vn + vn;
+    v3 w = V(v2 * N.x - wo.x, v2 * N.y - wo.y, v2 * N.z - wo.z);
+    float cos_wi_Ng = vdot(w, Ng);
+    if ((double)cos_wi_Ng < 0.01) {
+      float f = (float)(0.01 - (double)cos_wi_Ng);
+      w = V(f * Ng.x + w.x, f * Ng.y + w.y, f * Ng.z + w.z);
+      w = vnormalize(w);
+    }
+    dir[0] = w;
+    float k = Kr * M->comp[0];
+    col[0] = C(M->mirror.r * k, M->mirror.g * k, M->mirror.b * k);
+  }
 }
 
 /* emit: shinyDiffuseMat_t::emit (shinydiffuse.cc:251-257), lightMat_t::emit
  * (simple.cc:54-61) */
-static col3 mat_emit(const yk_material* M, const surfpt* sp, v3 wo, int includeLights) {
+static col3 mat_emit(const sdmat* M, const surfpt* sp, v3 wo, int includeLights) {
   if (M->type == YK_MAT_LIGHT) {
     if (!includeLights) return C(0, 0, 0);
-    col3 lc = C(M->color[0] * M->power, M->color[1] * M->power, M->color[2] * M->power);
-    if (M->double_sided) return lc;
+    if (M->double_sided) return M->light_col;
     float angle = vdot(wo, sp->N);
-    return (angle > 0) ? lc : C(0, 0, 0);
+    return (angle > 0) ? M->light_col : C(0, 0, 0);
   }
-  return cscale(M->emit, C(M->color[0], M->color[1], M->color[2]));
+  return M->emit_col;
 }
 
 /* -------------------------------------------------------------- light -- */
@@ -740,13 +935,14 @@ typedef struct {
   int pixelSample;
   unsigned int samplingOffs;
   int includeLights;
+  int raylevel;
 } rstate;
 
 /* mcIntegrator_t::doLightEstimation (area-light branch), mcintegrator.cc:73-195 */
 static col3 do_light_estimation(rstate* st, int li, const surfpt* sp, v3 wo, unsigned loffs) {
   col3 col = C(0, 0, 0);
   const struct arealight* A = &G.al[li];
-  const yk_material* M = mat_of(sp->mat);
+  const sdmat* M = mat_of(sp->mat);
   if (A->type != YK_LIGHT_AREA) { /* diracLight(): mcintegrator.cc:85-100 */
     col3 lcol;
     v3 ldir;
@@ -806,7 +1002,8 @@ static col3 do_light_estimation(rstate* st, int li, const surfpt* sp, v3 wo, uns
     int ok;
     v3 bdir = V(0, 0, 0);
     col3 surf = sd_sample(M, sp, wo, &bdir, s1, s2,
-                          BSDF_GLOSSY | BSDF_DIFFUSE | BSDF_DISPERSIVE | BSDF_REFLECT | BSDF_TRANSMIT, &spdf, &W, &ok);
+                          BSDF_GLOSSY | BSDF_DIFFUSE | BSDF_DISPERSIVE | BSDF_REFLECT | BSDF_TRANSMIT, &spdf, &W, &ok,
+                          NULL);
     float bt, lightPdf;
     col3 lcol;
     if (spdf > 1e-6f && al_intersect(A, sp->P, bdir, &bt, &lcol, &lightPdf)) {
@@ -853,19 +1050,51 @@ static col3 estimate_one_direct(rstate* st, const surfpt* sp, v3 wo, int n) {
 
 typedef struct { float r, g, b, a; } rgba;
 
+static rgba integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir, float tmin, float tmax);
+
+/* mcIntegrator_t::recursiveRaytrace, mcintegrator.cc:421-627: perfect
+ * specular reflection / refraction (shinydiffuse has no glossy or
+ * dispersive components). The state (includeLights, raylevel) is shared
+ * with the recursive integrate() calls, as in the reference. */
+static void recursive_raytrace(rstate* st, const yk_render_params* P, const surfpt* sp, unsigned bsdfs, v3 wo,
+                               col3* col, float* alpha) {
+  const sdmat* M = mat_of(sp->mat);
+  st->raylevel++;
+  if (st->raylevel <= P->raydepth) {
+    if ((bsdfs & (BSDF_SPECULAR | BSDF_FILTER)) && st->raylevel < 20) {
+      st->includeLights = 1;
+      int refl, refr;
+      v3 d[2];
+      col3 rc[2];
+      sd_get_specular(M, sp, wo, &refl, &refr, d, rc);
+      if (refl) {
+        rgba integ = integrate(st, P, sp->P, d[0], MIN_RAYDIST, -1.0f);
+        *col = cadd(*col, C(integ.r * rc[0].r, integ.g * rc[0].g, integ.b * rc[0].b));
+      }
+      if (refr) {
+        rgba integ = integrate(st, P, sp->P, d[1], MIN_RAYDIST, -1.0f);
+        *col = cadd(*col, C(integ.r * rc[1].r, integ.g * rc[1].g, integ.b * rc[1].b));
+        *alpha = integ.a;
+      }
+    }
+  }
+  st->raylevel--;
+}
+
 /* pathIntegrator_t::integrate, pathtracer.cc:134-333 */
 static rgba pt_integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir, float tmin, float tmax) {
   col3 col = C(0, 0, 0);
   float alpha = P->transp_background ? 0.0f : 1.0f;
   surfpt sp;
+  const int traceCaustics = P->caustic_type == YK_CAUSTIC_PATH;
   if (scene_intersect(from, dir, tmin, &tmax, &sp)) {
-    st->includeLights = 1;
-    const yk_material* M = mat_of(sp.mat);
+    if (st->raylevel == 0) st->includeLights = 1;
+    const sdmat* M = mat_of(sp.mat);
     unsigned bsdfs = mat_flags(sp.mat);
     v3 wo = vneg(dir);
     if (bsdfs & BSDF_EMIT) col = cadd(col, mat_emit(M, &sp, wo, st->includeLights));
     if (bsdfs & BSDF_DIFFUSE) col = cadd(col, estimate_all_direct(st, &sp, wo));
-    if (bsdfs & BSDF_DIFFUSE) {
+    if (bsdfs & BSDF_DIFFUSE) { /* path_flags = BSDF_DIFFUSE (no_recursive off) */
       col3 pathCol = C(0, 0, 0);
       unsigned path_flags = BSDF_DIFFUSE | BSDF_REFLECT | BSDF_TRANSMIT;
       int nSamples = P->path_samples > 1 ? P->path_samples : 1;
@@ -879,44 +1108,53 @@ static rgba pt_integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir,
         float s2 = (float)scrHalton(2, offs);
         float spdf;
         int ok;
-        scol = sd_sample(M, &sp, pwo, &pdir, s1, s2, path_flags, &spdf, &W, &ok);
+        unsigned sfl;
+        scol = sd_sample(M, &sp, pwo, &pdir, s1, s2, path_flags, &spdf, &W, &ok, &sfl);
         scol = cscale(W, scol);
         throughput = scol;
         st->includeLights = 0;
         float ptmax = -1.0f;
         if (!scene_intersect(sp.P, pdir, MIN_RAYDIST, &ptmax, &hit)) continue;
-        const yk_material* pm = mat_of(hit.mat);
+        const sdmat* pm = mat_of(hit.mat);
         unsigned matBSDFs = mat_flags(hit.mat);
         pwo = vneg(pdir);
         lcol = estimate_one_direct(st, &hit, pwo, (int)offs);
         if (matBSDFs & BSDF_EMIT) lcol = cadd(lcol, mat_emit(pm, &hit, pwo, st->includeLights));
         pathCol = cadd(pathCol, cmul(lcol, throughput));
+        int caustic = 0;
         for (int depth = 1; depth < P->bounces; ++depth) {
           int d4 = 4 * depth;
           float ss1 = (float)scrHalton(d4 + 3, offs);
           float ss2 = (float)scrHalton(d4 + 4, offs);
-          scol = sd_sample(pm, &hit, pwo, &pdir, ss1, ss2, BSDF_ALL, &spdf, &W, &ok);
+          /* pRay.dir keeps the previous direction when sample() returns early */
+          scol = sd_sample(pm, &hit, pwo, &pdir, ss1, ss2, BSDF_ALL, &spdf, &W, &ok, &sfl);
           scol = cscale(W, scol);
           if (cblack(scol)) break;
           throughput = cmul(throughput, scol);
-          st->includeLights = 0; /* caustic = traceCaustics && ... ; NONE/diffuse -> false */
+          caustic = traceCaustics && (sfl & (BSDF_SPECULAR | BSDF_GLOSSY | BSDF_FILTER));
+          st->includeLights = caustic;
           surfpt hit2;
           ptmax = -1.0f;
-          if (!scene_intersect(hit.P, pdir, MIN_RAYDIST, &ptmax, &hit2)) break;
+          if (!scene_intersect(hit.P, pdir, MIN_RAYDIST, &ptmax, &hit2)) {
+            if (caustic && G.has_bg) pathCol = cadd(pathCol, cmul(throughput, G.bg));
+            break;
+          }
           hit = hit2;
           pm = mat_of(hit.mat);
           matBSDFs = mat_flags(hit.mat);
           pwo = vneg(pdir);
           if (matBSDFs & BSDF_DIFFUSE) lcol = estimate_one_direct(st, &hit, pwo, (int)offs);
           else lcol = C(0, 0, 0);
-          /* "matBSDFs & (BSDF_EMIT && caustic)": caustic is false here */
+          /* "matBSDFs & (BSDF_EMIT && caustic)" == matBSDFs & BSDF_SPECULAR when caustic */
+          if (caustic && (matBSDFs & BSDF_SPECULAR)) lcol = cadd(lcol, mat_emit(pm, &hit, pwo, st->includeLights));
           pathCol = cadd(pathCol, cmul(lcol, throughput));
         }
       }
       float ns = (float)nSamples;
       col = cadd(col, C(pathCol.r / ns, pathCol.g / ns, pathCol.b / ns));
     }
-    alpha = 1.0f; /* getAlpha of opaque shinydiffuse/light_mat = 1 */
+    recursive_raytrace(st, P, &sp, bsdfs, wo, &col, &alpha);
+    alpha = 1.0f; /* transpRefractedBackground off */
   } else if (G.has_bg) { /* nothing hit, return background (pathtracer.cc:318-324) */
     col = cadd(col, G.bg);
   }
@@ -928,20 +1166,28 @@ static rgba pt_integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir,
 static rgba dl_integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir, float tmin, float tmax) {
   col3 col = C(0, 0, 0);
   float alpha = P->transp_background ? 0.0f : 1.0f;
+  int oldIncludeLights = st->includeLights;
   surfpt sp;
   if (scene_intersect(from, dir, tmin, &tmax, &sp)) {
-    const yk_material* M = mat_of(sp.mat);
+    const sdmat* M = mat_of(sp.mat);
     unsigned bsdfs = mat_flags(sp.mat);
     v3 wo = vneg(dir);
-    st->includeLights = 1;
+    if (st->raylevel == 0) st->includeLights = 1;
     if (bsdfs & BSDF_EMIT) col = cadd(col, mat_emit(M, &sp, wo, st->includeLights));
     if (bsdfs & BSDF_DIFFUSE) col = cadd(col, estimate_all_direct(st, &sp, wo));
+    recursive_raytrace(st, P, &sp, bsdfs, wo, &col, &alpha);
     alpha = 1.0f;
   } else if (G.has_bg) { /* directlight.cc:163-166 */
     col = cadd(col, G.bg);
   }
+  st->includeLights = oldIncludeLights;
   rgba r = {col.r, col.g, col.b, alpha};
   return r;
+}
+
+static rgba integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir, float tmin, float tmax) {
+  return (P->integrator == YK_INTEGRATOR_DIRECT) ? dl_integrate(st, P, from, dir, tmin, tmax)
+                                                 : pt_integrate(st, P, from, dir, tmin, tmax);
 }
 
 /* ------------------------------------------------------------- film -- */
@@ -1040,6 +1286,7 @@ int orc_load(const float* tri_verts, const int32_t* tri_mat, int32_t ntris, cons
   }
   camera_setup();
   lights_setup();
+  mats_setup();
   return 0;
 }
 
@@ -1158,6 +1405,7 @@ static int render_tiles(const yk_render_params* P, int shard, int nshards, float
           rstate st;
           st.samplingOffs = fnv_32a_buf((unsigned)i * fnv_32a_buf((unsigned)j));
           st.includeLights = 0;
+          st.raylevel = 0;
           for (int s = 0; s < n; ++s) {
             st.pixelSample = s;
             float dx = 0.5f, dy = 0.5f;
@@ -1165,8 +1413,7 @@ static int render_tiles(const yk_render_params* P, int shard, int nshards, float
             v3 from, dir;
             float tmin, tmax;
             camera_ray((float)j + dx, (float)i + dy, &from, &dir, &tmin, &tmax);
-            rgba c = (P->integrator == YK_INTEGRATOR_DIRECT) ? dl_integrate(&st, P, from, dir, tmin, tmax)
-                                                            : pt_integrate(&st, P, from, dir, tmin, tmax);
+            rgba c = integrate(&st, P, from, dir, tmin, tmax);
             c.r = 1.f * c.r; c.g = 1.f * c.g; c.b = 1.f * c.b; c.a = 1.f * c.a; /* wt * col */
             film_add(&F, c, j, i, dx, dy);
           }

@@ -104,3 +104,28 @@ def dirac_lights(resx, resy, integrator="cornell_pt", with_dirac=True):
     s.set_background(*BACKGROUND)
     s.build()
     return s, p
+
+
+def specular(resx, resy, integrator="cornell_pt", raydepth=3, caustic=False, nu=16, nv=10):
+    """Cornell box + a mirror sphere, a glass-like sphere (fresnel mirror +
+    transparency with a transmit filter) and a translucent sphere:
+    shinyDiffuseMat_t's specular / transmissive components and
+    recursiveRaytrace (mcintegrator.cc:421-627), §8(f) f1."""
+    s = Scene()
+    p = s.generate(integrator, resx, resy)
+    mirror = s.add_material(color=(0.9, 0.9, 0.9), diffuse_reflect=1.0, specular_reflect=0.85,
+                            mirror_color=(0.95, 0.9, 0.8))
+    glass = s.add_material(color=(0.6, 0.8, 1.0), diffuse_reflect=0.3, specular_reflect=1.0, fresnel_effect=True,
+                           ior=1.5, transparency=0.9, transmit_filter=0.6)
+    transl = s.add_material(color=(0.9, 0.7, 0.3), diffuse_reflect=0.5, translucency=0.6)
+    for (cx, cy, cz, r), m in (((-0.35, 1.42, 0.3, 0.22), mirror), ((0.4, 0.85, -0.3, 0.25), glass),
+                               ((0.0, 0.22, -0.6, 0.2), transl)):
+        pts, faces, nrm = uv_sphere(nu, nv, r, (cx, cy, cz))
+        oid = s.add_mesh(pts, faces, m)
+        s.set_mesh_normals(oid, nrm, faces, smooth=True)
+    if caustic:  # a caustic segment that escapes adds the background (pathtracer.cc:279-286)
+        s.set_background((0.3, 0.4, 0.5), 1.0)
+    s.build()
+    p.raydepth = raydepth
+    p.caustic_type = 1 if caustic else 0
+    return s, p

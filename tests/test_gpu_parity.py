@@ -13,7 +13,7 @@ from core_amd import _abi as A
 from core_amd.scene import probe_scene
 from oracle.oracle import Oracle
 from tests.raygen import edge_rays, random_rays
-from tests.scenes import dirac_lights, smooth_instanced
+from tests.scenes import dirac_lights, smooth_instanced, specular
 
 pytestmark = pytest.mark.gpu
 
@@ -28,6 +28,8 @@ def scene(name, resx, resy, nu=0, nv=0):
             s, p, _ = smooth_instanced(resx, resy, gen)
         elif name.startswith("dirac"):  # point + directional lights, constant background (§8 f1)
             s, p = dirac_lights(resx, resy, gen)
+        elif name.startswith("spec"):  # mirror / glass / translucent shinydiffuse + recursiveRaytrace (§8 f1)
+            s, p = specular(resx, resy, gen, raydepth=nu or 3, caustic=bool(nv))
         else:
             s, p = probe_scene(name, resx, resy, nu, nv)
         _SCENES[key] = (s, p, Oracle(s))
@@ -120,6 +122,11 @@ RENDER_CASES = [
     ("pt_dirac_bg", ("dirac", 72, 72, 0, 0), (0, 0, 72, 72), {}),
     ("dl_dirac_bg", ("dirac_dl", 72, 72, 0, 0), (0, 0, 72, 72), {}),
     ("pt_dirac_bg_opaque", ("dirac", 72, 72, 0, 0), (4, 4, 60, 60), {"transp_background": 0, "path_samples": 2}),
+    # specular / transmissive shinydiffuse + recursiveRaytrace (§8 f1): scene arg nu = raydepth, nv = caustic path
+    ("pt_spec_rd3", ("spec", 64, 64, 3, 0), (0, 0, 64, 64), {}),
+    ("dl_spec_rd3", ("spec_dl", 64, 64, 3, 0), (0, 0, 64, 64), {}),
+    ("pt_spec_rd5_caustic", ("spec", 64, 64, 5, 1), (0, 0, 64, 64), {"path_samples": 2}),
+    ("pt_spec_rd1_b5", ("spec", 48, 48, 1, 0), (0, 0, 48, 48), {"bounces": 5}),
 ]
 
 
