@@ -73,6 +73,27 @@ YK_MEMBER(InstBase, triangleObjectInstance_t, triangleObject_t*, mBase)
 YK_MEMBER(SdColor, shinyDiffuseMat_t, color_t, mDiffuseColor)
 YK_MEMBER(SdStrength, shinyDiffuseMat_t, float, mDiffuseStrength)
 YK_MEMBER(SdEmit, shinyDiffuseMat_t, color_t, mEmitColor)
+YK_MEMBER(SdMirrorColor, shinyDiffuseMat_t, color_t, mMirrorColor)
+YK_MEMBER(SdMirror, shinyDiffuseMat_t, float, mMirrorStrength)
+YK_MEMBER(SdTransp, shinyDiffuseMat_t, float, mTransparencyStrength)
+YK_MEMBER(SdTransl, shinyDiffuseMat_t, float, mTranslucencyStrength)
+YK_MEMBER(SdFilter, shinyDiffuseMat_t, float, mTransmitFilterStrength)
+YK_MEMBER(SdIsMirror, shinyDiffuseMat_t, bool, mIsMirror)
+YK_MEMBER(SdIsTransparent, shinyDiffuseMat_t, bool, mIsTransparent)
+YK_MEMBER(SdIsTranslucent, shinyDiffuseMat_t, bool, mIsTranslucent)
+YK_MEMBER(SdIsDiffuse, shinyDiffuseMat_t, bool, mIsDiffuse)
+YK_MEMBER(SdFresnel, shinyDiffuseMat_t, bool, mHasFresnelEffect)
+YK_MEMBER(SdIor2, shinyDiffuseMat_t, float, mIOR_Squared)
+YK_MEMBER(SdOrenNayar, shinyDiffuseMat_t, bool, mUseOrenNayar)
+YK_MEMBER(SdNBSDF, shinyDiffuseMat_t, int, nBSDF)
+YK_MEMBER(SdCFlags, shinyDiffuseMat_t, BSDF_t[4], cFlags)
+YK_MEMBER(SdCIndex, shinyDiffuseMat_t, int[4], cIndex)
+YK_MEMBER(SdDiffuseShader, shinyDiffuseMat_t, shaderNode_t*, mDiffuseShader)
+YK_MEMBER(SdBumpShader, shinyDiffuseMat_t, shaderNode_t*, mBumpShader)
+YK_MEMBER(SdMirrorShader, shinyDiffuseMat_t, shaderNode_t*, mMirrorShader)
+YK_MEMBER(SdMirrorColorShader, shinyDiffuseMat_t, shaderNode_t*, mMirrorColorShader)
+YK_MEMBER(SdTranspShader, shinyDiffuseMat_t, shaderNode_t*, mTransparencyShader)
+YK_MEMBER(SdTranslShader, shinyDiffuseMat_t, shaderNode_t*, mTranslucencyShader)
 YK_MEMBER(AlCorner, areaLight_t, point3d_t, corner)
 YK_MEMBER(AlToX, areaLight_t, vector3d_t, toX)
 YK_MEMBER(AlToY, areaLight_t, vector3d_t, toY)
@@ -328,10 +349,29 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     s.bsdf_flags = m->getFlags();
     if (const shinyDiffuseMat_t* sd = dynamic_cast<const shinyDiffuseMat_t*>(m)) {
       s.type = YK_MAT_SHINYDIFFUSE;
-      const color_t &c = GET(*sd, SdColor), &e = GET(*sd, SdEmit);
+      if (GET(*sd, SdDiffuseShader) || GET(*sd, SdBumpShader) || GET(*sd, SdMirrorShader) ||
+          GET(*sd, SdMirrorColorShader) || GET(*sd, SdTranspShader) || GET(*sd, SdTranslShader))
+        return unsupported("textured (shader-node) shinydiffuse is not on the GPU path");
+      if (GET(*sd, SdOrenNayar)) return unsupported("Oren-Nayar shinydiffuse is not on the GPU path");
+      const color_t &c = GET(*sd, SdColor), &e = GET(*sd, SdEmit), &mc = GET(*sd, SdMirrorColor);
       put3(s.color, c.R, c.G, c.B);
       put3(s.emit_color, e.R, e.G, e.B);
+      put3(s.mirror_color, mc.R, mc.G, mc.B);
       s.diffuse_strength = GET(*sd, SdStrength);
+      // getComponents (shinydiffuse.cc:82-98): the strengths of the
+      // components config() enabled, 0 elsewhere
+      s.component[0] = GET(*sd, SdIsMirror) ? GET(*sd, SdMirror) : 0.f;
+      s.component[1] = GET(*sd, SdIsTransparent) ? GET(*sd, SdTransp) : 0.f;
+      s.component[2] = GET(*sd, SdIsTranslucent) ? GET(*sd, SdTransl) : 0.f;
+      s.component[3] = GET(*sd, SdIsDiffuse) ? GET(*sd, SdStrength) : 0.f;
+      s.ncomp = GET(*sd, SdNBSDF);
+      for (int k = 0; k < 4; ++k) {
+        s.comp_flags[k] = GET(*sd, SdCFlags)[k];
+        s.comp_index[k] = GET(*sd, SdCIndex)[k];
+      }
+      s.transmit_filter = GET(*sd, SdFilter);
+      s.has_fresnel = GET(*sd, SdFresnel) ? 1 : 0;
+      s.ior_squared = GET(*sd, SdIor2);
     } else if (s.bsdf_flags == BSDF_EMIT) {
       // lightMat_t is defined in a .cc (simple.cc:36-70): read lightCol and
       // doubleSided back through its virtual emit()
