@@ -215,7 +215,31 @@ __device__ __forceinline__ bool trav_begin(const DScene& S, Trav& st, const yk_r
 // the near child is the right one and the left is pushed unless split < exit.
 // (The reference's "exit == split" branch follows "exit <= split" and is
 // never taken, NaN included.)
+// Triangle test of one leaf entry; true when an any-hit query is done.
 template <bool CLOSEST>
+__device__ __forceinline__ bool leaf_test(Trav& st, uint32_t p, float4 A, float4 E1, float4 E2, bool& occluded) {
+  float th, u, v;
+  if (mt_intersect(V3(A.x, A.y, A.z), V3(E1.x, E1.y, E1.z), V3(E2.x, E2.y, E2.z), st.o, st.d, th, u, v)) {
+    if (CLOSEST) {
+      if (th < st.Z && th >= st.tmin) {
+        st.Z = th;
+        st.prim = (int)p;
+        st.b1 = u;
+        st.b2 = v;
+      }
+    } else if (th < st.dist && th >= 0.f) {
+      occluded = true;
+      return true;
+    }
+  }
+  return false;
+}
+
+// PIPE: leaf loop software-pipelined one triangle ahead (the next entry's
+// index and vertices are loaded while the current one is tested). Used for
+// scenes with crowded leaves (hair: ~40 references per leaf), where the plain
+// loop pays two dependent memory round trips per triangle.
+template <bool CLOSEST, bool PIPE>
 __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneStack& stk, unsigned& nnodes,
                                           unsigned& ntris, bool& occluded) {
   if (st.dist < st.en_t) return true;
@@ -245,27 +269,39 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
     nnodes++;
   }
   const uint32_t n = nd.y >> 2, w0 = nd.x;
-  for (uint32_t i = 0; i < n; ++i) {
-    const uint32_t p = (n == 1) ? w0 : S.leaf[w0 + i];
-    ntris++;
+  if (!PIPE) {
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t p = (n == 1) ? w0 : S.leaf[w0 + i];
+      ntris++;
+      float4 A = S.tris[3 * p], E1 = S.tris[3 * p + 1], E2 = S.tris[3 * p + 2];
+      // keep the three loads together (the compiler would otherwise sink A's
+      // load past the det test: a second dependent round trip per triangle)
+      asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
+                   "+v"(E2.y), "+v"(E2.z));
+      if (leaf_test<CLOSEST>(st, p, A, E1, E2, occluded)) return true;
+    }
+  } else if (n > 0) {
+    uint32_t p = (n == 1) ? w0 : S.leaf[w0];
     float4 A = S.tris[3 * p], E1 = S.tris[3 * p + 1], E2 = S.tris[3 * p + 2];
-    // keep the three loads together (the compiler would otherwise sink A's
-    // load past the det test: a second dependent round trip per triangle)
-    asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x), "+v"(E2.y),
-                 "+v"(E2.z));
-    float th, u, v;
-    if (mt_intersect(V3(A.x, A.y, A.z), V3(E1.x, E1.y, E1.z), V3(E2.x, E2.y, E2.z), st.o, st.d, th, u, v)) {
-      if (CLOSEST) {
-        if (th < st.Z && th >= st.tmin) {
-          st.Z = th;
-          st.prim = (int)p;
-          st.b1 = u;
-          st.b2 = v;
-        }
-      } else if (th < st.dist && th >= 0.f) {
-        occluded = true;
-        return true;
+    uint32_t pn = (n > 1) ? S.leaf[w0 + 1] : 0u;
+    for (uint32_t i = 0; i < n; ++i) {
+      float4 An = A, E1n = E1, E2n = E2;
+      uint32_t pnn = 0u;
+      if (i + 1 < n) {
+        An = S.tris[3 * pn];
+        E1n = S.tris[3 * pn + 1];
+        E2n = S.tris[3 * pn + 2];
       }
+      if (i + 2 < n) pnn = S.leaf[w0 + i + 2];
+      asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
+                   "+v"(E2.y), "+v"(E2.z));
+      ntris++;
+      if (leaf_test<CLOSEST>(st, p, A, E1, E2, occluded)) return true;
+      A = An;
+      E1 = E1n;
+      E2 = E2n;
+      p = pn;
+      pn = pnn;
     }
   }
   if (CLOSEST && st.prim >= 0 && st.Z <= st.ex_t) return true;
@@ -311,7 +347,7 @@ struct RayCount {
   }
 };
 
-template <bool CLOSEST, int NSEG>
+template <bool CLOSEST, int NSEG, bool PIPE>
 __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx,
                                            RayCount rc, yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
                                            unsigned long long* __restrict__ work, unsigned long long* __restrict__ ctr,
@@ -399,7 +435,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
     const bool runaway = ++iters > (1u << 30);
     if (rid >= 0) {
       bool occ = false;
-      bool done = trav_step<CLOSEST>(S, st, stk, nnodes, ntris, occ);
+      bool done = trav_step<CLOSEST, PIPE>(S, st, stk, nnodes, ntris, occ);
       if (runaway) {
         st.prim = -2;
         done = true;
@@ -449,13 +485,33 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOS
 k_trace_closest(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                 yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                 unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<true, 8>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+  trace_body<true, 8, false>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
 k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false, 1>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+  trace_body<false, 1, false>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+}
+// crowded-leaf variants (PIPE leaf loop): one wave fewer per SIMD buys the
+// registers of the prefetched triangle without spilling
+#ifndef YK_CLOSEST_LP_WAVES
+#define YK_CLOSEST_LP_WAVES 4
+#endif
+#ifndef YK_SHADOW_LP_WAVES
+#define YK_SHADOW_LP_WAVES 5
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_LP_WAVES)))
+k_trace_closest_lp(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+                   yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
+                   unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
+  trace_body<true, 8, true>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+}
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_LP_WAVES)))
+k_trace_shadow_lp(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+                  yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
+                  unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
+  trace_body<false, 1, true>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 
 // ============================================================ shading
@@ -1771,6 +1827,8 @@ struct yk_device {
   DScene S{};
   int ntris = 0, max_depth = 0, nlights = 0, sum_light_slots = 0;
   bool spec = false;  // some material has SPECULAR|FILTER components: recursion pipeline
+  bool crowded_leaves = false;  // mean references per non-empty leaf above kCrowdedLeaf: PIPE leaf loop
+  int per_cu_lp[2] = {1, 1};
   // node store of the specular recursion (k_finish_spec / k_spawn / k_fold)
   DBuf<float> nE, nD, nP, nrcol, nalpha;
   DBuf<int> nflags, nchild, noverflow;
@@ -1951,12 +2009,14 @@ int refill_min() {
 template <bool CLOSEST>
 void enqueue_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* idx, RayCount n, yk_hit* hits,
                    uint8_t* occ, unsigned long long* work, unsigned long long* acc, hipEvent_t ev0, hipEvent_t ev1) {
-  const long long grid = (long long)d->cus * d->per_cu[CLOSEST];
+  const bool lp = d->crowded_leaves;
+  const long long grid = (long long)d->cus * (lp ? d->per_cu_lp[CLOSEST] : d->per_cu[CLOSEST]);
   const int ovf_depth = std::max(1, stack_depth(d) - kStackLds);
   P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
   if (ev0) HIPCHK(hipEventRecord(ev0, P.stream));
-  hipLaunchKernelGGL(CLOSEST ? k_trace_closest : k_trace_shadow, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays,
-                     idx, n, hits, occ, work, acc, P.ovf.p, ovf_depth, refill_min());
+  auto kern = CLOSEST ? (lp ? k_trace_closest_lp : k_trace_closest) : (lp ? k_trace_shadow_lp : k_trace_shadow);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays, idx, n, hits, occ, work, acc,
+                     P.ovf.p, ovf_depth, refill_min());
   HIPCHK(hipGetLastError());
   if (ev1) HIPCHK(hipEventRecord(ev1, P.stream));
 }
@@ -2020,6 +2080,10 @@ int yk_device_open(int32_t ordinal, yk_device** out) {
   d->per_cu[0] = std::max(1, blocks);
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_closest, 64, 0));
   d->per_cu[1] = std::max(1, blocks);
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow_lp, 64, 0));
+  d->per_cu_lp[0] = std::max(1, blocks);
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_closest_lp, 64, 0));
+  d->per_cu_lp[1] = std::max(1, blocks);
   upload_qmc();
   *out = d;
   return YK_OK;
@@ -2113,6 +2177,15 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   std::memcpy(d->S.bound, S.tree.bound, sizeof d->S.bound);
   d->S.nlights = (int)S.light_states.size();
   d->S.nnodes = (unsigned)nn;
+  {
+    static const double crowd = [] {
+      const char* e = std::getenv("YK_CROWDED_LEAF");
+      return e ? std::atof(e) : 8.0;
+    }();
+    const long long filled = (long long)S.tree.stats.leaves - S.tree.stats.empty_leaves;
+    const double mean = filled > 0 ? (double)S.tree.stats.leaf_prims / (double)filled : 0.0;
+    d->crowded_leaves = mean > crowd;
+  }
   d->nlights = (int)S.light_states.size();
   d->ntris = nt;
   d->max_depth = S.tree.max_depth;
