@@ -17,9 +17,16 @@
 
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <exception>
 #include <limits>
+#include <memory>
+#include <mutex>
 #include <stdexcept>
+#include <thread>
 
 namespace yk {
 namespace {
@@ -177,11 +184,49 @@ int tri_plane_clip(double pos, int axis, bool lower, Bound& box, const ClipDump*
   return 0;
 }
 
+// Subtree build jobs of the parallel build (see build_kdtree): a node whose
+// subtree is built by another Builder; stitched back in depth-first order.
+struct SubtreeTask {
+  std::vector<uint32_t> prims;
+  Bound bound;
+  int depth, badRefines;
+};
+constexpr uint32_t kTaskMarker = 0xFFFFFFFFu;  // word1 of a placeholder node
+
+struct TaskSink {
+  virtual uint32_t add(SubtreeTask&& t) = 0;  // returns the task id
+  uint32_t maxPrims = 0;                      // spawn nodes with kTriClipThresh < nPrims <= maxPrims
+  virtual ~TaskSink() = default;
+};
+
 class Builder {
  public:
   Builder(const float* verts, int np, KdTree& out, int depth, int leafSize, float costRatio,
           float emptyBonus)
-      : V(verts), totalPrims(np), T(out), costRatio(costRatio), eBonus(emptyBonus), maxDepth(depth) {}
+      : V(verts), totalPrims(np), T(out), costRatio(costRatio), eBonus(emptyBonus), eBonus0(emptyBonus),
+        maxDepth(depth) {}
+
+  // subtree builder sharing the prepared state of a top-level builder (all
+  // of it fixed before the top-level recursion starts; eBonus is the base
+  // value -- the running builder changes and restores its own copy per call)
+  Builder(const Builder& top, KdTree& out)
+      : V(top.V), totalPrims(top.totalPrims), T(out), costRatio(top.costRatio), eBonus(top.eBonus0),
+        eBonus0(top.eBonus0),
+        maxDepth(top.maxDepth), maxLeafSize(top.maxLeafSize), treeBound(top.treeBound), bounds(top.bounds) {
+    initScratch();
+  }
+
+  void buildSubtree(SubtreeTask& t) {
+    leftPrims.assign(std::max<size_t>(2 * kTriClipThresh, t.prims.size()), 0);
+    std::copy(t.prims.begin(), t.prims.end(), leftPrims.begin());
+    rightMem0 = 3u * (uint32_t)t.prims.size();
+    rightPrims.assign(rightMem0 + 4 * kTriClipThresh, 0);
+    T.nodes.reserve(t.prims.size() * 4 + 16);
+    buildTree((uint32_t)t.prims.size(), t.bound, leftPrims.data(), leftPrims.data(), rightPrims.data(), rightMem0,
+              t.depth, t.badRefines);
+  }
+
+  TaskSink* sink = nullptr;
 
   void run() {
     // kdtree.cc:84-99
@@ -195,7 +240,8 @@ class Builder {
     T.max_depth = maxDepth;
 
     // kdtree.cc:100-115 triangle bounds, tree bound, 0.1% inflation
-    allBounds.resize(totalPrims + kTriClipThresh + 1);
+    allBounds.resize(totalPrims);
+    bounds = allBounds.data();
     Bound tb;
     for (int i = 0; i < totalPrims; i++) {
       const float* t = V + 9 * (size_t)i;
@@ -227,9 +273,7 @@ class Builder {
     rightMem0 = 3u * (uint32_t)totalPrims;
     leftPrims.assign(std::max((uint32_t)(2 * kTriClipThresh), (uint32_t)totalPrims), 0);
     rightPrims.assign(rightMem0 + 4 * kTriClipThresh, 0);
-    for (int i = 0; i < 3; ++i) edges[i].resize(514);
-    clip.assign(maxDepth + 2, -1);
-    cdata.resize((size_t)(maxDepth + 2) * kTriClipThresh);
+    initScratch();
     for (int i = 0; i < totalPrims; i++) leftPrims[i] = (uint32_t)i;
 
     T.nodes.clear();
@@ -243,16 +287,25 @@ class Builder {
   const float* V;
   int totalPrims;
   KdTree& T;
-  float costRatio, eBonus;
+  float costRatio, eBonus, eBonus0;
   int maxDepth;
   unsigned maxLeafSize = 1;
   Bound treeBound;
-  std::vector<Bound> allBounds;
+  std::vector<Bound> allBounds;      // owned by the top-level builder
+  const Bound* bounds = nullptr;      // triangle bounds (shared, read only)
+  std::vector<Bound> clipBounds;      // bounds of clipped prims of the current small node
   std::vector<uint32_t> leftPrims, rightPrims;
   uint32_t rightMem0 = 0;
   std::vector<BoundEdge> edges[3];
   std::vector<int> clip;
   std::vector<ClipDump> cdata;
+
+  void initScratch() {
+    for (int i = 0; i < 3; ++i) edges[i].resize(514);
+    clip.assign(maxDepth + 2, -1);
+    cdata.resize((size_t)(maxDepth + 2) * kTriClipThresh);
+    clipBounds.resize(kTriClipThresh + 1);
+  }
 
   uint32_t newNode() {
     T.nodes.push_back(0);
@@ -325,7 +378,7 @@ class Builder {
       const float s = (float)kKdBins / d[axis];
       const float mn = nb.a[axis];
       for (uint32_t i = 0; i < nPrims; ++i) {
-        const Bound& bbox = allBounds[primIdx[i]];
+        const Bound& bbox = bounds[primIdx[i]];
         float t_low = bbox.a[axis];
         float t_up = bbox.g[axis];
         int b_left = (int)((t_low - mn) * s);
@@ -500,6 +553,20 @@ class Builder {
   // buildTree, kdtree.cc:462-666
   int buildTree(uint32_t nPrims, const Bound& nodeBound, uint32_t* primNums, uint32_t* lPrims,
                 uint32_t* rPrims, uint32_t rightMemSize, int depth, int badRefines) {
+    if (sink && depth > 0 && nPrims > (uint32_t)kTriClipThresh && nPrims <= sink->maxPrims) {
+      // parallel build: this subtree depends only on (prims, bound, depth,
+      // badRefines) -- clip state is -1 above the clipping threshold and
+      // eBonus is restored by every call -- so another Builder builds it
+      SubtreeTask t;
+      t.prims.assign(primNums, primNums + nPrims);
+      t.bound = nodeBound;
+      t.depth = depth;
+      t.badRefines = badRefines;
+      const uint32_t n = newNode();
+      T.nodes[2 * n] = sink->add(std::move(t));
+      T.nodes[2 * n + 1] = kTaskMarker;
+      return 0;
+    }
     if (nPrims <= (uint32_t)kTriClipThresh) {
       int oPrims[kTriClipThresh], nOverl = 0;
       double b_ext[2][3];
@@ -518,7 +585,7 @@ class Builder {
       for (uint32_t i = 0; i < nPrims; ++i) {
         uint32_t old_idx = 0;
         if (clip[depth] >= 0) old_idx = primNums[i + nPrims];
-        if (clipToBound((int)primNums[i], b_ext, clip[depth], allBounds[totalPrims + nOverl],
+        if (clipToBound((int)primNums[i], b_ext, clip[depth], clipBounds[nOverl],
                         c_old + old_idx, c_new + nOverl)) {
           T.stats.clip++;
           oPrims[nOverl] = (int)primNums[i];
@@ -541,9 +608,9 @@ class Builder {
     eBonus = (float)((double)eBonus * (1.1 - (double)((float)depth / (float)maxDepth)));
     if (nPrims > 128) pigeonMinCost(nPrims, nodeBound, primNums, split);
     else if (nPrims > (uint32_t)kTriClipThresh)
-      minimalCost(nPrims, nodeBound, primNums, allBounds.data(), false, split);
+      minimalCost(nPrims, nodeBound, primNums, bounds, false, split);
     else
-      minimalCost(nPrims, nodeBound, primNums, allBounds.data() + totalPrims, true, split);
+      minimalCost(nPrims, nodeBound, primNums, clipBounds.data(), true, split);
     eBonus = baseBonus;
 
     if (split.bestCost > split.oldCost) ++badRefines;
@@ -571,11 +638,11 @@ class Builder {
     if (nPrims > 128) {
       for (uint32_t i = 0; i < nPrims; i++) {
         uint32_t pn = primNums[i];
-        if (allBounds[pn].a[ax] >= split.t) {
+        if (bounds[pn].a[ax] >= split.t) {
           nRightPrims[n1++] = pn;
         } else {
           lPrims[n0++] = pn;
-          if (allBounds[pn].g[ax] > split.t) nRightPrims[n1++] = pn;
+          if (bounds[pn].g[ax] > split.t) nRightPrims[n1++] = pn;
         }
       }
       splitPos = split.t;
@@ -641,13 +708,153 @@ class Builder {
 
 }  // namespace
 
+namespace {
+
+void add_stats(KdBuildStats& a, const KdBuildStats& b) {
+  a.inodes += b.inodes;
+  a.leaves += b.leaves;
+  a.empty_leaves += b.empty_leaves;
+  a.leaf_prims += b.leaf_prims;
+  a.depth_limit_reached += b.depth_limit_reached;
+  a.bad_splits += b.bad_splits;
+  a.clip += b.clip;
+  a.null_clip += b.null_clip;
+  a.early_out += b.early_out;
+}
+
+// Thread pool of subtree builds. The top-level builder runs on the calling
+// thread and hands out subtrees as it reaches them; workers build them
+// concurrently; the caller joins the workers once its own recursion is done.
+class ParallelSink : public TaskSink {
+ public:
+  ParallelSink(const Builder& top, int nthreads) : top_(top) {
+    for (int i = 0; i < nthreads; ++i) workers_.emplace_back([this] { work(); });
+  }
+  uint32_t add(SubtreeTask&& t) override {
+    std::lock_guard<std::mutex> g(m_);
+    const uint32_t id = (uint32_t)results_.size();
+    results_.emplace_back(new KdTree());
+    queue_.push_back({id, std::move(t)});
+    cv_.notify_one();
+    return id;
+  }
+  void finish() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      closed_ = true;
+    }
+    cv_.notify_all();
+    work();  // the caller helps with the remaining subtrees
+    for (auto& w : workers_) w.join();
+    if (error_) std::rethrow_exception(error_);
+  }
+  std::vector<std::unique_ptr<KdTree>> results_;
+
+ private:
+  void work() {
+    for (;;) {
+      std::pair<uint32_t, SubtreeTask> job;
+      KdTree* out = nullptr;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [this] { return closed_ || !queue_.empty(); });
+        if (queue_.empty()) return;
+        job = std::move(queue_.front());
+        queue_.pop_front();
+        out = results_[job.first].get();
+      }
+      try {
+        Builder b(top_, *out);
+        b.buildSubtree(job.second);
+      } catch (...) {
+        std::lock_guard<std::mutex> g(m_);
+        if (!error_) error_ = std::current_exception();
+      }
+    }
+  }
+  const Builder& top_;
+  std::vector<std::thread> workers_;
+  std::deque<std::pair<uint32_t, SubtreeTask>> queue_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  bool closed_ = false;
+  std::exception_ptr error_;
+};
+
+// Depth-first copy of the top-level tree into out, splicing in the subtrees
+// at their placeholders: the node order, right-child indices and leaf list
+// order come out exactly as the serial recursion writes them.
+void stitch(const KdTree& top, uint32_t n, const std::vector<std::unique_ptr<KdTree>>& sub, KdTree& out) {
+  const uint32_t w0 = top.nodes[2 * n], w1 = top.nodes[2 * n + 1];
+  if (w1 == kTaskMarker) {
+    const KdTree& t = *sub[w0];
+    const uint32_t base = (uint32_t)(out.nodes.size() / 2), lbase = (uint32_t)out.leaf_prims.size();
+    for (size_t i = 0; i < t.nodes.size(); i += 2) {
+      uint32_t a = t.nodes[i], b = t.nodes[i + 1];
+      if ((b & 3u) == 3u) {
+        if ((b >> 2) > 1) a += lbase;
+      } else {
+        b = (b & 3u) | (((b >> 2) + base) << 2);
+      }
+      out.nodes.push_back(a);
+      out.nodes.push_back(b);
+    }
+    out.leaf_prims.insert(out.leaf_prims.end(), t.leaf_prims.begin(), t.leaf_prims.end());
+    add_stats(out.stats, t.stats);
+    return;
+  }
+  if ((w1 & 3u) == 3u) {
+    const uint32_t np = w1 >> 2;
+    uint32_t a = w0;
+    if (np > 1) {
+      a = (uint32_t)out.leaf_prims.size();
+      out.leaf_prims.insert(out.leaf_prims.end(), top.leaf_prims.begin() + w0, top.leaf_prims.begin() + w0 + np);
+    }
+    out.nodes.push_back(a);
+    out.nodes.push_back(w1);
+    return;
+  }
+  const size_t me = out.nodes.size();
+  out.nodes.push_back(w0);
+  out.nodes.push_back(w1 & 3u);
+  stitch(top, n + 1, sub, out);
+  out.nodes[me + 1] |= (uint32_t)(out.nodes.size() / 2) << 2;
+  stitch(top, w1 >> 2, sub, out);
+}
+
+int build_threads() {
+  const char* e = std::getenv("YK_BUILD_THREADS");
+  int n = e ? std::atoi(e) : (int)std::thread::hardware_concurrency();
+  return std::max(1, std::min(n, 16));  // 16: the CPU share of a GPU box
+}
+
+}  // namespace
+
 void build_kdtree(const float* tri_verts, int ntris, KdTree& out, int depth, int leaf_size,
                   float cost_ratio, float empty_bonus) {
   out = KdTree();
   if (ntris <= 0) throw std::invalid_argument("build_kdtree: empty scene");
   (void)leaf_size;
-  Builder b(tri_verts, ntris, out, depth, leaf_size, cost_ratio, empty_bonus);
+  const int nthreads = build_threads();
+  if (nthreads <= 1 || ntris < 100000) {
+    Builder b(tri_verts, ntris, out, depth, leaf_size, cost_ratio, empty_bonus);
+    b.run();
+    return;
+  }
+  // parallel build: the same recursion, subtrees of at most ntris/(16*threads)
+  // prims handed to a thread pool, then stitched in depth-first order
+  KdTree top;
+  Builder b(tri_verts, ntris, top, depth, leaf_size, cost_ratio, empty_bonus);
+  ParallelSink sink(b, nthreads - 1);
+  sink.maxPrims = (uint32_t)std::max<long long>(4096, (long long)ntris / (16ll * nthreads));
+  b.sink = &sink;
   b.run();
+  sink.finish();
+  out.nodes.reserve(top.nodes.size());
+  std::memcpy(out.bound, top.bound, sizeof out.bound);
+  out.max_depth = top.max_depth;
+  out.stats = top.stats;
+  stitch(top, 0, sink.results_, out);
 }
 
 }  // namespace yk
