@@ -71,7 +71,7 @@ class yk_render_params(C.Structure):
                 ("height", C.c_int32), ("xstart", C.c_int32), ("ystart", C.c_int32),
                 ("aa_samples", C.c_int32), ("aa_passes", C.c_int32), ("filter", C.c_int32),
                 ("aa_pixelwidth", C.c_float), ("tile_size", C.c_int32),
-                ("transp_background", C.c_int32)]
+                ("transp_background", C.c_int32), ("aa_inc_samples", C.c_int32), ("aa_threshold", C.c_float)]
 
     def copy(self):
         p = yk_render_params()

@@ -879,6 +879,9 @@ struct Batch {
 };
 
 struct RenderConst {
+  int ps;         // pixel sample index from B.psample (specular nodes, adaptive passes)
+  int multipass;  // AA_passes > 1: RI_vdC / RI_S sample positions (integrator.cc:276-281)
+  int pass_off;   // pixelSample offset of the pass
   int spec;       // specular recursion pipeline (scene has SPECULAR|FILTER materials)
   int trace_caustics;  // caustic_type path: traceCaustics (pathtracer.cc:389-397)
   int rdepth;     // raydepth
@@ -902,27 +905,41 @@ struct TileList {
   const int4* tiles;  // X, Y, W, H per tile of the batch
   const int* base;    // first camera-sample index of each tile
   int ntiles;
+  const int* pix;     // adaptive pass: the batch's resampled pixels ((y << 16) | x), tile order
 };
 
 __global__ void __launch_bounds__(256) k_camera(TileList TL, Batch B, RenderConst R, long long nc) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= nc) return;
-  int lo = 0, hi = TL.ntiles - 1;
-  while (lo < hi) {  // tile owning c
-    const int mid = (lo + hi + 1) >> 1;
-    if (TL.base[mid] <= c) lo = mid;
-    else hi = mid - 1;
+  int s, j, i;
+  if (TL.pix) {  // adaptive pass: only the flagged pixels, in tile / row order
+    const int packed = TL.pix[c / R.spp];
+    s = (int)(c % R.spp);
+    j = packed & 0xFFFF;
+    i = packed >> 16;
+  } else {
+    int lo = 0, hi = TL.ntiles - 1;
+    while (lo < hi) {  // tile owning c
+      const int mid = (lo + hi + 1) >> 1;
+      if (TL.base[mid] <= c) lo = mid;
+      else hi = mid - 1;
+    }
+    const int4 T = TL.tiles[lo];
+    const long long local = c - TL.base[lo];
+    s = (int)(local % R.spp);
+    const int pl = (int)(local / R.spp);
+    j = T.x + pl % T.z;
+    i = T.y + pl / T.z;
   }
-  const int4 T = TL.tiles[lo];
-  const long long local = c - TL.base[lo];
-  const int s = (int)(local % R.spp);
-  const int pl = (int)(local / R.spp);
-  const int j = T.x + pl % T.z, i = T.y + pl / T.z;
   const unsigned so = fnv32a((unsigned)i * fnv32a((unsigned)j));
+  const unsigned psample = (unsigned)(R.pass_off + s);  // rstate.pixelSample = pass_offs + sample
   B.soffs[c] = so;
-  if (R.spec) B.psample[c] = (unsigned)s;
+  if (R.ps) B.psample[c] = psample;
   float dx = 0.5f, dy = 0.5f;
-  if (R.spp > 1) {
+  if (R.multipass) {
+    dx = ri_vdc(psample, so);
+    dy = ri_s(psample, so);
+  } else if (R.spp > 1) {
     dx = (0.5f + (float)s) * R.d1;
     dy = ri_lp((unsigned)s + so, 0u);
   }
@@ -1081,7 +1098,7 @@ __device__ __forceinline__ void flush_shadow(const Batch& B, long long c, int ke
 // primary BSDF (pathtracer.cc:169-187). Returns the segment's ray.
 __device__ __forceinline__ yk_ray path_first_segment(const Batch& B, const RenderConst& R, long long c,
                                                      const SurfPt& sp, const DMat& M, v3 dir, int isub) {
-  const unsigned s = R.spec ? B.psample[c] : (unsigned)(c % R.spp);
+  const unsigned s = R.ps ? B.psample[c] : (unsigned)(c % R.spp);
   const unsigned offs = (unsigned)(R.nsub * (int)s) + B.soffs[c] + (unsigned)isub;
   const float s1 = ri_vdc(offs, 0u);
   const float s2 = (float)scr_halton(2, offs);
@@ -1132,7 +1149,7 @@ __global__ void __launch_bounds__(256) k_shade_primary(DScene S, Batch B, Render
       }
       if (M.flags & BSDF_DIFFUSE) {
         ph |= PH_DIFFUSE;
-        const unsigned s = R.spec ? B.psample[c] : (unsigned)(c % R.spp);
+        const unsigned s = R.ps ? B.psample[c] : (unsigned)(c % R.spp);
         int k0 = 0;
         for (int l = 0; l < R.nlights; ++l) {
           nr += gen_light(B, c, k0, l, sp, wo, s, B.soffs[c], (unsigned)l, traced);
@@ -1280,7 +1297,7 @@ __global__ void __launch_bounds__(256) k_shade_bounce(DScene S, Batch B, RenderC
       const SurfPt sp = make_surface(S, from, dir, h);
       const DMat& M = c_mats[sp.mat];
       const v3 pwo = vneg(dir);
-      const unsigned s = R.spec ? B.psample[c] : (unsigned)(c % R.spp);
+      const unsigned s = R.ps ? B.psample[c] : (unsigned)(c % R.spp);
       const unsigned offs = (unsigned)(R.nsub * (int)s) + B.soffs[c] + (unsigned)isub;
       int ps = PS_RESOLVE;
       // estimateOneDirectLight(state, hit, pwo, offs): always at the first
@@ -1560,6 +1577,7 @@ struct FilmConst {
   int tb0, tb1;                  // batch = owned tile ranks [tb0, tb1)
   int spp;
   float d1;
+  const int* pmap;  // adaptive pass: batch-local first sample of each film pixel, -1 = not resampled
   float table[256];
 };
 
@@ -1602,7 +1620,13 @@ __global__ void __launch_bounds__(256) k_film_gather(FilmConst F, const float4* 
       const long long tb = tile_base[rank - F.tb0];
       for (int sy = ya; sy <= yb; ++sy)
         for (int sx = xa; sx <= xb; ++sx) {
-          const long long cbase = tb + (long long)((sy - Y) * W + (sx - X)) * F.spp;
+          long long cbase;
+          if (F.pmap) {
+            cbase = F.pmap[(size_t)(sy - F.cy0) * F.w + (sx - F.cx0)];
+            if (cbase < 0) continue;
+          } else {
+            cbase = tb + (long long)((sy - Y) * W + (sx - X)) * F.spp;
+          }
           const int ox = tx - sx, oy = ty - sy;
           for (int s = 0; s < F.spp; ++s) {
             const float2 dd = sxy[cbase + s];
@@ -1630,6 +1654,37 @@ __global__ void __launch_bounds__(256) k_film_gather(FilmConst F, const float4* 
   px[2] = aB;
   px[3] = aA;
   px[4] = aW;
+}
+
+// imageFilm_t::nextPass (imagefilm.cc:213-271): flag the pixels whose
+// brightness differs from a neighbour's by >= threshold. Compiled form: the
+// centre as abscol2bri of col*(1/w); each neighbour folded as
+// |(c - (0.0722*B)*inv) - (0.7152*G + 0.2126*R)*inv|, |c| when its weight is 0.
+__global__ void k_aa_flags(const float* __restrict__ film, int w, int h, float thr, uint8_t* __restrict__ flags) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= (w - 1) * (h - 1)) return;
+  const int x = tid % (w - 1), y = tid / (w - 1);
+  const float* a = film + 5 * ((size_t)y * w + x);
+  float c = 0.f;
+  if (a[4] > 0.f) {
+    const float inv = 1.0f / a[4];
+    c = (0.2126f * fabsf(a[0] * inv) + 0.7152f * fabsf(a[1] * inv)) + 0.0722f * fabsf(a[2] * inv);
+  }
+  auto differs = [&](int nx, int ny) {
+    const float* b = film + 5 * ((size_t)ny * w + nx);
+    float d = c;
+    if (b[4] > 0.f) {
+      const float inv = 1.0f / b[4];
+      d = (c - (0.0722f * b[2]) * inv) - (0.2126f * b[0] + 0.7152f * b[1]) * inv;
+    }
+    return fabsf(d) >= thr;
+  };
+  bool need = false;
+  if (differs(x + 1, y)) { need = true; flags[(size_t)y * w + x + 1] = 1; }
+  if (differs(x, y + 1)) { need = true; flags[(size_t)(y + 1) * w + x] = 1; }
+  if (differs(x + 1, y + 1)) { need = true; flags[(size_t)(y + 1) * w + x + 1] = 1; }
+  if (x > 0 && differs(x - 1, y + 1)) { need = true; flags[(size_t)(y + 1) * w + x - 1] = 1; }
+  if (need) flags[(size_t)y * w + x] = 1;
 }
 
 // imageFilm_t::flush: pixel_t::normalized (colorA_t / f multiplies by 1.0/f,
@@ -2216,6 +2271,47 @@ int yk_trace_shadow(yk_device* d, const yk_ray* d_rays, int64_t n, uint8_t* d_oc
   YK_GUARD_END
 }
 
+// Filter functions of imageFilm_t (imagefilm.cc:81-123), in the survey
+// build's compiled forms: Gauss folds -6*log2(e) into one constant and drops
+// fExp2's upper clamp (the argument is never positive); Lanczos2 uses the
+// FAST_TRIG fSin on (float)(x*pi) and (float)(x*pi/2).
+static float host_fsin(float x) {  // fSin, mathOptimizations.h:249-268 (compiled form, see yk_math.h)
+  if ((double)x > YK_2PI_D || (double)x < -YK_2PI_D)
+    x -= (float)((int)(x * (float)0.15915494309189533577)) * (float)YK_2PI_D;
+  if ((double)x < -YK_PI_D) x += (float)YK_2PI_D;
+  else if ((double)x > YK_PI_D) x -= (float)YK_2PI_D;
+  x = ((float)1.27323954473516268615 * x) - (((float)0.40528473456935108578 * x) * std::fabs(x));
+  float r = x + (std::fabs(x) - 1.0f) * (0.225f * x);
+  if (r > 1.0f) r = 1.0f;
+  if (r < -1.0f) r = -1.0f;
+  return r;
+}
+static float filter_gauss(float dx, float dy) {
+  const float r2 = dx * dx + dy * dy;
+  float k;
+  const uint32_t kbits = 0xc10a7facu;  // (float)(-6 * (float)M_LOG2E)
+  std::memcpy(&k, &kbits, 4);
+  float x = r2 * k;
+  x = (x > -126.99999f) ? x : -126.99999f;  // f_LOW
+  const int ip = (int)(x - 0.5f);
+  const float fp = x - (float)ip;
+  const uint32_t eb = (uint32_t)(ip + 127) << 23;
+  float e;
+  std::memcpy(&e, &eb, 4);
+  const float poly = ((((1.8775767e-3f * fp + 8.9893397e-3f) * fp + 5.5826318e-2f) * fp + 2.4015361e-1f) * fp +
+                      6.9315308e-1f) * fp + 9.9999994e-1f;
+  const float v = (float)((double)(e * poly) - 0.00247875);
+  return (v > 0.f) ? v : 0.f;
+}
+static float filter_lanczos(float dx, float dy) {
+  const float x = std::sqrt(dx * dx + dy * dy);
+  if (x == 0.f) return 1.f;
+  if (!(x > -2.f) || !(x < 2.f)) return 0.f;
+  const float a = (float)((double)x * YK_PI_D);
+  const float b = (float)((double)x * (YK_PI_D * 0.5));
+  return (host_fsin(b) * host_fsin(a)) / (a * b);
+}
+
 static FilmConst make_film(const yk_render_params* p) {
   FilmConst F{};
   F.cx0 = p->xstart;
@@ -2247,6 +2343,10 @@ static FilmConst make_film(const yk_render_params* p) {
         if (xx >= 2.f) v = 0.f;
         else if (xx >= 1.f) v = (float)(xx * (xx * (xx * -0.38888889f + 2.0f) - 3.33333333f) + 1.77777778f);
         else v = (float)(xx * xx * (1.16666666f * xx - 2.0f) + 0.88888889f);
+      } else if (p->filter == YK_FILTER_GAUSS) {
+        v = filter_gauss(fx, fy);
+      } else if (p->filter == YK_FILTER_LANCZOS) {
+        v = filter_lanczos(fx, fy);
       }
       F.table[y * 16 + x] = v;
     }
@@ -2255,14 +2355,23 @@ static FilmConst make_film(const yk_render_params* p) {
   return F;
 }
 
-int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int32_t nshards, float* d_film,
-                    yk_stats* st) {
+}  // extern "C"
+
+// One renderPass (integrator.cc:172-224): n samples per pixel from pixel
+// sample `off`; flags (film-local bytes, host) restricts it to the pixels
+// imageFilm_t::nextPass flagged.
+struct PassSpec {
+  int n, off;
+  bool multipass;
+  const uint8_t* flags;
+};
+
+static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, int32_t nshards, float* d_film,
+                       yk_stats* st, const PassSpec& ps) {
   if (!d || !p || !d_film || nshards < 1 || shard < 0 || shard >= nshards)
     return set_error(YK_ERR_ARG, "yk_render_shard: bad arguments");
   if (!d->uploaded) return set_error(YK_ERR_STATE, "yk_render_shard: no scene uploaded");
-  if (p->aa_passes != 1) return set_error(YK_ERR_UNSUPPORTED, "only AA_passes = 1 is supported");
-  if (p->filter != YK_FILTER_BOX && p->filter != YK_FILTER_MITCHELL)
-    return set_error(YK_ERR_UNSUPPORTED, "filter not supported (box, mitchell)");
+  if (p->filter < YK_FILTER_BOX || p->filter > YK_FILTER_LANCZOS) return set_error(YK_ERR_ARG, "unknown filter");
   if (p->integrator != YK_INTEGRATOR_PATH && p->integrator != YK_INTEGRATOR_DIRECT)
     return set_error(YK_ERR_ARG, "unknown integrator");
   if (p->integrator == YK_INTEGRATOR_PATH && p->caustic_type != YK_CAUSTIC_NONE &&
@@ -2278,6 +2387,8 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   if (F.tile > 4096) return set_error(YK_ERR_UNSUPPORTED, "tile_size > 4096");
   F.shard = shard;
   F.nshards = nshards;
+  F.spp = ps.n;
+  F.d1 = (float)(1.0 / (double)(float)ps.n);
   const int spp = F.spp;
   const int nty = (p->height + F.tile - 1) / F.tile;
   const int ntiles = F.ntx * nty;
@@ -2298,6 +2409,9 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   R.trace_caustics = (p->integrator == YK_INTEGRATOR_PATH && p->caustic_type == YK_CAUSTIC_PATH) ? 1 : 0;
   R.rdepth = p->raydepth;
   R.level = 0;
+  R.multipass = ps.multipass ? 1 : 0;
+  R.pass_off = ps.off;
+  R.ps = (R.spec || R.multipass) ? 1 : 0;
   const int K = std::max(1, d->sum_light_slots);
   // specular recursion: generation g holds recursion level g; every node has
   // at most two children, so a batch of nc camera samples needs at most
@@ -2332,17 +2446,38 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   std::vector<int> base_all((size_t)nbatch * (tiles_per_batch + 1), 0);
   std::vector<long long> nc_of(nbatch);
   std::vector<int4> rect_of(nbatch);
+  // adaptive pass: flagged pixels per batch (tile order, rows, columns) and
+  // the film-pixel -> batch-local first sample map the gather reads
+  std::vector<int> pix_all;
+  std::vector<size_t> pix_off(nbatch, 0);
+  std::vector<int> pmap;
+  if (ps.flags) {
+    if (F.cx1 > 65535 || F.cy1 > 65535) return set_error(YK_ERR_UNSUPPORTED, "adaptive passes need coordinates < 65536");
+    pmap.assign((size_t)F.w * F.h, -1);
+  }
   for (int bi = 0; bi < nbatch; ++bi) {
     const size_t tb0 = (size_t)bi * tiles_per_batch, tb1 = std::min(owned.size(), tb0 + (size_t)tiles_per_batch);
     long long nc = 0;
     int rx0 = 1 << 30, ry0 = 1 << 30, rx1 = -(1 << 30), ry1 = -(1 << 30);
+    pix_off[bi] = pix_all.size();
     for (size_t k = tb0; k < tb1; ++k) {
       const int t = owned[k];
       const int X = F.cx0 + (t % F.ntx) * F.tile, Y = F.cy0 + (t / F.ntx) * F.tile;
       const int W = std::min(F.tile, F.cx1 - X), H = std::min(F.tile, F.cy1 - Y);
       tiles_all.push_back(make_int4(X, Y, W, H));
       base_all[(size_t)bi * (tiles_per_batch + 1) + (k - tb0)] = (int)nc;
-      nc += (long long)W * H * spp;
+      if (ps.flags) {
+        for (int yy = Y; yy < Y + H; ++yy)
+          for (int xx = X; xx < X + W; ++xx) {
+            const size_t fp = (size_t)(yy - F.cy0) * F.w + (xx - F.cx0);
+            if (!ps.flags[fp]) continue;
+            pmap[fp] = (int)nc;
+            pix_all.push_back((yy << 16) | xx);
+            nc += spp;
+          }
+      } else {
+        nc += (long long)W * H * spp;
+      }
       rx0 = std::min(rx0, X);
       ry0 = std::min(ry0, Y);
       rx1 = std::max(rx1, X + W);
@@ -2358,6 +2493,14 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   base_dev.ensure(base_all.size());
   HIPCHK(hipMemcpy(tiles_dev.p, tiles_all.data(), tiles_all.size() * sizeof(int4), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(base_dev.p, base_all.data(), base_all.size() * sizeof(int), hipMemcpyHostToDevice));
+  DBuf<int> pix_dev, pmap_dev;
+  if (ps.flags) {
+    pix_dev.ensure(std::max<size_t>(1, pix_all.size()));
+    pmap_dev.ensure(pmap.size());
+    if (!pix_all.empty())
+      HIPCHK(hipMemcpy(pix_dev.p, pix_all.data(), pix_all.size() * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(pmap_dev.p, pmap.data(), pmap.size() * sizeof(int), hipMemcpyHostToDevice));
+  }
 
   // ---- per-pipe device words: [0,8) accumulators {closest nodes, tris,
   // errors, rays; any-hit ...}; then per batch: queue-count words
@@ -2372,7 +2515,7 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
     const int nb_here = (nbatch - pi + npipes - 1) / npipes;
     P.words.ensure((size_t)(8 + (d->spec ? 0 : words_per_batch * nb_here)));
     HIPCHK(hipMemsetAsync(P.words.p, 0, P.words.n * sizeof(unsigned long long), P.stream));
-    Bp[pi] = P.bind(maxc, K, tiles_per_batch, d->spec);
+    Bp[pi] = P.bind(maxc, K, tiles_per_batch, R.ps != 0);
   }
   NodeStore NS{};
   if (d->spec) {
@@ -2421,7 +2564,13 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
       else enqueue_trace<false>(d, P, rays, idx, n, hits, occ, work, P.words.p + 4, e0, e1);
     };
     TileList TL{tiles_dev.p + (size_t)bi * tiles_per_batch, base_dev.p + (size_t)bi * (tiles_per_batch + 1),
-                (int)std::min<size_t>(tiles_per_batch, owned.size() - (size_t)bi * tiles_per_batch)};
+                (int)std::min<size_t>(tiles_per_batch, owned.size() - (size_t)bi * tiles_per_batch),
+                ps.flags ? pix_dev.p + pix_off[bi] : nullptr};
+    if (nc == 0) {  // adaptive pass with nothing to resample in this batch: keep the gather order chain
+      if (bi > 0) HIPCHK(hipStreamWaitEvent(P.stream, d->gather_ev[(bi - 1) % kPipes], 0));
+      HIPCHK(hipEventRecord(d->gather_ev[bi % kPipes], P.stream));
+      continue;
+    }
     hipLaunchKernelGGL(k_camera, dim3(grid_for(nc)), dim3(256), 0, P.stream, TL, B, R, nc);
     HIPCHK(hipGetLastError());
     if (d->spec) {
@@ -2522,6 +2671,7 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
     // film: in batch order (tile order), whichever pipe ran the batch
     if (bi > 0) HIPCHK(hipStreamWaitEvent(P.stream, d->gather_ev[(bi - 1) % kPipes], 0));
     FilmConst Fb = F;
+    Fb.pmap = ps.flags ? pmap_dev.p : nullptr;
     Fb.tb0 = bi * tiles_per_batch;
     Fb.tb1 = (int)std::min<size_t>(owned.size(), (size_t)(bi + 1) * tiles_per_batch);
     const int4 rc = rect_of[bi];
@@ -2567,6 +2717,47 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   }
   S->camera_samples += (uint64_t)samples_total;
   S->ms_total += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return YK_OK;
+  YK_GUARD_END
+}
+
+extern "C" {
+
+int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int32_t nshards, float* d_film,
+                    yk_stats* st) {
+  if (!d || !p || !d_film || nshards < 1 || shard < 0 || shard >= nshards)
+    return set_error(YK_ERR_ARG, "yk_render_shard: bad arguments");
+  if (p->aa_passes < 1) return set_error(YK_ERR_ARG, "AA_passes must be >= 1");
+  const int n0 = std::max(1, p->aa_samples);  // scene_t::setAntialiasing, scene.cc:736-742
+  if (p->aa_passes == 1) return render_pass(d, p, shard, nshards, d_film, st, PassSpec{n0, 0, false, nullptr});
+  // tiledIntegrator_t::render, integrator.cc:132-170: pass 0 everywhere, then
+  // AA_inc_samples more in the pixels imageFilm_t::nextPass flags
+  if (nshards != 1)
+    return set_error(YK_ERR_UNSUPPORTED, "AA_passes > 1 needs the whole film (nshards = 1): nextPass reads it");
+  const int inc = p->aa_inc_samples > 0 ? p->aa_inc_samples : n0;
+  int rc = render_pass(d, p, 0, 1, d_film, st, PassSpec{n0, 0, true, nullptr});
+  if (rc != YK_OK) return rc;
+  YK_GUARD_BEGIN
+  const int w = p->width, h = p->height;
+  std::vector<uint8_t> flags((size_t)w * h);
+  DBuf<uint8_t> flags_dev;
+  flags_dev.ensure(flags.size());
+  for (int pass = 1; pass < p->aa_passes; ++pass) {
+    const uint8_t* fl = nullptr;  // AA_threshold <= 0: doMoreSamples is always true
+    if (p->aa_threshold > 0.f) {
+      HIPCHK(hipMemsetAsync(flags_dev.p, 0, flags.size(), d->stream));
+      if (w > 1 && h > 1) {
+        hipLaunchKernelGGL(k_aa_flags, dim3(grid_for((long long)(w - 1) * (h - 1))), dim3(256), 0, d->stream, d_film,
+                           w, h, p->aa_threshold, flags_dev.p);
+        HIPCHK(hipGetLastError());
+      }
+      HIPCHK(hipMemcpyAsync(flags.data(), flags_dev.p, flags.size(), hipMemcpyDeviceToHost, d->stream));
+      HIPCHK(hipStreamSynchronize(d->stream));
+      fl = flags.data();
+    }
+    rc = render_pass(d, p, 0, 1, d_film, st, PassSpec{inc, n0 + (pass - 1) * inc, true, fl});
+    if (rc != YK_OK) return rc;
+  }
   return YK_OK;
   YK_GUARD_END
 }

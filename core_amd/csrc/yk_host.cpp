@@ -341,6 +341,8 @@ void yk_render_params_default(yk_render_params* p) {
   p->aa_pixelwidth = 1.5f;
   p->tile_size = 32;
   p->transp_background = 1;
+  p->aa_inc_samples = 0;  // = aa_samples
+  p->aa_threshold = 0.05f;
 }
 
 int yk_scene_generate(yk_scene* s, const char* name, int32_t p0, int32_t p1, int32_t resx,

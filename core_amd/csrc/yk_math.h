@@ -138,6 +138,12 @@ __device__ __forceinline__ float ri_vdc(unsigned bits, unsigned r) {
   bits = __builtin_bitreverse32(bits);
   return clamp01((float)((double)(bits ^ r) * YK_MULT_RATIO));
 }
+// RI_S, mcqmc.h:110-115
+__device__ __forceinline__ float ri_s(unsigned i, unsigned r) {
+  for (unsigned v = 1u << 31; i; i >>= 1, v ^= v >> 1)
+    if (i & 1) r ^= v;
+  return clamp01((float)((double)r * YK_MULT_RATIO));
+}
 // RI_LP, mcqmc.h:117-122
 __device__ __forceinline__ float ri_lp(unsigned i, unsigned r) {
   for (unsigned v = 1u << 31; i; i >>= 1, v |= v >> 1)

@@ -95,11 +95,14 @@ typedef struct yk_render_params {
   int32_t width, height;  /* render area ("width"/"height")                          */
   int32_t xstart, ystart; /* crop offset ("xstart"/"ystart")                         */
   int32_t aa_samples;     /* "AA_minsamples"                                         */
-  int32_t aa_passes;      /* "AA_passes" (only 1 supported)                          */
+  int32_t aa_passes;      /* "AA_passes" (> 1: adaptive passes, single shard only)   */
   int32_t filter;         /* YK_FILTER_*                                             */
   float aa_pixelwidth;    /* "AA_pixelwidth"                                         */
   int32_t tile_size;      /* "tile_size"                                             */
   int32_t transp_background; /* "bg_transp" (default 1)                             */
+  int32_t aa_inc_samples; /* "AA_inc_samples": samples per pass after the first (<= 0:
+                             aa_samples, scene_t::setAntialiasing scene.cc:736-742)    */
+  float aa_threshold;     /* "AA_threshold" (default 0.05): adaptive resampling     */
 } yk_render_params;
 
 /* one ray, 32 bytes: ray_t (ray.h:26-49) without time */

@@ -1195,6 +1195,29 @@ static rgba integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir, fl
 #define FILTER_TABLE_SIZE 16
 #define MAX_FILTER_SIZE 8
 static float f_box(float dx, float dy) { (void)dx; (void)dy; return 1.f; }
+/* Gauss, imagefilm.cc:97-101: compiled form folds -6*log2(e) into one
+ * constant (bits 0xc10a7fac) and drops fExp2's upper clamp */
+static float f_gauss(float dx, float dy) {
+  float r2 = dx * dx + dy * dy;
+  union { uint32_t u; float f; } k = {0xc10a7facu}, e;
+  float x = r2 * k.f;
+  x = (x > -126.99999f) ? x : -126.99999f;
+  int ip = (int)(x - 0.5f);
+  float fp = x - (float)ip;
+  e.u = (uint32_t)(ip + 127) << 23;
+  float poly = ((((1.8775767e-3f * fp + 8.9893397e-3f) * fp + 5.5826318e-2f) * fp + 2.4015361e-1f) * fp +
+                6.9315308e-1f) * fp + 9.9999994e-1f;
+  float v = (float)((double)(e.f * poly) - 0.00247875);
+  return (v > 0.f) ? v : 0.f;
+}
+/* Lanczos2, imagefilm.cc:104-119 */
+static float f_lanczos(float dx, float dy) {
+  float x = sqrtf(dx * dx + dy * dy);
+  if (x == 0.f) return 1.f;
+  if (!(x > -2.f) || !(x < 2.f)) return 0.f;
+  float a = (float)((double)x * M_PI_D), b = (float)((double)x * (M_PI_D * 0.5));
+  return (fSin(b) * fSin(a)) / (a * b);
+}
 static float f_mitchell(float dx, float dy) {
   float x = 2.f * sqrtf(dx * dx + dy * dy);
   if (x >= 2.f) return 0.f;
@@ -1219,6 +1242,8 @@ static void film_init(film_t* F, const yk_render_params* P) {
   F->filterw = (float)((double)P->aa_pixelwidth * 0.5);
   float (*ff)(float, float) = f_box;
   if (P->filter == YK_FILTER_MITCHELL) { ff = f_mitchell; F->filterw *= 2.6f; }
+  else if (P->filter == YK_FILTER_LANCZOS) ff = f_lanczos;
+  else if (P->filter == YK_FILTER_GAUSS) { ff = f_gauss; F->filterw *= 2.f; }
   float fw = F->filterw < 0.501f ? 0.501f : F->filterw;
   if (fw > 0.5f * MAX_FILTER_SIZE) fw = 0.5f * MAX_FILTER_SIZE;
   F->filterw = fw;
@@ -1252,6 +1277,44 @@ static void film_add(film_t* F, rgba c, int x, int y, float dx, float dy) {
       px[2] += wt * c.b;
       px[3] += wt * c.a;
       px[4] += wt;
+    }
+}
+
+/* imageFilm_t::nextPass flags, imagefilm.cc:226-271, compiled form: the
+ * centre as abscol2bri of col*(1/w) (float reciprocal); each neighbour as
+ * |(c - (0.0722*B)*inv) - (0.2126*R + 0.7152*G)*inv|, |c| at weight 0. */
+static float aa_center(const float* a) {
+  if (!(a[4] > 0.f)) return 0.f;
+  float inv = 1.0f / a[4];
+  return (0.2126f * fabsf(a[0] * inv) + 0.7152f * fabsf(a[1] * inv)) + 0.0722f * fabsf(a[2] * inv);
+}
+static int aa_differs(float c, const float* b, float thr) {
+  float d = c;
+  if (b[4] > 0.f) {
+    float inv = 1.0f / b[4];
+    d = (c - (0.0722f * b[2]) * inv) - (0.2126f * b[0] + 0.7152f * b[1]) * inv;
+  }
+  return fabsf(d) >= thr;
+}
+static void aa_flags(const film_t* F, float thr, unsigned char* flags) {
+  int w = F->w, h = F->h;
+  memset(flags, 0, (size_t)w * h);
+  for (int y = 0; y < h - 1; ++y)
+    for (int x = 0; x < w - 1; ++x) {
+      const float* px = F->acc + 5 * ((size_t)y * w + x);
+      float c = aa_center(px);
+      int need = 0;
+      if (aa_differs(c, px + 5, thr)) { need = 1; flags[(size_t)y * w + x + 1] = 1; }
+      if (aa_differs(c, F->acc + 5 * ((size_t)(y + 1) * w + x), thr)) { need = 1; flags[(size_t)(y + 1) * w + x] = 1; }
+      if (aa_differs(c, F->acc + 5 * ((size_t)(y + 1) * w + x + 1), thr)) {
+        need = 1;
+        flags[(size_t)(y + 1) * w + x + 1] = 1;
+      }
+      if (x > 0 && aa_differs(c, F->acc + 5 * ((size_t)(y + 1) * w + x - 1), thr)) {
+        need = 1;
+        flags[(size_t)(y + 1) * w + x - 1] = 1;
+      }
+      if (need) flags[(size_t)y * w + x] = 1;
     }
 }
 
@@ -1386,39 +1449,62 @@ int orc_render_shard(const yk_render_params* P, int32_t shard, int32_t nshards, 
 
 static int render_tiles(const yk_render_params* P, int shard, int nshards, float* rgba_out, float* film_sums,
                         uint64_t* counts) {
-  if (P->aa_passes != 1) return 4;
+  if (P->aa_passes < 1) return 4;
+  if (P->aa_passes > 1 && nshards != 1) return 4; /* nextPass reads the whole film */
   film_t F;
   film_init(&F, P);
   g_nclosest = g_nshadow = g_nodes_c = g_tris_c = g_nodes_s = g_tris_s = 0;
   int ts = P->tile_size > 0 ? P->tile_size : 32;
-  int n = P->aa_samples > 0 ? P->aa_samples : 1;
-  float d1 = (float)(1.0 / (double)(float)n);
   int nx = (F.w + ts - 1) / ts, ny = (F.h + ts - 1) / ts;
-  for (int ty = 0; ty < ny; ++ty)
-    for (int tx = 0; tx < nx; ++tx) {
-      if ((ty * nx + tx) % nshards != shard) continue;
-      int X = F.cx0 + tx * ts, Y = F.cy0 + ty * ts;
-      int W = (F.cx0 + F.w - X) < ts ? (F.cx0 + F.w - X) : ts;
-      int H = (F.cy0 + F.h - Y) < ts ? (F.cy0 + F.h - Y) : ts;
-      for (int i = Y; i < Y + H; ++i)
-        for (int j = X; j < X + W; ++j) {
-          rstate st;
-          st.samplingOffs = fnv_32a_buf((unsigned)i * fnv_32a_buf((unsigned)j));
-          st.includeLights = 0;
-          st.raylevel = 0;
-          for (int s = 0; s < n; ++s) {
-            st.pixelSample = s;
-            float dx = 0.5f, dy = 0.5f;
-            if (n > 1) { dx = (0.5f + (float)s) * d1; dy = RI_LP((unsigned)s + st.samplingOffs, 0); }
-            v3 from, dir;
-            float tmin, tmax;
-            camera_ray((float)j + dx, (float)i + dy, &from, &dir, &tmin, &tmax);
-            rgba c = integrate(&st, P, from, dir, tmin, tmax);
-            c.r = 1.f * c.r; c.g = 1.f * c.g; c.b = 1.f * c.b; c.a = 1.f * c.a; /* wt * col */
-            film_add(&F, c, j, i, dx, dy);
-          }
-        }
+  /* tiledIntegrator_t::render, integrator.cc:132-170 (scene_t::setAntialiasing
+   * clamps the sample counts, scene.cc:736-742) */
+  int n0 = P->aa_samples > 1 ? P->aa_samples : 1;
+  int inc = P->aa_inc_samples > 0 ? P->aa_inc_samples : n0;
+  unsigned char* flags = NULL;
+  for (int pass = 0; pass < P->aa_passes; ++pass) {
+    int n = pass == 0 ? n0 : inc;
+    int pass_offs = pass == 0 ? 0 : n0 + (pass - 1) * inc;
+    float d1 = (float)(1.0 / (double)(float)n);
+    int adaptive = 0;
+    if (pass > 0 && P->aa_threshold > 0.f) { /* imageFilm_t::nextPass, imagefilm.cc:213-271 */
+      if (!flags) flags = (unsigned char*)malloc((size_t)F.w * F.h);
+      aa_flags(&F, P->aa_threshold, flags);
+      adaptive = 1;
     }
+    for (int ty = 0; ty < ny; ++ty)
+      for (int tx = 0; tx < nx; ++tx) {
+        if ((ty * nx + tx) % nshards != shard) continue;
+        int X = F.cx0 + tx * ts, Y = F.cy0 + ty * ts;
+        int W = (F.cx0 + F.w - X) < ts ? (F.cx0 + F.w - X) : ts;
+        int H = (F.cy0 + F.h - Y) < ts ? (F.cy0 + F.h - Y) : ts;
+        for (int i = Y; i < Y + H; ++i)
+          for (int j = X; j < X + W; ++j) {
+            if (adaptive && !flags[(size_t)(i - F.cy0) * F.w + (j - F.cx0)]) continue; /* doMoreSamples */
+            rstate st;
+            st.samplingOffs = fnv_32a_buf((unsigned)i * fnv_32a_buf((unsigned)j));
+            st.includeLights = 0;
+            st.raylevel = 0;
+            for (int s = 0; s < n; ++s) {
+              st.pixelSample = pass_offs + s;
+              float dx = 0.5f, dy = 0.5f;
+              if (P->aa_passes > 1) { /* scrambled vdC / Sobol for multipass AA */
+                dx = RI_vdC((unsigned)st.pixelSample, st.samplingOffs);
+                dy = RI_S((unsigned)st.pixelSample, st.samplingOffs);
+              } else if (n > 1) {
+                dx = (0.5f + (float)s) * d1;
+                dy = RI_LP((unsigned)s + st.samplingOffs, 0);
+              }
+              v3 from, dir;
+              float tmin, tmax;
+              camera_ray((float)j + dx, (float)i + dy, &from, &dir, &tmin, &tmax);
+              rgba c = integrate(&st, P, from, dir, tmin, tmax);
+              c.r = 1.f * c.r; c.g = 1.f * c.g; c.b = 1.f * c.b; c.a = 1.f * c.a; /* wt * col */
+              film_add(&F, c, j, i, dx, dy);
+            }
+          }
+      }
+  }
+  free(flags);
   size_t npx = (size_t)F.w * F.h;
   for (size_t p = 0; p < npx; ++p) {
     float* a = F.acc + 5 * p;

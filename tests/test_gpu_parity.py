@@ -110,6 +110,20 @@ RENDER_CASES = [
     ("dl_cornell", ("cornell_dl", 128, 128, 0, 0), (16, 20, 80, 72), {}),
     ("pt_cornell", ("cornell_pt", 64, 64, 0, 0), (0, 0, 64, 64), {}),
     ("pt_cornell_mitchell", ("cornell_pt", 64, 64, 0, 0), (5, 3, 50, 45), {"filter": A.YK_FILTER_MITCHELL}),
+    # Gauss / Lanczos2 filter tables (imagefilm.cc:97-119, compiled forms; parity unpinned vs reference outputs)
+    ("pt_cornell_gauss", ("cornell_pt", 64, 64, 0, 0), (3, 2, 56, 50),
+     {"filter": A.YK_FILTER_GAUSS, "aa_pixelwidth": 1.5}),
+    ("pt_cornell_lanczos", ("cornell_pt", 64, 64, 0, 0), (0, 0, 64, 64),
+     {"filter": A.YK_FILTER_LANCZOS, "aa_pixelwidth": 2.0}),
+    ("dl_cornell_gauss_wide", ("cornell_dl", 96, 96, 0, 0), (10, 12, 70, 60),
+     {"filter": A.YK_FILTER_GAUSS, "aa_pixelwidth": 3.0}),
+    # adaptive AA passes (integrator.cc:132-170, imageFilm_t::nextPass imagefilm.cc:213-271)
+    ("pt_cornell_aa3", ("cornell_pt", 64, 64, 0, 0), (0, 0, 64, 64),
+     {"aa_samples": 4, "aa_passes": 3, "aa_inc_samples": 2, "aa_threshold": 0.05}),
+    ("dl_cornell_aa2_thr0", ("cornell_dl", 64, 64, 0, 0), (4, 4, 50, 50),
+     {"aa_samples": 2, "aa_passes": 2, "aa_inc_samples": 3, "aa_threshold": 0.0}),
+    ("pt_spec_aa2_mitchell", ("spec", 48, 48, 3, 0), (0, 0, 48, 48),
+     {"aa_samples": 2, "aa_passes": 2, "aa_inc_samples": 2, "aa_threshold": 0.02, "filter": A.YK_FILTER_MITCHELL}),
     ("pt_cornell_2sub", ("cornell_pt", 48, 48, 0, 0), (0, 0, 48, 48), {"path_samples": 2, "aa_samples": 3}),
     ("pt_bumpy", ("bumpy", 96, 54, 120, 61), (0, 0, 96, 54), {}),
     ("pt_bumpy_tile16", ("bumpy", 96, 54, 120, 61), (10, 5, 70, 40), {"tile_size": 16, "bounces": 5}),
