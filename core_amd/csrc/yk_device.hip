@@ -166,6 +166,13 @@ struct Trav {
   int prim;
 };
 
+struct __attribute__((aligned(8))) NodePair {
+  uint32_t a, b, c, d;
+};
+__device__ __forceinline__ NodePair ld_pair(const uint2* nodes, int i) {
+  return *reinterpret_cast<const NodePair*>(nodes + i);
+}
+
 // v[axis] for axis in 0..2 via selects (no dynamic register indexing)
 __device__ __forceinline__ float sel3(v3 v, uint32_t ax) { return ax == 0u ? v.x : (ax == 1u ? v.y : v.z); }
 
@@ -244,7 +251,12 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
                                           unsigned& ntris, bool& occluded) {
   if (st.dist < st.en_t) return true;
   int node = st.node;
-  uint2 nd = S.nodes[node];
+  // node pairs: every load brings nodes[node] and nodes[node + 1] (the left
+  // child), so a descent to the left child right after a load needs no
+  // memory round trip (the node array carries one padding node)
+  NodePair q = ld_pair(S.nodes, node);
+  uint2 nd = make_uint2(q.a, q.b), nx = make_uint2(q.c, q.d);
+  bool have = true;
   nnodes++;
   for (;;) {
     const uint32_t ax = nd.y & 3u;
@@ -264,8 +276,17 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
       st.ex_w = (uint32_t)(far_ + 1) | (ax << 30);
       exit_pb(st);
     }
-    node = left_first ? node + 1 : right;
-    nd = S.nodes[node];
+    if (left_first && have) {
+      node = node + 1;
+      nd = nx;
+      have = false;
+    } else {
+      node = left_first ? node + 1 : right;
+      q = ld_pair(S.nodes, node);
+      nd = make_uint2(q.a, q.b);
+      nx = make_uint2(q.c, q.d);
+      have = true;
+    }
     nnodes++;
   }
   const uint32_t n = nd.y >> 2, w0 = nd.x;
@@ -2186,7 +2207,8 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   d->tris.ensure(tris.size());
   d->ng.ensure(ng.size());
   const size_t nn = S.tree.nodes.size() / 2;
-  d->nodes.ensure(nn);
+  d->nodes.ensure(nn + 1);  // + one padding node for the node-pair loads
+  HIPCHK(hipMemset(d->nodes.p + nn, 0, sizeof(uint2)));
   d->leaf.ensure(std::max<size_t>(S.tree.leaf_prims.size(), 1));
   HIPCHK(hipMemcpy(d->tris.p, tris.data(), tris.size() * sizeof(float4), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d->ng.p, ng.data(), ng.size() * sizeof(float4), hipMemcpyHostToDevice));
