@@ -16,7 +16,8 @@ YK_ERR_ARG, YK_ERR_STATE, YK_ERR_HIP, YK_ERR_UNSUPPORTED, YK_ERR_ALLOC, YK_ERR_I
 YK_MAT_SHINYDIFFUSE, YK_MAT_LIGHT = 0, 1
 YK_LIGHT_AREA, YK_LIGHT_POINT, YK_LIGHT_DIRECTIONAL = 0, 1, 2
 YK_MESH_SMOOTH, YK_MESH_NORMALS_EXPORTED = 1, 2
-YK_INTEGRATOR_DIRECT, YK_INTEGRATOR_PATH = 0, 1
+YK_INTEGRATOR_DIRECT, YK_INTEGRATOR_PATH, YK_INTEGRATOR_PHOTON = 0, 1, 2
+YK_PHOTON_MAP_DIFFUSE, YK_PHOTON_MAP_CAUSTIC, YK_PHOTON_MAP_RADIANCE = 0, 1, 2
 YK_FILTER_BOX, YK_FILTER_MITCHELL, YK_FILTER_GAUSS, YK_FILTER_LANCZOS = 0, 1, 2, 3
 YK_CAUSTIC_NONE, YK_CAUSTIC_PATH = 0, 1
 
@@ -65,13 +66,30 @@ class yk_camera_state(C.Structure):
                 ("near_p", f3), ("far_p", f3), ("resx", C.c_int32), ("resy", C.c_int32)]
 
 
+class yk_photon_params(C.Structure):
+    _fields_ = [("photons", C.c_int32), ("caustic_photons", C.c_int32), ("diffuse_radius", C.c_float),
+                ("caustic_radius", C.c_float), ("search", C.c_int32), ("caustic_mix", C.c_int32),
+                ("bounces", C.c_int32), ("final_gather", C.c_int32), ("fg_samples", C.c_int32),
+                ("fg_bounces", C.c_int32), ("fg_min_pathlen", C.c_float), ("show_map", C.c_int32),
+                ("seed", C.c_int32)]
+
+
+class yk_photon_info(C.Structure):
+    _fields_ = [("diffuse_photons", C.c_int32), ("diffuse_paths", C.c_int32), ("caustic_photons", C.c_int32),
+                ("caustic_paths", C.c_int32), ("rad_candidates", C.c_int32), ("radiance_photons", C.c_int32),
+                ("seed_out", C.c_int32), ("tree_depth", C.c_int32), ("photon_rays", C.c_uint64),
+                ("ms_shoot", C.c_double), ("ms_tree", C.c_double), ("ms_pregather", C.c_double),
+                ("ms_total", C.c_double)]
+
+
 class yk_render_params(C.Structure):
     _fields_ = [("integrator", C.c_int32), ("raydepth", C.c_int32), ("path_samples", C.c_int32),
                 ("bounces", C.c_int32), ("caustic_type", C.c_int32), ("width", C.c_int32),
                 ("height", C.c_int32), ("xstart", C.c_int32), ("ystart", C.c_int32),
                 ("aa_samples", C.c_int32), ("aa_passes", C.c_int32), ("filter", C.c_int32),
                 ("aa_pixelwidth", C.c_float), ("tile_size", C.c_int32),
-                ("transp_background", C.c_int32), ("aa_inc_samples", C.c_int32), ("aa_threshold", C.c_float)]
+                ("transp_background", C.c_int32), ("aa_inc_samples", C.c_int32), ("aa_threshold", C.c_float),
+                ("photon", yk_photon_params)]
 
     def copy(self):
         p = yk_render_params()
@@ -153,6 +171,8 @@ SIGNATURES = {
     "yk_film_resolve": (C.c_int, [P, C.POINTER(yk_render_params), P, P]),
     "yk_render_film": (C.c_int, [P, C.POINTER(yk_render_params), i32, i32, fp, C.POINTER(yk_stats)]),
     "yk_render": (C.c_int, [P, C.POINTER(yk_render_params), fp, C.POINTER(yk_stats)]),
+    "yk_photon_build": (C.c_int, [P, C.POINTER(yk_render_params), C.POINTER(yk_photon_info)]),
+    "yk_photon_export": (C.c_int, [P, i32, fp, i32, i32p]),
 }
 
 _lib = None

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../../include/yk_api.h"
+#include "photon_map.h"
 #include "scene.h"
 #include "yk_internal.h"
 #include "yk_math.h"
@@ -66,6 +67,7 @@ struct DLight {  // areaLight_t members after its constructor (arealight.cc:30-4
   int nslots;  // shadow slots per doLightEstimation: 2*samples (area + MIS half), 1 (Dirac)
   float pos[3], dir[3], radius;  // pointLight_t / directionalLight_t members
   int infinite;
+  float normal[3], du[3], dv[3];  // areaLight_t emitPhoton frame: normal = -fnormal, du = |toX|, dv = normal ^ du
 };
 
 struct DCam {  // perspectiveCam_t after camera_t ctor + setAxis
@@ -916,6 +918,8 @@ struct RenderConst {
   int has_bg;     // constant background color for camera-ray misses
   float bg[3];
   float d1;       // 1/spp as renderTile computes it
+  int pm_fg;      // photon mapping with final gathering: col += pathCol / nSampl at the finish
+  int pm_showmap; // photon mapping show_map: no direct light
 };
 
 // ------------------------------------------------------------ kernels
@@ -1166,10 +1170,13 @@ __global__ void __launch_bounds__(256) k_shade_primary(DScene S, Batch B, Render
         const c3 e = mat_emit(M, sp, wo, true);
         if (R.spec) em = e;
         else col = cadd(col, e);
+        // photonIntegrator_t::integrate adds emit() a second time after
+        // includeLights = false (photonintegr.cc:812-831)
+        if (R.integrator == YK_INTEGRATOR_PHOTON && !R.pm_showmap) col = cadd(col, mat_emit(M, sp, wo, false));
         if (M.type == YK_MAT_LIGHT) ph |= PH_LIGHT;
       }
-      if (M.flags & BSDF_DIFFUSE) {
-        ph |= PH_DIFFUSE;
+      if (M.flags & BSDF_DIFFUSE) ph |= PH_DIFFUSE;
+      if ((M.flags & BSDF_DIFFUSE) && !R.pm_showmap) {
         const unsigned s = R.ps ? B.psample[c] : (unsigned)(c % R.spp);
         int k0 = 0;
         for (int l = 0; l < R.nlights; ++l) {
@@ -1414,7 +1421,7 @@ __global__ void __launch_bounds__(256) k_finish(Batch B, RenderConst R, long lon
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= nc) return;
   c3 col = C3(B.col[3 * c], B.col[3 * c + 1], B.col[3 * c + 2]);
-  if (R.integrator == YK_INTEGRATOR_PATH && (B.prim_hit[c] & PH_DIFFUSE)) {
+  if ((R.integrator == YK_INTEGRATOR_PATH || R.pm_fg) && (B.prim_hit[c] & PH_DIFFUSE)) {
     const float ns = (float)R.nsub;
     col = cadd(col, C3(B.pathcol[3 * c] / ns, B.pathcol[3 * c + 1] / ns, B.pathcol[3 * c + 2] / ns));
   }
@@ -1728,6 +1735,8 @@ __global__ void k_film_resolve(const float* __restrict__ film, float* __restrict
   rgba[4 * p + 3] = al;
 }
 
+#include "yk_photon.inc"
+
 }  // namespace yk
 
 // ============================================================ host side
@@ -1793,6 +1802,7 @@ struct Pipe {
   DBuf<unsigned> psample;
   DBuf<uint8_t> incl, caus;
   DBuf<float> emit0;
+  DBuf<float> fgl, fglen;  // final gathering: lcol (3 per sample) and path length
   void create() {
     HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&ev0));
@@ -1913,6 +1923,14 @@ struct yk_device {
   DBuf<unsigned long long> ncount, spec_words;
   bool has_bg = false;
   float bg[3] = {0.f, 0.f, 0.f};
+  std::vector<DLight> lights_host;
+  // photon maps of yk_photon_build (photonIntegrator_t::preprocess)
+  bool pm_ready = false;
+  yk_photon_params pm_params{};
+  DBuf<uint2> dm_nodes, rm_nodes;
+  DBuf<float4> dm_pos, dm_dir, dm_col, rm_pos, rm_dir, rm_col;
+  std::vector<float> dm_host, rm_host;  // 9 floats per photon, photon-vector order
+  int dm_paths = 0;
   Pipe pipe[kPipes];
   hipEvent_t gather_ev[kPipes] = {};
   ~yk_device() {
@@ -1976,6 +1994,23 @@ DLight make_light(const yk_area_light_state& L) {
   D.samples = L.samples;
   D.type = YK_LIGHT_AREA;
   D.nslots = 2 * L.samples;
+  // emitPhoton frame (arealight.cc:40-43): normal = -fnormal; du = toX.normalize(); dv = normal ^ du
+  float du[3] = {x[0], x[1], x[2]};
+  float len = du[0] * du[0] + du[1] * du[1] + du[2] * du[2];
+  if (len != 0.f) {
+    len = 1.0f / std::sqrt(len);
+    du[0] *= len;
+    du[1] *= len;
+    du[2] *= len;
+  }
+  const float n[3] = {-f[0], -f[1], -f[2]};
+  for (int k = 0; k < 3; ++k) {
+    D.normal[k] = n[k];
+    D.du[k] = du[k];
+  }
+  D.dv[0] = n[1] * du[2] - n[2] * du[1];
+  D.dv[1] = n[2] * du[0] - n[0] * du[2];
+  D.dv[2] = n[0] * du[1] - n[1] * du[0];
   return D;
 }
 
@@ -2240,6 +2275,8 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   }
   if (sum_slots > 8192) return set_error(YK_ERR_UNSUPPORTED, "too many light samples per shading point");
   d->sum_light_slots = sum_slots;
+  d->lights_host = lights;
+  d->pm_ready = false;
   d->has_bg = S.has_background;
   for (int k = 0; k < 3; ++k) d->bg[k] = S.background[k];
   if (!lights.empty())
@@ -2379,6 +2416,8 @@ static FilmConst make_film(const yk_render_params* p) {
 
 }  // extern "C"
 
+#include "yk_photon_host.inc"
+
 // One renderPass (integrator.cc:172-224): n samples per pixel from pixel
 // sample `off`; flags (film-local bytes, host) restricts it to the pixels
 // imageFilm_t::nextPass flagged.
@@ -2394,8 +2433,13 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     return set_error(YK_ERR_ARG, "yk_render_shard: bad arguments");
   if (!d->uploaded) return set_error(YK_ERR_STATE, "yk_render_shard: no scene uploaded");
   if (p->filter < YK_FILTER_BOX || p->filter > YK_FILTER_LANCZOS) return set_error(YK_ERR_ARG, "unknown filter");
-  if (p->integrator != YK_INTEGRATOR_PATH && p->integrator != YK_INTEGRATOR_DIRECT)
+  if (p->integrator != YK_INTEGRATOR_PATH && p->integrator != YK_INTEGRATOR_DIRECT &&
+      p->integrator != YK_INTEGRATOR_PHOTON)
     return set_error(YK_ERR_ARG, "unknown integrator");
+  const bool pm = p->integrator == YK_INTEGRATOR_PHOTON;
+  if (pm && !d->pm_ready) return set_error(YK_ERR_STATE, "photon mapping: call yk_photon_build first (preprocess)");
+  if (pm && std::memcmp(&p->photon, &d->pm_params, sizeof(yk_photon_params)) != 0)
+    return set_error(YK_ERR_STATE, "photon mapping: the maps were built with different photon parameters");
   if (p->integrator == YK_INTEGRATOR_PATH && p->caustic_type != YK_CAUSTIC_NONE &&
       p->caustic_type != YK_CAUSTIC_PATH)
     return set_error(YK_ERR_UNSUPPORTED, "pathtracing needs caustic_type none or path");
@@ -2420,6 +2464,10 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   RenderConst R{};
   R.spp = spp;
   R.nsub = p->integrator == YK_INTEGRATOR_PATH ? std::max(1, p->path_samples) : 1;
+  R.pm_fg = (pm && p->photon.final_gather && !p->photon.show_map) ? 1 : 0;
+  R.pm_showmap = (pm && p->photon.show_map) ? 1 : 0;
+  if (R.pm_fg) R.nsub = std::max(1, p->photon.fg_samples);  // nSampl = max(1, nPaths / rayDivision)
+  const PMConst PMC = pm ? pm_const(d, p->photon) : PMConst{};
   R.bounces = p->bounces;
   R.integrator = p->integrator;
   R.transp_bg = p->transp_background;
@@ -2460,8 +2508,9 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   const int nbatch = (int)((owned.size() + tiles_per_batch - 1) / tiles_per_batch);
   const int npipes = d->spec ? 1 : std::min(kPipes, std::max(1, nbatch));
   const bool path = p->integrator == YK_INTEGRATOR_PATH;
-  const int bounces = path ? R.bounces : 0;
-  const int nsub = path ? R.nsub : 1;
+  // final gathering: hits 0..fg_bounces of each gather path, queue words up to fg_bounces + 1
+  const int bounces = path ? R.bounces : (R.pm_fg ? p->photon.fg_bounces + 1 : 0);
+  const int nsub = (path || R.pm_fg) ? R.nsub : 1;
 
   // ---- tile lists of all batches, uploaded once
   std::vector<int4> tiles_all;
@@ -2538,6 +2587,10 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     P.words.ensure((size_t)(8 + (d->spec ? 0 : words_per_batch * nb_here)));
     HIPCHK(hipMemsetAsync(P.words.p, 0, P.words.n * sizeof(unsigned long long), P.stream));
     Bp[pi] = P.bind(maxc, K, tiles_per_batch, R.ps != 0);
+    if (R.pm_fg) {
+      P.fgl.ensure(3 * maxc);
+      P.fglen.ensure(maxc);
+    }
   }
   NodeStore NS{};
   if (d->spec) {
@@ -2665,6 +2718,30 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     trace(false, B.s_rays, B.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, B.s_occl);
     hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
     HIPCHK(hipGetLastError());
+    if (pm && (PMC.show_map || !PMC.final_gather)) {
+      hipLaunchKernelGGL(k_pm_post, dim3(grid_for(nc, 64)), dim3(64), 0, P.stream, d->S, B, PMC, nc);
+      HIPCHK(hipGetLastError());
+    }
+    // final gathering (photonintegr.cc:637-790): gather path index outermost,
+    // pathCol accumulated across paths in the reference's order
+    for (int isub = 0; isub < (R.pm_fg ? nsub : 0); ++isub) {
+      hipLaunchKernelGGL(k_fg_start, dim3(grid_for(nc)), dim3(256), 0, P.stream, d->S, B, R, nc, isub, P.fgl.p,
+                         qw(isub, 0));
+      HIPCHK(hipGetLastError());
+      int qin = 1;
+      for (int it = 0; it <= p->photon.fg_bounces; ++it) {
+        const unsigned long long* in_w = qw(isub, it);
+        unsigned long long* out_w = qw(isub, it + 1);
+        trace(true, B.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, B.q_hits[qin], nullptr);
+        hipLaunchKernelGGL(k_fg_hit, dim3(grid_for(nc)), dim3(256), 0, P.stream, d->S, B, R, PMC, in_w, it, isub, qin,
+                           P.fgl.p, P.fglen.p, out_w);
+        HIPCHK(hipGetLastError());
+        if (it < p->photon.fg_bounces) trace(false, B.s_rays, B.s_idx, RayCount{out_w, 0, 0}, nullptr, B.s_occl);
+        hipLaunchKernelGGL(k_fg_resolve, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, in_w, qin, P.fgl.p);
+        HIPCHK(hipGetLastError());
+        qin ^= 1;
+      }
+    }
     // sub-path index outermost: pathCol is shared across sub-paths and
     // accumulated in the reference's order (pathtracer.cc:164-298)
     for (int isub = 0; isub < (path ? nsub : 0); ++isub) {

@@ -343,6 +343,21 @@ void yk_render_params_default(yk_render_params* p) {
   p->transp_background = 1;
   p->aa_inc_samples = 0;  // = aa_samples
   p->aa_threshold = 0.05f;
+  // photonIntegrator_t::factory (photonintegr.cc:884-960)
+  yk_photon_params& q = p->photon;
+  q.photons = 100000;
+  q.caustic_photons = 500000;
+  q.diffuse_radius = 0.1f;
+  q.caustic_radius = 0.01f;
+  q.search = 50;
+  q.caustic_mix = 50;
+  q.bounces = 5;
+  q.final_gather = 1;
+  q.fg_samples = 32;
+  q.fg_bounces = 2;
+  q.fg_min_pathlen = 0.1f;  // = diffuseRadius
+  q.show_map = 0;
+  q.seed = 123212;          // myseed, vector3d.cc:185
 }
 
 int yk_scene_generate(yk_scene* s, const char* name, int32_t p0, int32_t p1, int32_t resx,

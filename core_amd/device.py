@@ -95,3 +95,18 @@ class Device:
         st = stats if stats is not None else A.yk_stats()
         A.check(A.lib().yk_render(self._p, C.byref(params), out.ctypes.data_as(A.fp), C.byref(st)))
         return out
+
+    # -- photon mapping ---------------------------------------------------
+    def photon_build(self, params):
+        """photonIntegrator_t::preprocess on the device -> yk_photon_info"""
+        info = A.yk_photon_info()
+        A.check(A.lib().yk_photon_build(self._p, C.byref(params), C.byref(info)))
+        return info
+
+    def photon_map(self, which):
+        """(n, 9) float32 [pos, dir, color] of map `which` (YK_PHOTON_MAP_*), photon-vector order"""
+        n = C.c_int32()
+        A.check(A.lib().yk_photon_export(self._p, which, None, 0, C.byref(n)))
+        out = np.zeros((max(n.value, 1), 9), np.float32)
+        A.check(A.lib().yk_photon_export(self._p, which, out.ctypes.data_as(A.fp), n.value, C.byref(n)))
+        return out[:n.value]

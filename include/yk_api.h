@@ -82,9 +82,28 @@ typedef struct yk_camera { /* perspectiveCam_t::factory, perspectiveCamera.cc:19
   float focal, aspect_ratio, near_clip, far_clip;
 } yk_camera;
 
-enum { YK_INTEGRATOR_DIRECT = 0, YK_INTEGRATOR_PATH = 1 };
+enum { YK_INTEGRATOR_DIRECT = 0, YK_INTEGRATOR_PATH = 1, YK_INTEGRATOR_PHOTON = 2 };
 enum { YK_FILTER_BOX = 0, YK_FILTER_MITCHELL = 1, YK_FILTER_GAUSS = 2, YK_FILTER_LANCZOS = 3 };
 enum { YK_CAUSTIC_NONE = 0, YK_CAUSTIC_PATH = 1 };
+
+/* photonIntegrator_t parameters (photonintegr.cc:884-960 factory; defaults
+ * in brackets, set by yk_render_params_default). */
+typedef struct yk_photon_params {
+  int32_t photons;         /* "photons" [100000]: diffuse photons shot                */
+  int32_t caustic_photons; /* "cPhotons" [500000]                                     */
+  float diffuse_radius;    /* "diffuseRadius" [0.1]                                   */
+  float caustic_radius;    /* "causticRadius" [0.01]                                  */
+  int32_t search;          /* "search" [50]: nDiffuseSearch                           */
+  int32_t caustic_mix;     /* "caustic_mix" [= search]: nCausSearch                   */
+  int32_t bounces;         /* "bounces" [5]: maxBounces of the photon paths           */
+  int32_t final_gather;    /* "finalGather" [1]                                       */
+  int32_t fg_samples;      /* "fg_samples" [32]: nPaths                               */
+  int32_t fg_bounces;      /* "fg_bounces" [2]: gatherBounces                         */
+  float fg_min_pathlen;    /* "fg_min_pathlen" [= diffuseRadius]: gatherDist          */
+  int32_t show_map;        /* "show_map" [0]                                          */
+  int32_t seed;            /* the global ourRandom() state (myseed, vector3d.cc:185)
+                              when preprocess() starts [123212]                       */
+} yk_photon_params;
 
 typedef struct yk_render_params {
   int32_t integrator;     /* YK_INTEGRATOR_*                                         */
@@ -103,6 +122,7 @@ typedef struct yk_render_params {
   int32_t aa_inc_samples; /* "AA_inc_samples": samples per pass after the first (<= 0:
                              aa_samples, scene_t::setAntialiasing scene.cc:736-742)    */
   float aa_threshold;     /* "AA_threshold" (default 0.05): adaptive resampling     */
+  yk_photon_params photon; /* integrator == YK_INTEGRATOR_PHOTON                   */
 } yk_render_params;
 
 /* one ray, 32 bytes: ray_t (ray.h:26-49) without time */
@@ -288,6 +308,32 @@ int yk_render_film(yk_device* d, const yk_render_params* p, int32_t shard, int32
                    yk_stats* st);
 /* convenience: whole frame on one device, RGBA float image to host memory */
 int yk_render(yk_device* d, const yk_render_params* p, float* rgba_host, yk_stats* st);
+
+/* ---- photon mapping (photonIntegrator_t, photonintegr.cc) ---- */
+typedef struct yk_photon_info {
+  int32_t diffuse_photons;   /* diffuseMap.nPhotons()                                */
+  int32_t diffuse_paths;     /* diffuseMap.nPaths(): last path index that stored one */
+  int32_t caustic_photons;   /* causticMap.nPhotons()                                */
+  int32_t caustic_paths;
+  int32_t rad_candidates;    /* radiance points chosen by ourRandom() < 0.125        */
+  int32_t radiance_photons;  /* radiance points left after the 0.01*r elimination    */
+  int32_t seed_out;          /* myseed after preprocess                              */
+  int32_t tree_depth;        /* deepest diffuse-map kd-tree leaf                     */
+  uint64_t photon_rays;      /* scene_t::intersect calls of the photon paths         */
+  double ms_shoot, ms_tree, ms_pregather, ms_total;
+} yk_photon_info;
+
+/* photonIntegrator_t::preprocess (photonintegr.cc:126-633): shoot the diffuse
+ * photons on the device, build the photon kd-trees (kdtree::pointKdTree,
+ * pkdtree.h) on the host, pre-gather the radiance photons of final gathering
+ * on the device. The maps stay resident for yk_render_shard with
+ * p->integrator == YK_INTEGRATOR_PHOTON. Area and point lights; shinydiffuse
+ * without specular components (the caustic map stays empty). */
+int yk_photon_build(yk_device* d, const yk_render_params* p, yk_photon_info* info);
+enum { YK_PHOTON_MAP_DIFFUSE = 0, YK_PHOTON_MAP_CAUSTIC = 1, YK_PHOTON_MAP_RADIANCE = 2 };
+/* copy a map out in photon-vector order: 9 floats per photon (pos, dir, color);
+ * cap = capacity in photons; *n_out = photons in the map */
+int yk_photon_export(yk_device* d, int32_t which, float* out, int32_t cap, int32_t* n_out);
 
 #ifdef __cplusplus
 }

@@ -44,6 +44,8 @@ def lib():
         L.orc_fsin.argtypes = [C.c_float]
         L.orc_halton_seq.argtypes = [C.c_int, C.c_uint, C.c_int, vp]
         L.orc_faure.argtypes = [C.c_int, vp]
+        L.orc_photon_build.argtypes = [vp, vp, vp]
+        L.orc_photon_export.argtypes = [C.c_int32, vp, C.c_int32]
         _lib = L
     return _lib
 
@@ -136,3 +138,24 @@ class Oracle:
         out = np.zeros((h * w * spp, 8), np.float32)
         lib().orc_camera_rays(x0, y0, w, h, spp, out.ctypes.data)
         return out
+
+    def photon_build(self, params):
+        """photonIntegrator_t::preprocess -> dict of the map statistics"""
+        self._activate()
+        info = np.zeros(8, np.int32)
+        rays = np.zeros(1, np.uint64)
+        rc = lib().orc_photon_build(C.addressof(params), info.ctypes.data, rays.ctypes.data)
+        if rc:
+            raise RuntimeError(f"orc_photon_build failed ({rc})")
+        keys = ("diffuse_photons", "diffuse_paths", "caustic_photons", "caustic_paths", "rad_candidates",
+                "radiance_photons", "seed_out")
+        d = {k: int(info[i]) for i, k in enumerate(keys)}
+        d["photon_rays"] = int(rays[0])
+        return d
+
+    def photon_map(self, which):
+        """(n, 9) float32 [pos, dir, color] of map `which` (0 diffuse, 2 radiance)"""
+        n = lib().orc_photon_export(which, None, 0)
+        out = np.zeros((max(n, 1), 9), np.float32)
+        lib().orc_photon_export(which, out.ctypes.data, n)
+        return out[:n]

@@ -258,7 +258,7 @@ typedef struct {
   yk_camera cam;
   /* derived area-light data, areaLight_t ctor arealight.cc:30-49 */
   struct arealight {
-    v3 corner, c2, c3, c4, toX, toY, fnormal, normal;
+    v3 corner, c2, c3, c4, toX, toY, fnormal, normal, du, dv;
     col3 color;
     float area, inv_area;
     int samples;
@@ -856,6 +856,8 @@ static void lights_setup(void) {
     A->area = vl;
     A->inv_area = 1.0f / vl;
     A->normal = vneg(f);
+    A->du = vnormalize(A->toX); /* du = toX; du.normalize(); dv = normal ^ du */
+    A->dv = vcross(A->normal, A->du);
     A->c2 = vadd(corner, A->toX);
     A->c3 = vadd(corner, vadd(A->toX, A->toY));
     A->c4 = vadd(corner, A->toY);
@@ -1185,9 +1187,607 @@ static rgba dl_integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir,
   return r;
 }
 
+static rgba pm_integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir, float tmin, float tmax);
+
 static rgba integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir, float tmin, float tmax) {
+  if (P->integrator == YK_INTEGRATOR_PHOTON) return pm_integrate(st, P, from, dir, tmin, tmax);
   return (P->integrator == YK_INTEGRATOR_DIRECT) ? dl_integrate(st, P, from, dir, tmin, tmax)
                                                  : pt_integrate(st, P, from, dir, tmin, tmax);
+}
+
+/* -------------------------------------------------------- photon map -- */
+/* photonIntegrator_t (photonintegr.cc), photonMap_t (photon.h, photon.cc),
+ * kdtree::pointKdTree (pkdtree.h). Diffuse map + final gathering; the caustic
+ * map stays empty because the supported materials have no specular, glossy
+ * or dispersive component (a photon is only caustic after sampling one,
+ * photonintegr.cc:303-305). */
+
+typedef struct { v3 pos, dir; col3 c; } photon; /* photon_t without _SMALL_PHOTONS: pos, dir, color */
+typedef struct { v3 pos, normal; col3 refl, transm; int use; } raddata; /* radData_t, photon.h:133-141 */
+typedef struct { float division; int32_t data; uint32_t flags; } pnode; /* kdNode, pkdtree.h:17-43 */
+typedef struct { pnode* nodes; int next; const float* pos; int stride; } ptree; /* pos: element i at pos[i*stride] */
+typedef struct { int32_t idx; float d2; } found; /* foundPhoton_t; layout shared with stl_ref.cc */
+
+void orc_stl_make_heap(void* a, int32_t n);
+void orc_stl_replace_top(void* a, int32_t n, int32_t idx, float d2);
+void orc_stl_nth_element(int32_t* idx, int32_t n, int32_t k, const float* pos, int32_t stride, int32_t axis);
+
+static v3 pt_pos(const ptree* T, int i) {
+  const float* p = T->pos + (size_t)i * T->stride;
+  return V(p[0], p[1], p[2]);
+}
+
+/* pointKdTree::buildTree, pkdtree.h:122-148 */
+static void pt_build_rec(ptree* T, int start, int end, const float* bnd, int32_t* prims) {
+  if (end - start == 1) {
+    T->nodes[T->next].flags = 3u;
+    T->nodes[T->next].data = prims[start];
+    T->next++;
+    return;
+  }
+  float dx = bnd[3] - bnd[0], dy = bnd[4] - bnd[1], dz = bnd[5] - bnd[2]; /* bound_t::largestAxis, bound.h:118-122 */
+  int axis = (dx > dy) ? ((dx > dz) ? 0 : 2) : ((dy > dz) ? 1 : 2);
+  int splitEl = (int)(((unsigned)start + (unsigned)end) / 2u);
+  orc_stl_nth_element(prims + start, end - start, splitEl - start, T->pos, T->stride, axis);
+  int cur = T->next;
+  float splitPos = T->pos[(size_t)prims[splitEl] * T->stride + axis];
+  T->nodes[cur].division = splitPos;
+  T->nodes[cur].flags = (uint32_t)axis;
+  T->next++;
+  float bl[6], br[6];
+  memcpy(bl, bnd, sizeof bl);
+  memcpy(br, bnd, sizeof br);
+  bl[3 + axis] = splitPos;
+  br[axis] = splitPos;
+  pt_build_rec(T, start, splitEl, bl, prims);
+  T->nodes[cur].flags = (T->nodes[cur].flags & 3u) | ((uint32_t)T->next << 2);
+  pt_build_rec(T, splitEl, end, br, prims);
+}
+
+/* pointKdTree ctor, pkdtree.h:93-120 */
+static void pt_build(ptree* T, const float* pos, int stride, int n) {
+  free(T->nodes);
+  T->nodes = NULL;
+  T->next = 0;
+  T->pos = pos;
+  T->stride = stride;
+  if (n <= 0) return;
+  T->nodes = (pnode*)calloc((size_t)4 * n, sizeof(pnode));
+  int32_t* el = (int32_t*)malloc(sizeof(int32_t) * (size_t)n);
+  float b[6];
+  for (int k = 0; k < 3; ++k) b[k] = b[3 + k] = pos[k];
+  for (int i = 0; i < n; ++i) {
+    el[i] = i;
+    for (int k = 0; k < 3; ++k) { /* bound_t::include: std::min / std::max */
+      float v = pos[(size_t)i * stride + k];
+      if (v < b[k]) b[k] = v;
+      if (b[3 + k] < v) b[3 + k] = v;
+    }
+  }
+  pt_build_rec(T, 0, n, b, el);
+  free(el);
+}
+
+typedef void (*lookup_proc)(void* ctx, int idx, float dist2, float* maxd2);
+
+/* pointKdTree::lookup, NON_REC_LOOKUP form (pkdtree.h:180-236) */
+static void pt_lookup(const ptree* T, v3 p, lookup_proc proc, void* ctx, float* maxd2) {
+  struct { int node; float s; int axis; } stack[KD_MAX_STACK];
+  int cur = 0, farc, sp = 1;
+  stack[sp].node = -1;
+  for (;;) {
+    while ((T->nodes[cur].flags & 3u) != 3u) {
+      int axis = (int)(T->nodes[cur].flags & 3u);
+      float split = T->nodes[cur].division;
+      int right = (int)(T->nodes[cur].flags >> 2);
+      if (vget(p, axis) <= split) { farc = right; cur = cur + 1; }
+      else { farc = cur + 1; cur = right; }
+      ++sp;
+      stack[sp].node = farc;
+      stack[sp].axis = axis;
+      stack[sp].s = split;
+    }
+    int d = T->nodes[cur].data;
+    v3 v = vsub(pt_pos(T, d), p);
+    float dist2 = v.x * v.x + v.y * v.y + v.z * v.z; /* lengthSqr */
+    if (dist2 < *maxd2) proc(ctx, d, dist2, maxd2);
+    if (stack[sp].node < 0) return;
+    int axis = stack[sp].axis;
+    dist2 = vget(p, axis) - stack[sp].s;
+    dist2 *= dist2;
+    while (dist2 > *maxd2) {
+      --sp;
+      if (stack[sp].node < 0) return;
+      axis = stack[sp].axis;
+      dist2 = vget(p, axis) - stack[sp].s;
+      dist2 *= dist2;
+    }
+    cur = stack[sp].node;
+    --sp;
+  }
+}
+
+/* photonGather_t::operator(), photon.cc:53-73 */
+typedef struct { found* f; int k, n; } gather_ctx;
+static void proc_gather(void* vctx, int idx, float dist2, float* maxd2) {
+  gather_ctx* g = (gather_ctx*)vctx;
+  if (g->n < g->k) {
+    g->f[g->n].idx = idx;
+    g->f[g->n].d2 = dist2;
+    g->n++;
+    if (g->n == g->k) {
+      orc_stl_make_heap(g->f, g->k);
+      *maxd2 = g->f[0].d2;
+    }
+  } else {
+    orc_stl_replace_top(g->f, g->k, idx, dist2);
+    *maxd2 = g->f[0].d2;
+  }
+}
+
+/* nearestPhoton_t, photon.h:167-176 */
+typedef struct { const photon* ph; v3 n; int nearest; } nearest_ctx;
+static void proc_nearest(void* vctx, int idx, float dist2, float* maxd2) {
+  nearest_ctx* c = (nearest_ctx*)vctx;
+  if (vdot(c->ph[idx].dir, c->n) > 0.f) {
+    c->nearest = idx;
+    *maxd2 = dist2;
+  }
+}
+
+/* eliminatePhoton_t, photon.h:179-187 */
+typedef struct { raddata* rd; v3 n; } elim_ctx;
+static void proc_elim(void* vctx, int idx, float dist2, float* maxd2) {
+  elim_ctx* c = (elim_ctx*)vctx;
+  (void)dist2;
+  (void)maxd2;
+  if (vdot(c->rd[idx].normal, c->n) > 0.f) c->rd[idx].use = 0;
+}
+
+typedef struct {
+  photon* ph;
+  int n, cap, paths;
+  ptree tree;
+} pmap;
+static pmap g_dmap, g_rmap;
+static int g_pm_ready;
+static int g_myseed;
+
+static void pmap_push(pmap* m, v3 pos, v3 dir, col3 c) {
+  if (m->n == m->cap) {
+    m->cap = m->cap ? 2 * m->cap : 1024;
+    m->ph = (photon*)realloc(m->ph, sizeof(photon) * (size_t)m->cap);
+  }
+  photon* p = &m->ph[m->n++];
+  p->pos = pos;
+  p->dir = dir;
+  p->c = c;
+}
+
+/* photonMap_t::gather, photon.cc:115-121 */
+static int pmap_gather(const pmap* m, v3 P, found* f, int K, float* sqRadius) {
+  gather_ctx g = {f, K, 0};
+  pt_lookup(&m->tree, P, proc_gather, &g, sqRadius);
+  return g.n;
+}
+
+/* photonMap_t::findNearest, photon.cc:123-129; -1 = none */
+static int pmap_nearest(const pmap* m, v3 P, v3 n, float dist) {
+  nearest_ctx c = {m->ph, n, -1};
+  pt_lookup(&m->tree, P, proc_nearest, &c, &dist);
+  return c.nearest;
+}
+
+/* ourRandom, vector3d.h:352-362 (Park-Miller minimal standard, global myseed) */
+static float our_random(void) {
+  const int a = 0x000041A7, m = 0x7FFFFFFF, q = 0x0001F31D, r = 0x00000B14;
+  g_myseed = a * (g_myseed % q) - r * (g_myseed / q);
+  if (g_myseed < 0) g_myseed += m;
+  return (float)g_myseed / (float)m;
+}
+
+/* material_t::getReflectivity, material.cc:48-66 */
+static col3 get_reflectivity(const sdmat* M, const surfpt* sp, unsigned flags) {
+  if (!(flags & (BSDF_TRANSMIT | BSDF_REFLECT) & M->flags)) return C(0, 0, 0);
+  float W = 0.f;
+  col3 total = C(0, 0, 0);
+  for (int i = 0; i < 16; ++i) {
+    float s1 = (float)(0.03125 + 0.0625 * (double)(float)i);
+    float s2 = RI_vdC((unsigned)i, 0);
+    float s3 = (float)scrHalton(2, (unsigned)i);
+    float s4 = (float)scrHalton(3, (unsigned)i);
+    v3 wo = sample_cos_hemisphere(sp->N, sp->NU, sp->NV, s1, s2), wi = V(0, 0, 0);
+    float pdf;
+    int ok;
+    col3 col = sd_sample(M, sp, wo, &wi, s3, s4, flags, &pdf, &W, &ok, NULL);
+    total = cadd(total, C(col.r * W, col.g * W, col.b * W));
+  }
+  return C(total.r * 0.0625f, total.g * 0.0625f, total.b * 0.0625f);
+}
+
+static float cmax(col3 c) { /* color_t::maximum: std::max(R, std::max(G, B)) */
+  float gb = (c.g < c.b) ? c.b : c.g;
+  return (c.r < gb) ? gb : c.r;
+}
+
+/* material_t::scatterPhoton, material.cc:29-46 (pSample_t s(s1,s2,s3,BSDF_ALL,lcol,alpha)) */
+static int scatter_photon(const sdmat* M, const surfpt* sp, v3 wi, v3* wo, float s1, float s2, float s3, col3 lcol,
+                          col3 alpha, col3* color, unsigned* sflags) {
+  float W = 0.f, pdf = 0.f;
+  int ok;
+  col3 scol = sd_sample(M, sp, wi, wo, s1, s2, BSDF_ALL, &pdf, &W, &ok, sflags);
+  if (pdf > 1.0e-6f) {
+    col3 cnew = cmul(cmul(lcol, alpha), scol);
+    cnew = C(cnew.r * W, cnew.g * W, cnew.b * W);
+    float new_max = cmax(cnew), old_max = cmax(lcol);
+    float q = new_max / old_max;
+    float prob = (q < 1.f) ? q : 1.f; /* std::min(1.f, q) */
+    if (s3 <= prob && prob > 1e-4f) {
+      *color = C(cnew.r / prob, cnew.g / prob, cnew.b / prob);
+      return 1;
+    }
+  }
+  return 0;
+}
+
+/* light_t::emitPhoton: areaLight_t (arealight.cc:98-104), pointLight_t
+ * (pointlight.cc:91-97, SampleSphere sample_utils.h:54-72) */
+static col3 emit_photon(const struct arealight* A, float s1, float s2, float s3, float s4, v3* from, v3* dir,
+                        float* ipdf) {
+  if (A->type == YK_LIGHT_POINT) {
+    *from = A->pos;
+    v3 d;
+    d.z = 1.0f - 2.0f * s1;
+    float r = 1.0f - d.z * d.z;
+    if (r > 0.0f) {
+      r = sqrtf(r);
+      float a = (float)(M_2PI_D * (double)s2);
+      d.x = fCos(a) * r;
+      d.y = fSin(a) * r;
+    } else {
+      d.x = 0.0f;
+      d.y = 0.0f;
+    }
+    *dir = d;
+    *ipdf = (float)(4.0 * M_PI_D);
+    return A->color;
+  }
+  *ipdf = A->area;
+  *from = vadd(vadd(A->corner, vmul(s3, A->toX)), vmul(s4, A->toY));
+  *dir = sample_cos_hemisphere(A->normal, A->du, A->dv, s1, s2);
+  return A->color;
+}
+
+/* light_t::totalEnergy().energy() (arealight.cc:66, pointlight.cc:32; color.h:77) */
+static float light_energy(const struct arealight* A) {
+  col3 e;
+  if (A->type == YK_LIGHT_POINT) {
+    col3 c4 = C(A->color.r * 4.0f, A->color.g * 4.0f, A->color.b * 4.0f);
+    e = C(c4.r * (float)M_PI_D, c4.g * (float)M_PI_D, c4.b * (float)M_PI_D);
+  } else {
+    e = C(A->color.r * A->area, A->color.g * A->area, A->color.b * A->area);
+  }
+  return ((e.r + e.g) + e.b) * 0.333333f;
+}
+
+static int pm_supported(void) {
+  for (int m = 0; m < G.nmats; ++m)
+    if (g_sd[m].flags & (BSDF_SPECULAR | BSDF_GLOSSY | BSDF_DISPERSIVE | BSDF_FILTER)) return 0;
+  for (int l = 0; l < G.nlights; ++l)
+    if (G.al[l].type == YK_LIGHT_DIRECTIONAL) return 0;
+  return 1;
+}
+
+static uint64_t g_photon_rays;
+
+/* photonIntegrator_t::preprocess, photonintegr.cc:126-633 (diffuse map,
+ * radiance-point elimination, threaded pre-gather of preGatherWorker_t,
+ * radiance map). info: the yk_photon_info integer fields in order
+ * (diffuse_photons, diffuse_paths, caustic_photons, caustic_paths,
+ * rad_candidates, radiance_photons, seed_out); *rays = intersect calls. */
+int orc_photon_build(const yk_render_params* P, int32_t* info, uint64_t* rays) {
+  const yk_photon_params* pp = &P->photon;
+  if (!pm_supported()) return 4;
+  if (pp->photons <= 0 || pp->search <= 0 || G.nlights <= 0) return 1;
+  g_pm_ready = 0;
+  g_dmap.n = g_rmap.n = 0;
+  g_dmap.paths = g_rmap.paths = 0;
+  g_myseed = pp->seed;
+  uint64_t rays0 = g_nclosest;
+  int nL = G.nlights;
+  float fNumLights = (float)nL;
+  /* pdf1D_t(energies) + CumulateStep1dDF, sample_utils.h:85-118 */
+  float* func = (float*)malloc(sizeof(float) * nL);
+  float* cdf = (float*)malloc(sizeof(float) * (nL + 1));
+  for (int i = 0; i < nL; ++i) func[i] = light_energy(&G.al[i]);
+  double c = 0.0, delta = 1.0 / (double)nL;
+  cdf[0] = 0.0f;
+  for (int i = 1; i < nL + 1; ++i) {
+    c += (double)func[i - 1] * delta;
+    cdf[i] = (float)c;
+  }
+  float integral = (float)c;
+  for (int i = 1; i < nL + 1; ++i) cdf[i] /= integral;
+  float invIntegral = 1.f / integral;
+  float invDiffPhotons = 1.f / (float)pp->photons;
+  raddata* rad = NULL;
+  int nrad = 0, caprad = 0;
+  for (unsigned curr = 0; curr < (unsigned)pp->photons; ++curr) {
+    float s1 = RI_vdC(curr, 0), s2 = (float)scrHalton(2, curr), s3 = (float)scrHalton(3, curr),
+          s4 = (float)scrHalton(4, curr);
+    float sL = (float)curr * invDiffPhotons;
+    /* pdf1D_t::DSample, sample_utils.h:141-157 */
+    int lightNum;
+    float lightNumPdf;
+    if (sL == 0.f) {
+      lightNum = 0;
+    } else {
+      int k = 0;
+      while (k < nL + 1 && cdf[k] < sL) ++k; /* std::lower_bound */
+      lightNum = k - 1;
+      if (lightNum < 0) lightNum = 0;
+    }
+    if (lightNum >= nL) { free(func); free(cdf); free(rad); return 6; }
+    lightNumPdf = func[lightNum] * invIntegral;
+    v3 from, dir;
+    float lightPdf;
+    col3 pcol = emit_photon(&G.al[lightNum], s1, s2, s3, s4, &from, &dir, &lightPdf);
+    float k = (fNumLights * lightPdf) / lightNumPdf;
+    pcol = C(pcol.r * k, pcol.g * k, pcol.b * k);
+    if (cblack(pcol)) continue;
+    int nBounces = 0, causticPhoton = 0, directPhoton = 1;
+    surfpt sp;
+    float tmax = -1.0f;
+    while (scene_intersect(from, dir, MIN_RAYDIST, &tmax, &sp)) {
+      v3 wi = vneg(dir), wo = V(0, 0, 0);
+      const sdmat* M = mat_of(sp.mat);
+      unsigned bsdfs = M->flags;
+      if (bsdfs & BSDF_DIFFUSE) {
+        if (!causticPhoton) {
+          pmap_push(&g_dmap, sp.P, wi, pcol);
+          g_dmap.paths = (int)curr;
+        }
+        if (pp->final_gather && our_random() < 0.125 && !causticPhoton) {
+          if (nrad == caprad) {
+            caprad = caprad ? 2 * caprad : 1024;
+            rad = (raddata*)realloc(rad, sizeof(raddata) * (size_t)caprad);
+          }
+          raddata* r = &rad[nrad++];
+          r->pos = sp.P;
+          r->normal = (vdot(sp.Ng, wi) < 0) ? vneg(sp.N) : sp.N; /* FACE_FORWARD */
+          r->refl = get_reflectivity(M, &sp, BSDF_DIFFUSE | BSDF_GLOSSY | BSDF_REFLECT);
+          r->transm = get_reflectivity(M, &sp, BSDF_DIFFUSE | BSDF_GLOSSY | BSDF_TRANSMIT);
+          r->use = 1;
+        }
+      }
+      if (nBounces == pp->bounces) break;
+      int d5 = 3 * nBounces + 5;
+      float s5 = (float)scrHalton(d5, curr), s6 = (float)scrHalton(d5 + 1, curr), s7 = (float)scrHalton(d5 + 2, curr);
+      col3 ncol;
+      unsigned sfl = 0;
+      if (!scatter_photon(M, &sp, wi, &wo, s5, s6, s7, pcol, C(1.f, 1.f, 1.f), &ncol, &sfl)) break;
+      pcol = ncol;
+      causticPhoton = ((sfl & (BSDF_GLOSSY | BSDF_SPECULAR | BSDF_DISPERSIVE)) && directPhoton) ||
+                      ((sfl & (BSDF_GLOSSY | BSDF_SPECULAR | BSDF_FILTER | BSDF_DISPERSIVE)) && causticPhoton);
+      directPhoton = (sfl & BSDF_FILTER) && directPhoton;
+      from = sp.P;
+      dir = wo;
+      tmax = -1.0f;
+      ++nBounces;
+    }
+  }
+  g_photon_rays = g_nclosest - rays0;
+  free(func);
+  free(cdf);
+  info[0] = g_dmap.n;
+  info[1] = g_dmap.paths;
+  info[2] = 0;
+  info[3] = 0;
+  info[4] = nrad;
+  if (g_dmap.n < 50) { free(rad); return 2; } /* "Too few diffuse photons" */
+  pt_build(&g_dmap.tree, &g_dmap.ph[0].pos.x, (int)(sizeof(photon) / sizeof(float)), g_dmap.n);
+  if (pp->final_gather) {
+    /* remove too close radiance points (photonintegr.cc:551-566) */
+    ptree rt = {0};
+    pt_build(&rt, &rad[0].pos.x, (int)(sizeof(raddata) / sizeof(float)), nrad);
+    int* cleaned = (int*)malloc(sizeof(int) * (size_t)(nrad > 0 ? nrad : 1));
+    int nclean = 0;
+    float maxrad = 0.01f * pp->diffuse_radius;
+    for (int i = 0; i < nrad; ++i) {
+      if (rad[i].use) {
+        cleaned[nclean++] = i;
+        elim_ctx ec = {rad, rad[i].normal};
+        float md = maxrad;
+        pt_lookup(&rt, rad[i].pos, proc_elim, &ec, &md);
+      }
+    }
+    free(rt.nodes);
+    /* preGatherWorker_t::body, photonintegr.cc:50-96 */
+    found* gathered = (found*)malloc(sizeof(found) * (size_t)pp->search);
+    float dsRadius_2 = pp->diffuse_radius * pp->diffuse_radius;
+    float iScale = (float)(1.0 / ((double)(float)g_dmap.paths * M_PI_D));
+    for (int n = 0; n < nclean; ++n) {
+      const raddata* r = &rad[cleaned[n]];
+      float radius = dsRadius_2;
+      int ng = pmap_gather(&g_dmap, r->pos, gathered, pp->search, &radius);
+      col3 sum = C(0, 0, 0);
+      if (ng > 0) {
+        float scale = iScale / radius;
+        for (int i = 0; i < ng; ++i) {
+          const photon* ph = &g_dmap.ph[gathered[i].idx];
+          col3 f = (vdot(r->normal, ph->dir) > 0.f) ? r->refl : r->transm;
+          sum = cadd(sum, cmul(C(f.r * scale, f.g * scale, f.b * scale), ph->c));
+        }
+      }
+      pmap_push(&g_rmap, r->pos, r->normal, sum);
+    }
+    free(gathered);
+    free(cleaned);
+    if (g_rmap.n == 0) { free(rad); return 2; }
+    pt_build(&g_rmap.tree, &g_rmap.ph[0].pos.x, (int)(sizeof(photon) / sizeof(float)), g_rmap.n);
+  }
+  free(rad);
+  info[5] = g_rmap.n;
+  info[6] = g_myseed;
+  *rays = g_photon_rays;
+  g_pm_ready = 1;
+  return 0;
+}
+
+/* which: 0 diffuse, 1 caustic (always empty here), 2 radiance; 9 floats per photon */
+int orc_photon_export(int32_t which, float* out, int32_t cap) {
+  const pmap* m = which == 0 ? &g_dmap : (which == 2 ? &g_rmap : NULL);
+  int n = m ? m->n : 0;
+  for (int i = 0; i < n && i < cap; ++i) {
+    const photon* p = &m->ph[i];
+    float v[9] = {p->pos.x, p->pos.y, p->pos.z, p->dir.x, p->dir.y, p->dir.z, p->c.r, p->c.g, p->c.b};
+    memcpy(out + 9 * (size_t)i, v, sizeof v);
+  }
+  return n;
+}
+
+/* photonIntegrator_t::finalGathering, photonintegr.cc:637-790 (rayDivision 1) */
+static col3 final_gathering(rstate* st, const yk_render_params* P, const surfpt* sp, v3 wo) {
+  const yk_photon_params* pp = &P->photon;
+  const float lookupRad = (4 * pp->diffuse_radius) * pp->diffuse_radius;
+  col3 pathCol = C(0, 0, 0);
+  float W = 0.f;
+  int nSampl = pp->fg_samples > 1 ? pp->fg_samples : 1;
+  for (int i = 0; i < nSampl; ++i) {
+    surfpt hit = *sp, hit2;
+    v3 pwo = wo, pdir = V(0, 0, 0);
+    const sdmat* pm = mat_of(sp->mat);
+    unsigned offs = (unsigned)(pp->fg_samples * st->pixelSample) + st->samplingOffs + (unsigned)i;
+    col3 lcol = C(0, 0, 0), scol;
+    float s1 = RI_vdC(offs, 0), s2 = (float)scrHalton(2, offs), spdf;
+    int ok;
+    unsigned sfl;
+    scol = sd_sample(pm, &hit, pwo, &pdir, s1, s2, BSDF_DIFFUSE | BSDF_REFLECT | BSDF_TRANSMIT, &spdf, &W, &ok, NULL);
+    scol = C(scol.r * W, scol.g * W, scol.b * W);
+    if (cblack(scol)) continue;
+    col3 throughput = scol;
+    float ptmax = -1.0f;
+    if (!scene_intersect(hit.P, pdir, MIN_RAYDIST, &ptmax, &hit2)) continue; /* hit background */
+    hit = hit2;
+    pm = mat_of(hit.mat);
+    float length = ptmax;
+    unsigned matBSDFs = pm->flags;
+    int has_spec = (matBSDFs & BSDF_SPECULAR) != 0, caustic = 0;
+    int close = length < pp->fg_min_pathlen;
+    int do_bounce = close || has_spec, did_hit = 1;
+    for (int depth = 0; depth < pp->fg_bounces && do_bounce; ++depth) {
+      int d4 = 4 * depth;
+      pwo = vneg(pdir);
+      matBSDFs = pm->flags;
+      if (matBSDFs & BSDF_DIFFUSE) {
+        if (close) {
+          lcol = estimate_one_direct(st, &hit, pwo, (int)offs);
+        } else if (caustic) {
+          v3 sf = (vdot(hit.Ng, pwo) < 0) ? vneg(hit.N) : hit.N;
+          int nr = pmap_nearest(&g_rmap, hit.P, sf, lookupRad);
+          if (nr >= 0) lcol = g_rmap.ph[nr].c;
+        }
+        if (close || caustic) {
+          if (matBSDFs & BSDF_EMIT) lcol = cadd(lcol, mat_emit(pm, &hit, pwo, st->includeLights));
+          pathCol = cadd(pathCol, cmul(lcol, throughput));
+        }
+      }
+      s1 = (float)scrHalton(d4 + 3, offs);
+      s2 = (float)scrHalton(d4 + 4, offs);
+      unsigned fl = close ? BSDF_ALL : (BSDF_SPECULAR | BSDF_REFLECT | BSDF_TRANSMIT | BSDF_FILTER);
+      scol = sd_sample(pm, &hit, pwo, &pdir, s1, s2, fl, &spdf, &W, &ok, &sfl);
+      if (spdf <= 1.0e-6f) {
+        did_hit = 0;
+        break;
+      }
+      scol = C(scol.r * W, scol.g * W, scol.b * W);
+      throughput = cmul(throughput, scol);
+      ptmax = -1.0f;
+      if (!scene_intersect(hit.P, pdir, MIN_RAYDIST, &ptmax, &hit2)) {
+        if (caustic && G.has_bg) pathCol = cadd(pathCol, cmul(throughput, G.bg));
+        did_hit = 0;
+        break;
+      }
+      hit = hit2;
+      pm = mat_of(hit.mat);
+      length += ptmax;
+      caustic = (caustic || !depth) && (sfl & (BSDF_SPECULAR | BSDF_FILTER));
+      close = length < pp->fg_min_pathlen;
+      do_bounce = caustic || close;
+    }
+    if (did_hit) {
+      matBSDFs = pm->flags;
+      if (matBSDFs & (BSDF_DIFFUSE | BSDF_GLOSSY)) {
+        v3 nwo = vneg(pdir);
+        v3 sf = (vdot(hit.Ng, nwo) < 0) ? vneg(hit.N) : hit.N;
+        int nr = pmap_nearest(&g_rmap, hit.P, sf, lookupRad);
+        if (nr >= 0) lcol = g_rmap.ph[nr].c;
+        if (matBSDFs & BSDF_EMIT) lcol = cadd(lcol, mat_emit(pm, &hit, nwo, st->includeLights));
+        pathCol = cadd(pathCol, cmul(lcol, throughput));
+      }
+    }
+  }
+  float ns = (float)nSampl;
+  return C(pathCol.r / ns, pathCol.g / ns, pathCol.b / ns);
+}
+
+/* photonIntegrator_t::integrate, photonintegr.cc:792-882 */
+static rgba pm_integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir, float tmin, float tmax) {
+  const yk_photon_params* pp = &P->photon;
+  col3 col = C(0, 0, 0);
+  float alpha = P->transp_background ? 0.0f : 1.0f;
+  int oldIncludeLights = st->includeLights;
+  surfpt sp;
+  if (scene_intersect(from, dir, tmin, &tmax, &sp)) {
+    if (st->raylevel == 0) st->includeLights = 1;
+    const sdmat* M = mat_of(sp.mat);
+    unsigned bsdfs = M->flags;
+    v3 wo = vneg(dir);
+    col = cadd(col, mat_emit(M, &sp, wo, st->includeLights));
+    st->includeLights = 0;
+    if (pp->final_gather) {
+      if (pp->show_map) {
+        v3 N = (vdot(sp.Ng, wo) < 0) ? vneg(sp.N) : sp.N;
+        int nr = pmap_nearest(&g_rmap, sp.P, N, (4 * pp->diffuse_radius) * pp->diffuse_radius);
+        if (nr >= 0) col = cadd(col, g_rmap.ph[nr].c);
+      } else {
+        if (bsdfs & BSDF_EMIT) col = cadd(col, mat_emit(M, &sp, wo, st->includeLights));
+        if (bsdfs & BSDF_DIFFUSE) {
+          col = cadd(col, estimate_all_direct(st, &sp, wo));
+          col = cadd(col, final_gathering(st, P, &sp, wo));
+        }
+      }
+    } else {
+      if (pp->show_map) {
+        v3 N = (vdot(sp.Ng, wo) < 0) ? vneg(sp.N) : sp.N;
+        int nr = pmap_nearest(&g_dmap, sp.P, N, pp->diffuse_radius);
+        if (nr >= 0) col = cadd(col, g_dmap.ph[nr].c);
+      } else {
+        if (bsdfs & BSDF_EMIT) col = cadd(col, mat_emit(M, &sp, wo, st->includeLights));
+        if (bsdfs & BSDF_DIFFUSE) col = cadd(col, estimate_all_direct(st, &sp, wo));
+        found* gathered = (found*)malloc(sizeof(found) * (size_t)pp->search);
+        float radius = pp->diffuse_radius; /* "actually the square radius" */
+        int ng = g_dmap.n > 0 ? pmap_gather(&g_dmap, sp.P, gathered, pp->search, &radius) : 0;
+        if (ng > 0) {
+          float scale = (float)(1.0 / ((double)((float)g_dmap.paths * radius) * M_PI_D));
+          for (int i = 0; i < ng; ++i) {
+            const photon* ph = &g_dmap.ph[gathered[i].idx];
+            col3 surf = sd_eval(M, &sp, wo, ph->dir, BSDF_DIFFUSE);
+            col = cadd(col, cmul(C(surf.r * scale, surf.g * scale, surf.b * scale), ph->c));
+          }
+        }
+        free(gathered);
+      }
+    }
+    /* estimateCausticPhotons: the caustic map is empty (not ready) -> 0 */
+    recursive_raytrace(st, P, &sp, bsdfs, wo, &col, &alpha);
+    alpha = 1.0f; /* bg_transp_refract: getAlpha() = 1 for non-transparent materials */
+  } else if (G.has_bg) {
+    col = cadd(col, G.bg);
+  }
+  st->includeLights = oldIncludeLights;
+  rgba r = {col.r, col.g, col.b, alpha};
+  return r;
 }
 
 /* ------------------------------------------------------------- film -- */
@@ -1450,7 +2050,8 @@ int orc_render_shard(const yk_render_params* P, int32_t shard, int32_t nshards, 
 static int render_tiles(const yk_render_params* P, int shard, int nshards, float* rgba_out, float* film_sums,
                         uint64_t* counts) {
   if (P->aa_passes < 1) return 4;
-  if (P->aa_passes > 1 && nshards != 1) return 4; /* nextPass reads the whole film */
+  if (P->aa_passes > 1 && nshards != 1) return 4;
+  if (P->integrator == YK_INTEGRATOR_PHOTON && !g_pm_ready) return 3; /* preprocess() not run */ /* nextPass reads the whole film */
   film_t F;
   film_init(&F, P);
   g_nclosest = g_nshadow = g_nodes_c = g_tris_c = g_nodes_s = g_tris_s = 0;

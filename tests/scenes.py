@@ -129,3 +129,28 @@ def specular(resx, resy, integrator="cornell_pt", raydepth=3, caustic=False, nu=
     p.raydepth = raydepth
     p.caustic_type = 1 if caustic else 0
     return s, p
+
+
+def photon_scene(resx, resy, kind):
+    """Scenes for the photon-mapping integrator (photonintegr.cc): "translucent"
+    is the Cornell box with a translucent sphere (the DIFFUSE|TRANSMIT
+    component: transmitted radiance-point reflectivity, photons scattered
+    through); "point" adds a point light next to the area light (two
+    emitters: pdf1D_t light choice, pointLight_t::emitPhoton); "smooth_inst"
+    is the instanced smooth scene."""
+    if kind == "smooth_inst":
+        s, p, _ = smooth_instanced(resx, resy, "cornell_pt")
+        return s, p
+    s = Scene()
+    p = s.generate("cornell_pt", resx, resy)
+    if kind == "translucent":
+        transl = s.add_material(color=(0.9, 0.7, 0.3), diffuse_reflect=0.5, translucency=0.6)
+        pts, faces, nrm = uv_sphere(16, 10, 0.3, (0.1, 0.5, -0.4))
+        oid = s.add_mesh(pts, faces, transl)
+        s.set_mesh_normals(oid, nrm, faces, smooth=True)
+    elif kind == "point":
+        s.add_point_light((0.35, 1.55, -0.3), (1.0, 0.9, 0.7), 0.8)
+    else:
+        raise ValueError(kind)
+    s.build()
+    return s, p
