@@ -1252,7 +1252,7 @@ __device__ __forceinline__ c3 resolve_light(const Batch& B, long long c, int k0,
 // col += estimateAllDirectLight (sum over lights, starting from 0)
 __global__ void __launch_bounds__(256) k_resolve_primary(Batch B, RenderConst R, long long nc) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= nc || !(B.prim_hit[c] & PH_DIFFUSE)) return;
+  if (c >= nc || !(B.prim_hit[c] & PH_DIFFUSE) || R.pm_showmap) return;
   c3 dl = C3(0.f, 0.f, 0.f);
   int k0 = 0;
   for (int l = 0; l < R.nlights; ++l) {
