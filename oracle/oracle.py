@@ -46,6 +46,8 @@ def lib():
         L.orc_faure.argtypes = [C.c_int, vp]
         L.orc_photon_build.argtypes = [vp, vp, vp]
         L.orc_photon_export.argtypes = [C.c_int32, vp, C.c_int32]
+        L.orc_point_gather.argtypes = [vp, C.c_int32, vp, C.c_int32, vp, vp, vp]
+        L.orc_point_nearest.argtypes = [vp, vp, C.c_int32, vp, vp, C.c_float]
         _lib = L
     return _lib
 
@@ -159,3 +161,24 @@ class Oracle:
         out = np.zeros((max(n, 1), 9), np.float32)
         lib().orc_photon_export(which, out.ctypes.data, n)
         return out[:n]
+
+
+def point_gather(pos, q, K, sqr):
+    """photonMap_t::gather over points pos (n,3): (idx, d2) in heap order, shrunk radius"""
+    pos = np.ascontiguousarray(pos, np.float32)
+    q = np.ascontiguousarray(q, np.float32)
+    r = np.array([sqr], np.float32)
+    idx = np.zeros(K, np.int32)
+    d2 = np.zeros(K, np.float32)
+    n = lib().orc_point_gather(pos.ctypes.data, len(pos), q.ctypes.data, K, r.ctypes.data, idx.ctypes.data,
+                               d2.ctypes.data)
+    return idx[:n], d2[:n], float(r[0])
+
+
+def point_nearest(pos, dirs, q, nrm, dist):
+    """photonMap_t::findNearest: index of the nearest point with dir . nrm > 0 within dist (squared), or -1"""
+    pos = np.ascontiguousarray(pos, np.float32)
+    dirs = np.ascontiguousarray(dirs, np.float32)
+    q = np.ascontiguousarray(q, np.float32)
+    nrm = np.ascontiguousarray(nrm, np.float32)
+    return lib().orc_point_nearest(pos.ctypes.data, dirs.ctypes.data, len(pos), q.ctypes.data, nrm.ctypes.data, dist)

@@ -2142,3 +2142,33 @@ void orc_halton_seq(int base, unsigned start, int n, float* out) {
   for (int i = 0; i < n; ++i) out[i] = hal_next(&h);
 }
 void orc_faure(int dim, int* out) { qmc_init(); for (int i = 0; i < g_prims[dim]; ++i) out[i] = g_faure[dim][i]; }
+
+/* pointKdTree probes for the unit tests: build a tree over n points (3
+ * floats each) and run photonMap_t::gather / findNearest-style lookups.
+ * gather: *sqr in = squared search radius, out = the shrunk radius; returns
+ * the number found, out_idx / out_d2 in heap order. nearest: dirs (3 floats
+ * per point) and normal n; returns the index or -1. */
+int orc_point_gather(const float* pos, int32_t n, const float* q, int32_t K, float* sqr, int32_t* out_idx,
+                     float* out_d2) {
+  ptree T = {0};
+  pt_build(&T, pos, 3, n);
+  found* f = (found*)malloc(sizeof(found) * (size_t)(K > 0 ? K : 1));
+  gather_ctx g = {f, K, 0};
+  pt_lookup(&T, V(q[0], q[1], q[2]), proc_gather, &g, sqr);
+  for (int i = 0; i < g.n; ++i) { out_idx[i] = f[i].idx; out_d2[i] = f[i].d2; }
+  free(f);
+  free(T.nodes);
+  return g.n;
+}
+
+int orc_point_nearest(const float* pos, const float* dirs, int32_t n, const float* q, const float* nrm, float dist) {
+  ptree T = {0};
+  pt_build(&T, pos, 3, n);
+  photon* ph = (photon*)calloc((size_t)n, sizeof(photon));
+  for (int i = 0; i < n; ++i) ph[i].dir = V(dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2]);
+  nearest_ctx c = {ph, V(nrm[0], nrm[1], nrm[2]), -1};
+  pt_lookup(&T, V(q[0], q[1], q[2]), proc_nearest, &c, &dist);
+  free(ph);
+  free(T.nodes);
+  return c.nearest;
+}
