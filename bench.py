@@ -50,6 +50,11 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--integrator", default="path", choices=["path", "photon"],
+                    help="path: the headline pathtracing integrator; photon: photonmapping with final gathering "
+                         "(the photon maps are built once before timing, like the kd-tree)")
+    ap.add_argument("--photons", type=int, default=100000, help="photon: diffuse photons (reference default)")
+    ap.add_argument("--fg-samples", type=int, default=32, help="photon: final-gather paths per hit (default 32)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target length of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -80,6 +85,12 @@ def main():
     p.aa_samples = args.spp
     dev = Device(local)
     dev.upload(scene)
+    pm_info = None
+    if args.integrator == "photon":  # photonIntegrator_t::preprocess, once per scene (not timed)
+        p.integrator = A.YK_INTEGRATOR_PHOTON
+        p.photon.photons = args.photons
+        p.photon.fg_samples = args.fg_samples
+        pm_info = dev.photon_build(p)
     film = dev.new_film(p)
 
     def barrier():
@@ -138,7 +149,7 @@ def main():
     dom = kc if kc["ms"] >= ks["ms"] else ks
     traffic = None
     traffic_note = None
-    if os.path.exists(args.traffic) and args.scene == "bumpy":  # the committed PMC summary is of the bumpy run
+    if os.path.exists(args.traffic) and args.scene == "bumpy" and pm_info is None:  # PMC summary of the PT bumpy run
         with open(args.traffic) as f:
             tj = json.load(f)
         key = "closest" if dom is kc else "shadow"
@@ -163,8 +174,9 @@ def main():
         cpu = cpu_baseline(scene, p, args.cpu_seconds)
 
     out = {
-        "metric": "Mrays/s (primary+shadow), 1M-tri scene" if args.scene == "bumpy" else
-                  "Mrays/s (primary+shadow), 10M-tri hair scene (C5 shape)",
+        "metric": ("Mrays/s (primary+shadow), 1M-tri scene" if args.scene == "bumpy" else
+                   "Mrays/s (primary+shadow), 10M-tri hair scene (C5 shape)") +
+                  (", photon mapping" if pm_info is not None else ""),
         "value": round(value, 3),
         "unit": "Mrays/s",
         "n_gpus": world,
@@ -178,7 +190,10 @@ def main():
         "data": (f"synthetic: procedural displaced sphere + floor" if args.scene == "bumpy" else
                  f"synthetic: {args.strands} curve strands x {args.strand_points} points on a sphere + floor") +
                 f", {info.ntris} tris, kd-tree built on host ({t_build:.1f} s, not timed)",
-        "config": {"workload": f"{args.scene} {info.ntris} tris, pathtracing bounces {p.bounces}, "
+        "config": {"workload": f"{args.scene} {info.ntris} tris, " +
+                               (f"pathtracing bounces {p.bounces}, " if pm_info is None else
+                                f"photonmapping {p.photon.photons} photons, final gather {p.photon.fg_samples} paths "
+                                f"x {p.photon.fg_bounces} bounces, search {p.photon.search}, ") +
                                f"{p.width}x{p.height}, {p.aa_samples} spp, {info.nlights} area light(s) 1 sample",
                    "tris": int(info.ntris), "width": p.width, "height": p.height, "spp": p.aa_samples,
                    "parallelism": f"tiles%{world}" if world > 1 else "single",
@@ -191,6 +206,11 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
+    if pm_info is not None:
+        out["config"]["photon_maps"] = {
+            "diffuse_photons": pm_info.diffuse_photons, "radiance_photons": pm_info.radiance_photons,
+            "photon_rays": int(pm_info.photon_rays), "preprocess_ms": round(pm_info.ms_total, 1),
+            "shoot_ms": round(pm_info.ms_shoot, 1), "pregather_ms": round(pm_info.ms_pregather, 1)}
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
@@ -203,6 +223,8 @@ def cpu_baseline(scene, p, seconds):
     from oracle.oracle import Oracle
     orc = Oracle(scene)
     q = A.yk_render_params.from_buffer_copy(p)
+    if q.integrator == A.YK_INTEGRATOR_PHOTON:
+        orc.photon_build(q)  # the oracle's own preprocess (not timed, like the device's)
     q.width, q.height = 16, 16
     q.xstart, q.ystart = p.width // 2, p.height // 2
     t0 = time.perf_counter()

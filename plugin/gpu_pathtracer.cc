@@ -276,6 +276,18 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     if (yk_scene_set_camera_state(ys, &cs) != YK_OK) return fail();
     if (yk_scene_build(ys) != YK_OK) return fail();
     if (yk_device_open(0, &dev) != YK_OK || yk_device_upload(dev, ys) != YK_OK) return fail();
+    if (params.integrator == YK_INTEGRATOR_PHOTON) {
+      // photonIntegrator_t::preprocess (photonintegr.cc:126-633) on the
+      // device; the radiance points draw from the global ourRandom() state
+      // (myseed, vector3d.cc:185), which continues afterwards as if the
+      // reference had drawn them
+      params.photon.seed = myseed;
+      yk_photon_info info{};
+      if (yk_photon_build(dev, &params, &info) != YK_OK) return fail();
+      myseed = info.seed_out;
+      Y_INFO << integratorName << ": " << info.diffuse_photons << " diffuse photons, " << info.radiance_photons
+             << " radiance photons (" << info.ms_total << " ms)" << yendl;
+    }
     return true;
   }
 
@@ -339,6 +351,54 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     pm.getParam("bg_transp", bg);
     p.transp_background = bg;
     return new gpuTiledIntegrator_t(p, "DirectLight");
+  }
+  // photonIntegrator_t::factory (photonintegr.cc:884-960): same parameter
+  // names and defaults (yk_render_params_default)
+  static integrator_t* factory_photon(paraMap_t& pm, renderEnvironment_t&) {
+    yk_render_params p;
+    yk_render_params_default(&p);
+    p.integrator = YK_INTEGRATOR_PHOTON;
+    yk_photon_params& q = p.photon;
+    bool transp_shad = false, fg = true, show_map = false, bg = true;
+    int raydepth = 5, photons = q.photons, cphotons = q.caustic_photons, search = q.search, bounces = q.bounces,
+        fg_samples = q.fg_samples, fg_bounces = q.fg_bounces;
+    float ds_rad = q.diffuse_radius, c_rad = q.caustic_radius;
+    pm.getParam("transpShad", transp_shad);
+    pm.getParam("raydepth", raydepth);
+    pm.getParam("photons", photons);
+    pm.getParam("cPhotons", cphotons);
+    pm.getParam("diffuseRadius", ds_rad);
+    pm.getParam("causticRadius", c_rad);
+    pm.getParam("search", search);
+    int caustic_mix = search;
+    pm.getParam("caustic_mix", caustic_mix);
+    pm.getParam("bounces", bounces);
+    pm.getParam("finalGather", fg);
+    pm.getParam("fg_samples", fg_samples);
+    pm.getParam("fg_bounces", fg_bounces);
+    float gather_dist = ds_rad;
+    pm.getParam("fg_min_pathlen", gather_dist);
+    pm.getParam("show_map", show_map);
+    pm.getParam("bg_transp", bg);
+    bool use_sss = false;
+    pm.getParam("useSSS", use_sss);
+    if (transp_shad) { Y_ERROR << "PhotonMap: transparent shadows are not on the GPU path" << yendl; return nullptr; }
+    if (use_sss) { Y_ERROR << "PhotonMap: SSS photons are not on the GPU path" << yendl; return nullptr; }
+    p.raydepth = raydepth;
+    p.transp_background = bg;
+    q.photons = photons;
+    q.caustic_photons = cphotons;
+    q.diffuse_radius = ds_rad;
+    q.caustic_radius = c_rad;
+    q.search = search;
+    q.caustic_mix = caustic_mix;
+    q.bounces = bounces;
+    q.final_gather = fg;
+    q.fg_samples = fg_samples;
+    q.fg_bounces = fg_bounces;
+    q.fg_min_pathlen = gather_dist;
+    q.show_map = show_map;
+    return new gpuTiledIntegrator_t(p, "PhotonMap");
   }
 
  private:
@@ -417,6 +477,7 @@ YAFRAYPLUGIN_EXPORT void registerPlugin(renderEnvironment_t& render) {
   // (registerFactory is a map assignment, environment.cc:738-742)
   render.registerFactory("pathtracing", gpuTiledIntegrator_t::factory_path);
   render.registerFactory("directlighting", gpuTiledIntegrator_t::factory_direct);
+  render.registerFactory("photonmapping", gpuTiledIntegrator_t::factory_photon);
 }
 }
 
