@@ -565,6 +565,10 @@ __device__ __forceinline__ SurfPt make_surface(const DScene& S, v3 from, v3 dir,
   return sp;
 }
 
+__device__ __forceinline__ v3 face_forward(v3 Ng, v3 N, v3 I) {  // FACE_FORWARD, material.h:30
+  return (vdot(Ng, I) < 0.f) ? vneg(N) : N;
+}
+
 // getFresnel, shinydiffuse.cc:100-122. Compiled form: c = |N.wo| (the
 // face-forward sign folded into fabs), g tested as ior2 + c*c < 1,
 // 0.5*(g-c)^2 as ((g-c)*(g-c))*0.5, aux = (g+c)*c.
@@ -1144,7 +1148,15 @@ __device__ __forceinline__ yk_ray path_first_segment(const Batch& B, const Rende
 // Camera-ray hit (pathtracer.cc:146-160, directlight.cc:124-135): emission
 // and the estimateAllDirectLight shadow rays; for the path tracer also the
 // first segment of sub-path 0 (appended to bounce queue 1).
-__global__ void __launch_bounds__(256) k_shade_primary(DScene S, Batch B, RenderConst R, long long nc,
+#ifndef YK_SHADE_WAVES
+#define YK_SHADE_WAVES 0  // 0: compiler's choice (128 / 122 VGPRs -> 4 waves per SIMD)
+#endif
+#if YK_SHADE_WAVES > 0
+#define YK_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(YK_SHADE_WAVES)))
+#else
+#define YK_SHADE_ATTR
+#endif
+__global__ void __launch_bounds__(256) YK_SHADE_ATTR k_shade_primary(DScene S, Batch B, RenderConst R, long long nc,
                                                        unsigned long long* __restrict__ qword) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = c < nc;
@@ -1168,7 +1180,10 @@ __global__ void __launch_bounds__(256) k_shade_primary(DScene S, Batch B, Render
         // spec mode: emission is added at the fold, where state.includeLights
         // of this recursion level is known (lightMat_t::emit depends on it)
         const c3 e = mat_emit(M, sp, wo, true);
-        if (R.spec) em = e;
+        // photon mapping: includeLights is true at every recursion level
+        // (recursiveRaytrace sets it, integrate() restores it), so its
+        // emission needs no fold-time decision
+        if (R.spec && R.integrator != YK_INTEGRATOR_PHOTON) em = e;
         else col = cadd(col, e);
         // photonIntegrator_t::integrate adds emit() a second time after
         // includeLights = false (photonintegr.cc:812-831)
@@ -1296,7 +1311,7 @@ __global__ void __launch_bounds__(256) k_path_start(DScene S, Batch B, RenderCon
 // (pathtracer.cc:189-298): estimateOneDirectLight shadow rays, emission,
 // and the BSDF sample of the next segment. One thread per live path (entry
 // qi of the input bounce queue, owned by camera sample c).
-__global__ void __launch_bounds__(256) k_shade_bounce(DScene S, Batch B, RenderConst R,
+__global__ void __launch_bounds__(256) YK_SHADE_ATTR k_shade_bounce(DScene S, Batch B, RenderConst R,
                                                       const unsigned long long* __restrict__ qin_word, int depth,
                                                       int isub, int qin, unsigned long long* __restrict__ qword) {
   const long long nq = (long long)(*qin_word >> 32);  // live paths (device-side count)
@@ -1421,7 +1436,7 @@ __global__ void __launch_bounds__(256) k_finish(Batch B, RenderConst R, long lon
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= nc) return;
   c3 col = C3(B.col[3 * c], B.col[3 * c + 1], B.col[3 * c + 2]);
-  if ((R.integrator == YK_INTEGRATOR_PATH || R.pm_fg) && (B.prim_hit[c] & PH_DIFFUSE)) {
+  if (R.integrator == YK_INTEGRATOR_PATH && (B.prim_hit[c] & PH_DIFFUSE)) {
     const float ns = (float)R.nsub;
     col = cadd(col, C3(B.pathcol[3 * c] / ns, B.pathcol[3 * c + 1] / ns, B.pathcol[3 * c + 2] / ns));
   }
@@ -1458,6 +1473,7 @@ struct NodeStore {
   unsigned long long* count;  // allocated node ids
   long long cap;
   int* overflow;
+  float* malpha;  // photon mapping: material_t::getAlpha at the node's hit (1 unless transparent)
 };
 
 // Terms of the n entries of one chunk (node ids base..base+n-1).
@@ -1488,6 +1504,7 @@ __global__ void __launch_bounds__(256) k_finish_spec(Batch B, RenderConst R, Nod
   NS.P[3 * node + 2] = P.b;
   NS.child[2 * node] = -1;
   NS.child[2 * node + 1] = -1;
+  NS.malpha[node] = 1.f;
   if (R.level == 0) NS.alpha[node] = B.alpha[i];
 }
 
@@ -1507,6 +1524,13 @@ __global__ void __launch_bounds__(256) k_spawn(DScene S, Batch B, RenderConst R,
   if (!(M.flags & (BSDF_SPECULAR | BSDF_FILTER))) return;
   const long long node = base + i;
   NS.flags[node] |= NF_SPEC;
+  if (R.integrator == YK_INTEGRATOR_PHOTON && (M.flags & BSDF_FILTER)) {
+    // shinyDiffuseMat_t::getAlpha (shinydiffuse.cc:457-469) of a transparent material
+    const v3 wo = vneg(dir);
+    const float Kr = mat_fresnel(M, wo, face_forward(sp.Ng, sp.N, wo));
+    const float refl = (1.f - M.comp[0] * Kr) * M.comp[1];
+    NS.malpha[node] = 1.f - refl;
+  }
   bool refl, refr;
   v3 d[2];
   c3 col[2];
@@ -1538,7 +1562,10 @@ __global__ void __launch_bounds__(256) k_fold(Batch B, RenderConst R, NodeStore 
   constexpr int kMaxLevel = 22;
   int nodes[kMaxLevel], stage[kMaxLevel];
   c3 acc[kMaxLevel];
-  const bool pt = R.integrator == YK_INTEGRATOR_PATH;
+  float alp[kMaxLevel];  // photon mapping: integrate()'s alpha, set by the refract child
+  const bool pt = R.integrator == YK_INTEGRATOR_PATH, pm = R.integrator == YK_INTEGRATOR_PHOTON;
+  const float a_init = R.transp_bg ? 0.f : 1.f;
+  float result_alpha = 0.f;
   bool e = true;  // state.includeLights
   int dd = 0;
   nodes[0] = (int)c;
@@ -1560,6 +1587,7 @@ __global__ void __launch_bounds__(256) k_fold(Batch B, RenderConst R, NodeStore 
         if (F & NF_SPEC) e = true;
       }
       acc[dd] = col;
+      alp[dd] = a_init;
       stage[dd] = 1;
       const int ch = (F & NF_HIT) ? NS.child[2 * n] : -1;
       if (ch >= 0 && dd + 1 < kMaxLevel) {
@@ -1580,17 +1608,22 @@ __global__ void __launch_bounds__(256) k_fold(Batch B, RenderConst R, NodeStore 
       }
     }
     const c3 v = acc[dd];
+    // photonintegr.cc:862-866: alpha = m_alpha + (1 - m_alpha) * alpha on a hit
+    const float m = NS.malpha[n];
+    const float va = (F & NF_HIT) ? m + (1.f - m) * alp[dd] : a_init;
     if (dd == 0) {
       result = v;
+      result_alpha = va;
       break;
     }
     --dd;
     const int pn = nodes[dd];
     const int k = stage[dd] - 1;
+    if (k == 1) alp[dd] = va;  // recursiveRaytrace: alpha = integ.A of the refracted ray
     const float* rc = NS.rcol + 6 * pn + 3 * k;
     acc[dd] = cadd(acc[dd], C3(v.r * rc[0], v.g * rc[1], v.b * rc[2]));
   }
-  B.samples[c] = make_float4(result.r, result.g, result.b, NS.alpha[c]);
+  B.samples[c] = make_float4(result.r, result.g, result.b, pm ? result_alpha : NS.alpha[c]);
 }
 
 // ------------------------------------------------------------ film
@@ -1916,7 +1949,7 @@ struct yk_device {
   bool crowded_leaves = false;  // mean references per non-empty leaf above kCrowdedLeaf: PIPE leaf loop
   int per_cu_lp[2] = {1, 1};
   // node store of the specular recursion (k_finish_spec / k_spawn / k_fold)
-  DBuf<float> nE, nD, nP, nrcol, nalpha;
+  DBuf<float> nE, nD, nP, nrcol, nalpha, nmalpha;
   DBuf<int> nflags, nchild, noverflow;
   DBuf<yk_ray> nray;
   DBuf<unsigned> nsoffs, npsample;
@@ -1927,10 +1960,11 @@ struct yk_device {
   // photon maps of yk_photon_build (photonIntegrator_t::preprocess)
   bool pm_ready = false;
   yk_photon_params pm_params{};
-  DBuf<uint2> dm_nodes, rm_nodes;
-  DBuf<float4> dm_pos, dm_dir, dm_col, rm_pos, rm_dir, rm_col;
-  std::vector<float> dm_host, rm_host;  // 9 floats per photon, photon-vector order
-  int dm_paths = 0;
+  DBuf<uint2> dm_nodes, rm_nodes, cm_nodes;
+  DBuf<float4> dm_pos, dm_dir, dm_col, rm_pos, rm_dir, rm_col, cm_pos, cm_dir, cm_col;
+  std::vector<float> dm_host, rm_host, cm_host;  // 9 floats per photon, photon-vector order
+  int dm_paths = 0, cm_paths = 0;
+  std::vector<unsigned> mat_flags;  // bsdfFlags per material
   Pipe pipe[kPipes];
   hipEvent_t gather_ev[kPipes] = {};
   ~yk_device() {
@@ -2257,8 +2291,10 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
                      hipMemcpyHostToDevice));
   std::vector<DMat> mats;
   d->spec = false;
+  d->mat_flags.clear();
   for (const auto& m : S.material_states) {
     mats.push_back(make_mat(m));
+    d->mat_flags.push_back(m.bsdf_flags);
     if (m.bsdf_flags & (BSDF_SPECULAR | BSDF_FILTER)) d->spec = true;
   }
   if (!mats.empty()) HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_mats), mats.data(), mats.size() * sizeof(DMat)));
@@ -2607,9 +2643,11 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     d->npsample.ensure(cap);
     d->ncount.ensure(1);
     d->noverflow.ensure(1);
+    d->nmalpha.ensure(cap);
     d->spec_words.ensure((size_t)words_per_batch);
     NS = NodeStore{d->nE.p,   d->nD.p,     d->nP.p,       d->nflags.p, d->nchild.p,  d->nrcol.p,    d->nalpha.p,
-                   d->nray.p, d->nsoffs.p, d->npsample.p, d->ncount.p, (long long)cap, d->noverflow.p};
+                   d->nray.p, d->nsoffs.p, d->npsample.p, d->ncount.p, (long long)cap, d->noverflow.p,
+                   d->nmalpha.p};
     HIPCHK(hipMemsetAsync(d->noverflow.p, 0, sizeof(int), d->pipe[0].stream));
   }
   struct Timed {
@@ -2637,6 +2675,36 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
       evn[pi] += 2;
       if (closest) enqueue_trace<true>(d, P, rays, idx, n, hits, occ, work, P.words.p, e0, e1);
       else enqueue_trace<false>(d, P, rays, idx, n, hits, occ, work, P.words.p + 4, e0, e1);
+    };
+    // photonIntegrator_t::integrate after the direct light: show_map /
+    // diffuse-map estimate, final gathering, caustics (photonintegr.cc:819-852)
+    auto pm_entries = [&](const Batch& Bc, const RenderConst& Rc, long long n) {
+      if (pm && (PMC.show_map || !PMC.final_gather)) {
+        hipLaunchKernelGGL(k_pm_post, dim3(grid_for(n, 64)), dim3(64), 0, P.stream, d->S, Bc, PMC, n);
+        HIPCHK(hipGetLastError());
+      }
+      // final gathering (photonintegr.cc:637-790): gather path index outermost,
+      // pathCol accumulated across paths in the reference's order
+      for (int isub = 0; isub < (R.pm_fg ? nsub : 0); ++isub) {
+        hipLaunchKernelGGL(k_fg_start, dim3(grid_for(n)), dim3(256), 0, P.stream, d->S, Bc, Rc, n, isub, P.fgl.p,
+                           qw(isub, 0));
+        HIPCHK(hipGetLastError());
+        int qin = 1;
+        for (int it = 0; it <= p->photon.fg_bounces; ++it) {
+          const unsigned long long* in_w = qw(isub, it);
+          unsigned long long* out_w = qw(isub, it + 1);
+          trace(true, Bc.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, Bc.q_hits[qin], nullptr);
+          hipLaunchKernelGGL(k_fg_hit, dim3(grid_for(n)), dim3(256), 0, P.stream, d->S, Bc, Rc, PMC, in_w, it, isub, qin,
+                             P.fgl.p, P.fglen.p, out_w);
+          HIPCHK(hipGetLastError());
+          if (it < p->photon.fg_bounces) trace(false, Bc.s_rays, Bc.s_idx, RayCount{out_w, 0, 0}, nullptr, Bc.s_occl);
+          hipLaunchKernelGGL(k_fg_resolve, dim3(grid_for(n)), dim3(256), 0, P.stream, Bc, Rc, in_w, qin, P.fgl.p);
+          HIPCHK(hipGetLastError());
+          qin ^= 1;
+        }
+      }
+      hipLaunchKernelGGL(k_pm_finish, dim3(grid_for(n, 64)), dim3(64), 0, P.stream, d->S, Bc, Rc, PMC, n);
+      HIPCHK(hipGetLastError());
     };
     TileList TL{tiles_dev.p + (size_t)bi * tiles_per_batch, base_dev.p + (size_t)bi * (tiles_per_batch + 1),
                 (int)std::min<size_t>(tiles_per_batch, owned.size() - (size_t)bi * tiles_per_batch),
@@ -2680,6 +2748,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
             qin ^= 1;
           }
         }
+        if (pm) pm_entries(Bc, Rc, n);
         hipLaunchKernelGGL(k_finish_spec, dim3(grid_for(n)), dim3(256), 0, P.stream, Bc, Rc, NS, node_base, n);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_spawn, dim3(grid_for(n)), dim3(256), 0, P.stream, d->S, Bc, Rc, NS, node_base, n);
@@ -2718,30 +2787,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     trace(false, B.s_rays, B.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, B.s_occl);
     hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
     HIPCHK(hipGetLastError());
-    if (pm && (PMC.show_map || !PMC.final_gather)) {
-      hipLaunchKernelGGL(k_pm_post, dim3(grid_for(nc, 64)), dim3(64), 0, P.stream, d->S, B, PMC, nc);
-      HIPCHK(hipGetLastError());
-    }
-    // final gathering (photonintegr.cc:637-790): gather path index outermost,
-    // pathCol accumulated across paths in the reference's order
-    for (int isub = 0; isub < (R.pm_fg ? nsub : 0); ++isub) {
-      hipLaunchKernelGGL(k_fg_start, dim3(grid_for(nc)), dim3(256), 0, P.stream, d->S, B, R, nc, isub, P.fgl.p,
-                         qw(isub, 0));
-      HIPCHK(hipGetLastError());
-      int qin = 1;
-      for (int it = 0; it <= p->photon.fg_bounces; ++it) {
-        const unsigned long long* in_w = qw(isub, it);
-        unsigned long long* out_w = qw(isub, it + 1);
-        trace(true, B.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, B.q_hits[qin], nullptr);
-        hipLaunchKernelGGL(k_fg_hit, dim3(grid_for(nc)), dim3(256), 0, P.stream, d->S, B, R, PMC, in_w, it, isub, qin,
-                           P.fgl.p, P.fglen.p, out_w);
-        HIPCHK(hipGetLastError());
-        if (it < p->photon.fg_bounces) trace(false, B.s_rays, B.s_idx, RayCount{out_w, 0, 0}, nullptr, B.s_occl);
-        hipLaunchKernelGGL(k_fg_resolve, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, in_w, qin, P.fgl.p);
-        HIPCHK(hipGetLastError());
-        qin ^= 1;
-      }
-    }
+    if (pm) pm_entries(B, R, nc);
     // sub-path index outermost: pathCol is shared across sub-paths and
     // accumulated in the reference's order (pathtracer.cc:164-298)
     for (int isub = 0; isub < (path ? nsub : 0); ++isub) {

@@ -1197,10 +1197,9 @@ static rgba integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir, fl
 
 /* -------------------------------------------------------- photon map -- */
 /* photonIntegrator_t (photonintegr.cc), photonMap_t (photon.h, photon.cc),
- * kdtree::pointKdTree (pkdtree.h). Diffuse map + final gathering; the caustic
- * map stays empty because the supported materials have no specular, glossy
- * or dispersive component (a photon is only caustic after sampling one,
- * photonintegr.cc:303-305). */
+ * kdtree::pointKdTree (pkdtree.h): diffuse map, final gathering, caustic map
+ * (shinydiffuse's mirror component starts caustic photons, its transparency
+ * keeps them caustic) and mcIntegrator_t::estimateCausticPhotons. */
 
 typedef struct { v3 pos, dir; col3 c; } photon; /* photon_t without _SMALL_PHOTONS: pos, dir, color */
 typedef struct { v3 pos, normal; col3 refl, transm; int use; } raddata; /* radData_t, photon.h:133-141 */
@@ -1349,7 +1348,7 @@ typedef struct {
   int n, cap, paths;
   ptree tree;
 } pmap;
-static pmap g_dmap, g_rmap;
+static pmap g_dmap, g_rmap, g_cmap;
 static int g_pm_ready;
 static int g_myseed;
 
@@ -1471,8 +1470,6 @@ static float light_energy(const struct arealight* A) {
 }
 
 static int pm_supported(void) {
-  for (int m = 0; m < G.nmats; ++m)
-    if (g_sd[m].flags & (BSDF_SPECULAR | BSDF_GLOSSY | BSDF_DISPERSIVE | BSDF_FILTER)) return 0;
   for (int l = 0; l < G.nlights; ++l)
     if (G.al[l].type == YK_LIGHT_DIRECTIONAL) return 0;
   return 1;
@@ -1485,15 +1482,13 @@ static uint64_t g_photon_rays;
  * radiance map). info: the yk_photon_info integer fields in order
  * (diffuse_photons, diffuse_paths, caustic_photons, caustic_paths,
  * rad_candidates, radiance_photons, seed_out); *rays = intersect calls. */
-int orc_photon_build(const yk_render_params* P, int32_t* info, uint64_t* rays) {
-  const yk_photon_params* pp = &P->photon;
-  if (!pm_supported()) return 4;
-  if (pp->photons <= 0 || pp->search <= 0 || G.nlights <= 0) return 1;
-  g_pm_ready = 0;
-  g_dmap.n = g_rmap.n = 0;
-  g_dmap.paths = g_rmap.paths = 0;
-  g_myseed = pp->seed;
-  uint64_t rays0 = g_nclosest;
+/* One photon pass of preprocess: the diffuse pass (photonintegr.cc:219-314)
+ * or the caustic pass (:316-460). Both shoot nphotons paths from the lights
+ * chosen by pdf1D_t over their energies; the diffuse pass stores non-caustic
+ * photons and draws one ourRandom() per diffuse hit for the radiance points,
+ * the caustic pass stores caustic photons. */
+static int shoot_photons(const yk_photon_params* pp, int caustic_pass, unsigned nphotons, pmap* map, raddata** rad,
+                         int* nrad, int* caprad) {
   int nL = G.nlights;
   float fNumLights = (float)nL;
   /* pdf1D_t(energies) + CumulateStep1dDF, sample_utils.h:85-118 */
@@ -1509,16 +1504,13 @@ int orc_photon_build(const yk_render_params* P, int32_t* info, uint64_t* rays) {
   float integral = (float)c;
   for (int i = 1; i < nL + 1; ++i) cdf[i] /= integral;
   float invIntegral = 1.f / integral;
-  float invDiffPhotons = 1.f / (float)pp->photons;
-  raddata* rad = NULL;
-  int nrad = 0, caprad = 0;
-  for (unsigned curr = 0; curr < (unsigned)pp->photons; ++curr) {
+  float invPhotons = 1.f / (float)nphotons;
+  for (unsigned curr = 0; curr < nphotons; ++curr) {
     float s1 = RI_vdC(curr, 0), s2 = (float)scrHalton(2, curr), s3 = (float)scrHalton(3, curr),
           s4 = (float)scrHalton(4, curr);
-    float sL = (float)curr * invDiffPhotons;
+    float sL = (float)curr * invPhotons;
     /* pdf1D_t::DSample, sample_utils.h:141-157 */
     int lightNum;
-    float lightNumPdf;
     if (sL == 0.f) {
       lightNum = 0;
     } else {
@@ -1527,8 +1519,8 @@ int orc_photon_build(const yk_render_params* P, int32_t* info, uint64_t* rays) {
       lightNum = k - 1;
       if (lightNum < 0) lightNum = 0;
     }
-    if (lightNum >= nL) { free(func); free(cdf); free(rad); return 6; }
-    lightNumPdf = func[lightNum] * invIntegral;
+    if (lightNum >= nL) { free(func); free(cdf); return 6; }
+    float lightNumPdf = func[lightNum] * invIntegral;
     v3 from, dir;
     float lightPdf;
     col3 pcol = emit_photon(&G.al[lightNum], s1, s2, s3, s4, &from, &dir, &lightPdf);
@@ -1543,21 +1535,28 @@ int orc_photon_build(const yk_render_params* P, int32_t* info, uint64_t* rays) {
       const sdmat* M = mat_of(sp.mat);
       unsigned bsdfs = M->flags;
       if (bsdfs & BSDF_DIFFUSE) {
-        if (!causticPhoton) {
-          pmap_push(&g_dmap, sp.P, wi, pcol);
-          g_dmap.paths = (int)curr;
-        }
-        if (pp->final_gather && our_random() < 0.125 && !causticPhoton) {
-          if (nrad == caprad) {
-            caprad = caprad ? 2 * caprad : 1024;
-            rad = (raddata*)realloc(rad, sizeof(raddata) * (size_t)caprad);
+        if (caustic_pass) {
+          if (causticPhoton) {
+            pmap_push(map, sp.P, wi, pcol);
+            map->paths = (int)curr;
           }
-          raddata* r = &rad[nrad++];
-          r->pos = sp.P;
-          r->normal = (vdot(sp.Ng, wi) < 0) ? vneg(sp.N) : sp.N; /* FACE_FORWARD */
-          r->refl = get_reflectivity(M, &sp, BSDF_DIFFUSE | BSDF_GLOSSY | BSDF_REFLECT);
-          r->transm = get_reflectivity(M, &sp, BSDF_DIFFUSE | BSDF_GLOSSY | BSDF_TRANSMIT);
-          r->use = 1;
+        } else {
+          if (!causticPhoton) {
+            pmap_push(map, sp.P, wi, pcol);
+            map->paths = (int)curr;
+          }
+          if (pp->final_gather && our_random() < 0.125 && !causticPhoton) {
+            if (*nrad == *caprad) {
+              *caprad = *caprad ? 2 * *caprad : 1024;
+              *rad = (raddata*)realloc(*rad, sizeof(raddata) * (size_t)*caprad);
+            }
+            raddata* r = &(*rad)[(*nrad)++];
+            r->pos = sp.P;
+            r->normal = (vdot(sp.Ng, wi) < 0) ? vneg(sp.N) : sp.N; /* FACE_FORWARD */
+            r->refl = get_reflectivity(M, &sp, BSDF_DIFFUSE | BSDF_GLOSSY | BSDF_REFLECT);
+            r->transm = get_reflectivity(M, &sp, BSDF_DIFFUSE | BSDF_GLOSSY | BSDF_TRANSMIT);
+            r->use = 1;
+          }
         }
       }
       if (nBounces == pp->bounces) break;
@@ -1576,16 +1575,44 @@ int orc_photon_build(const yk_render_params* P, int32_t* info, uint64_t* rays) {
       ++nBounces;
     }
   }
-  g_photon_rays = g_nclosest - rays0;
   free(func);
   free(cdf);
+  return 0;
+}
+
+/* photonIntegrator_t::preprocess, photonintegr.cc:126-633 (diffuse map,
+ * caustic map, radiance-point elimination, threaded pre-gather of
+ * preGatherWorker_t, radiance map). info: the yk_photon_info integer fields
+ * in order (diffuse_photons, diffuse_paths, caustic_photons, caustic_paths,
+ * rad_candidates, radiance_photons, seed_out); *rays = intersect calls. */
+int orc_photon_build(const yk_render_params* P, int32_t* info, uint64_t* rays) {
+  const yk_photon_params* pp = &P->photon;
+  if (!pm_supported()) return 4;
+  if (pp->photons <= 0 || pp->search <= 0 || G.nlights <= 0) return 1;
+  g_pm_ready = 0;
+  g_dmap.n = g_rmap.n = g_cmap.n = 0;
+  g_dmap.paths = g_rmap.paths = g_cmap.paths = 0;
+  g_myseed = pp->seed;
+  uint64_t rays0 = g_nclosest;
+  raddata* rad = NULL;
+  int nrad = 0, caprad = 0;
+  int rc = shoot_photons(pp, 0, (unsigned)pp->photons, &g_dmap, &rad, &nrad, &caprad);
+  /* caustic pass: every light shoots caustic photons (light_t::shootsCausticP
+   * defaults to true); photons become caustic only after a specular sample */
+  int any_specular = 0; /* without a SPECULAR component no photon becomes caustic: the pass stores nothing */
+  for (int m = 0; m < G.nmats; ++m) any_specular |= (g_sd[m].flags & BSDF_SPECULAR) != 0;
+  if (!rc && pp->caustic_photons > 0 && any_specular)
+    rc = shoot_photons(pp, 1, (unsigned)pp->caustic_photons, &g_cmap, NULL, NULL, NULL);
+  if (rc) { free(rad); return rc; }
+  g_photon_rays = g_nclosest - rays0;
   info[0] = g_dmap.n;
   info[1] = g_dmap.paths;
-  info[2] = 0;
-  info[3] = 0;
+  info[2] = g_cmap.n;
+  info[3] = g_cmap.paths;
   info[4] = nrad;
   if (g_dmap.n < 50) { free(rad); return 2; } /* "Too few diffuse photons" */
   pt_build(&g_dmap.tree, &g_dmap.ph[0].pos.x, (int)(sizeof(photon) / sizeof(float)), g_dmap.n);
+  if (g_cmap.n > 0) pt_build(&g_cmap.tree, &g_cmap.ph[0].pos.x, (int)(sizeof(photon) / sizeof(float)), g_cmap.n);
   if (pp->final_gather) {
     /* remove too close radiance points (photonintegr.cc:551-566) */
     ptree rt = {0};
@@ -1634,9 +1661,9 @@ int orc_photon_build(const yk_render_params* P, int32_t* info, uint64_t* rays) {
   return 0;
 }
 
-/* which: 0 diffuse, 1 caustic (always empty here), 2 radiance; 9 floats per photon */
+/* which: 0 diffuse, 1 caustic, 2 radiance; 9 floats per photon */
 int orc_photon_export(int32_t which, float* out, int32_t cap) {
-  const pmap* m = which == 0 ? &g_dmap : (which == 2 ? &g_rmap : NULL);
+  const pmap* m = which == 0 ? &g_dmap : (which == 2 ? &g_rmap : &g_cmap);
   int n = m ? m->n : 0;
   for (int i = 0; i < n && i < cap; ++i) {
     const photon* p = &m->ph[i];
@@ -1731,6 +1758,42 @@ static col3 final_gathering(rstate* st, const yk_render_params* P, const surfpt*
   return C(pathCol.r / ns, pathCol.g / ns, pathCol.b / ns);
 }
 
+/* mcIntegrator_t::estimateCausticPhotons, mcintegrator.cc:384-419; kernel(),
+ * sample_utils.h:27-31 */
+static col3 estimate_caustic(const yk_render_params* P, const surfpt* sp, v3 wo) {
+  const yk_photon_params* pp = &P->photon;
+  if (g_cmap.n == 0) return C(0, 0, 0); /* !causticMap.ready() */
+  int K = pp->caustic_mix;
+  found* gathered = (found*)malloc(sizeof(found) * (size_t)(K > 0 ? K : 1));
+  float gRadiusSquare = pp->caustic_radius * pp->caustic_radius;
+  int ng = pmap_gather(&g_cmap, sp->P, gathered, K, &gRadiusSquare);
+  gRadiusSquare = 1.f / gRadiusSquare;
+  col3 sum = C(0, 0, 0);
+  if (ng > 0) {
+    const sdmat* M = mat_of(sp->mat);
+    for (int i = 0; i < ng; ++i) {
+      const photon* ph = &g_cmap.ph[gathered[i].idx];
+      col3 surf = sd_eval(M, sp, wo, ph->dir, BSDF_ALL);
+      float s = 1.f - gathered[i].d2 * gRadiusSquare;
+      float k = (float)(((double)(3.f * gRadiusSquare) * M_1_PI_D) * (double)s * (double)s);
+      sum = cadd(sum, cmul(C(surf.r * k, surf.g * k, surf.b * k), ph->c));
+    }
+    float inv = 1.f / (float)g_cmap.paths;
+    sum = C(sum.r * inv, sum.g * inv, sum.b * inv);
+  }
+  free(gathered);
+  return sum;
+}
+
+/* shinyDiffuseMat_t::getAlpha, shinydiffuse.cc:457-469 */
+static float sd_get_alpha(const sdmat* M, const surfpt* sp, v3 wo) {
+  if (!M->is_transparent) return 1.f;
+  v3 N = (vdot(sp->Ng, wo) < 0) ? vneg(sp->N) : sp->N;
+  float Kr = sd_fresnel(M, wo, N);
+  float refl = (1.f - M->comp[0] * Kr) * M->comp[1];
+  return 1.f - refl;
+}
+
 /* photonIntegrator_t::integrate, photonintegr.cc:792-882 */
 static rgba pm_integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir, float tmin, float tmax) {
   const yk_photon_params* pp = &P->photon;
@@ -1779,9 +1842,12 @@ static rgba pm_integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir,
         free(gathered);
       }
     }
-    /* estimateCausticPhotons: the caustic map is empty (not ready) -> 0 */
+    if (bsdfs & BSDF_DIFFUSE) col = cadd(col, estimate_caustic(P, &sp, wo));
     recursive_raytrace(st, P, &sp, bsdfs, wo, &col, &alpha);
-    alpha = 1.0f; /* bg_transp_refract: getAlpha() = 1 for non-transparent materials */
+    { /* transpRefractedBackground (bg_transp_refract, default on) */
+      float m_alpha = sd_get_alpha(M, &sp, wo);
+      alpha = m_alpha + (1.f - m_alpha) * alpha;
+    }
   } else if (G.has_bg) {
     col = cadd(col, G.bg);
   }

@@ -17,7 +17,7 @@ import pytest
 from core_amd import _abi as A
 from core_amd.scene import probe_scene
 from oracle.oracle import Oracle
-from tests.scenes import photon_scene
+from tests.scenes import photon_scene, specular
 
 pytestmark = pytest.mark.gpu
 
@@ -31,6 +31,8 @@ def scene(name, resx, resy):
             s, p = probe_scene("bumpy", resx, resy, 120, 61)
         elif name == "cornell":
             s, p = probe_scene("cornell_pt", resx, resy)
+        elif name.startswith("spec"):  # mirror / glass / translucent spheres: caustic map + recursion
+            s, p = specular(resx, resy, "cornell_pt", raydepth=3, caustic=name == "spec_bg")
         else:
             s, p = photon_scene(resx, resy, name)
         _SCENES[key] = (s, p, Oracle(s))
@@ -60,6 +62,9 @@ CASES = [
     ("point", {"fg_min_pathlen": 0.5}),
     ("smooth_inst", {}),
     ("bumpy", {"photons": 30000}),
+    ("spec", {"caustic_photons": 20000, "caustic_radius": 0.1, "caustic_mix": 20}),
+    ("spec", {"caustic_photons": 20000, "caustic_radius": 0.1, "final_gather": 0, "fg_min_pathlen": 0.5}),
+    ("spec_bg", {"caustic_photons": 30000, "caustic_radius": 0.08, "fg_min_pathlen": 0.6, "fg_bounces": 3}),
 ]
 
 
@@ -81,7 +86,8 @@ def test_photon_maps_and_render_bit_exact(gpu_device, case):
     assert info.radiance_photons == info_o["radiance_photons"]
     assert info.seed_out == info_o["seed_out"]
     assert info.photon_rays == info_o["photon_rays"]
-    for which in (A.YK_PHOTON_MAP_DIFFUSE, A.YK_PHOTON_MAP_RADIANCE):
+    assert info.caustic_photons == info_o["caustic_photons"] and info.caustic_paths == info_o["caustic_paths"]
+    for which in (A.YK_PHOTON_MAP_DIFFUSE, A.YK_PHOTON_MAP_CAUSTIC, A.YK_PHOTON_MAP_RADIANCE):
         g, o = gpu_device.photon_map(which), orc.photon_map(which)
         assert g.shape == o.shape, which
         bad = (g.view(np.uint32) != o.view(np.uint32)).any(axis=1)

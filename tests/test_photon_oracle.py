@@ -120,3 +120,16 @@ def test_photon_render_after_preprocess():
     rgba, _, cnt = orc.render(_pm(p, photons=3000, fg_samples=2))
     # camera rays + gather segments; finite, non-negative radiance
     assert cnt["closest"] > 16 * 16 and np.isfinite(rgba).all() and (rgba >= 0).all()
+
+
+def test_caustic_map_only_with_specular_materials():
+    from tests.scenes import specular
+    s, p = specular(16, 16, "cornell_pt", raydepth=3)
+    orc = O.Oracle(s)
+    a = orc.photon_build(_pm(p, photons=4000, caustic_photons=6000))
+    assert a["caustic_photons"] > 0 and a["caustic_paths"] < 6000
+    cm = orc.photon_map(1)
+    assert cm.shape == (a["caustic_photons"], 9) and (cm[:, 6:9] >= 0).all()
+    s2, p2 = probe_scene("cornell_pt", 16, 16)
+    b = O.Oracle(s2).photon_build(_pm(p2, photons=4000, caustic_photons=6000))
+    assert b["caustic_photons"] == 0
