@@ -68,6 +68,9 @@ struct DLight {  // areaLight_t members after its constructor (arealight.cc:30-4
   float pos[3], dir[3], radius;  // pointLight_t / directionalLight_t members
   int infinite;
   float normal[3], du[3], dv[3];  // areaLight_t emitPhoton frame: normal = -fnormal, du = |toX|, dv = normal ^ du
+  // directionalLight_t after init(scene) (directional.cc:52-75): photon disk
+  // centre / radius (infinite: scene-bound centre and world radius), createCS frame
+  float epos[3], edu[3], edv[3], eradius, wradius;
 };
 
 struct DCam {  // perspectiveCam_t after camera_t ctor + setAxis
@@ -2063,6 +2066,36 @@ DLight make_dirac_light(const yk_dirac_light_state& L) {
   return D;
 }
 
+// directionalLight_t ctor createCS(direction, du, dv) + init(scene)
+// (directional.cc:52-75) -- host IEEE arithmetic, -ffp-contract=off
+void directional_photon_frame(DLight& D, const float* bound) {
+  const float* N = D.dir;
+  if (N[0] == 0.f && N[1] == 0.f) {  // createCS, vector3d.h:316-334
+    D.edu[0] = N[2] < 0.f ? -1.f : 1.f;
+    D.edu[1] = 0.f;
+    D.edu[2] = 0.f;
+    D.edv[0] = 0.f;
+    D.edv[1] = 1.f;
+    D.edv[2] = 0.f;
+  } else {
+    const float d = 1.0f / std::sqrt(N[1] * N[1] + N[0] * N[0]);
+    D.edu[0] = N[1] * d;
+    D.edu[1] = -N[0] * d;
+    D.edu[2] = 0.f;
+    D.edv[0] = N[1] * D.edu[2] - N[2] * D.edu[1];
+    D.edv[1] = N[2] * D.edu[0] - N[0] * D.edu[2];
+    D.edv[2] = N[0] * D.edu[1] - N[1] * D.edu[0];
+  }
+  const float dx = bound[3] - bound[0], dy = bound[4] - bound[1], dz = bound[5] - bound[2];
+  D.wradius = (float)(0.5 * (double)std::sqrt(dx * dx + dy * dy + dz * dz));
+  for (int k = 0; k < 3; ++k) D.epos[k] = D.pos[k];
+  D.eradius = D.radius;
+  if (D.infinite) {
+    for (int k = 0; k < 3; ++k) D.epos[k] = 0.5f * (bound[k] + bound[3 + k]);
+    D.eradius = D.wradius;
+  }
+}
+
 DMat make_mat(const yk_material_state& m) {
   DMat M{};
   M.type = m.type;
@@ -2306,6 +2339,7 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
       lights.push_back(make_light(S.light_states[i]));
     } else {
       lights.push_back(make_dirac_light(S.dirac_states[i]));
+      if (lights.back().type == YK_LIGHT_DIRECTIONAL) directional_photon_frame(lights.back(), S.tree.bound);
     }
     sum_slots += lights.back().nslots;
   }

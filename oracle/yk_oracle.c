@@ -267,6 +267,10 @@ typedef struct {
     v3 pos, dir;
     float radius;
     int infinite;
+    /* directionalLight_t after init(scene) (directional.cc:52-75): photon
+     * emission disk centre, radius, createCS frame, world radius */
+    v3 epos, edu, edv;
+    float eradius, world_radius;
   } * al;
   int has_bg;  /* constBackground_t, textureback.cc:187-218 */
   col3 bg;
@@ -833,6 +837,21 @@ static void lights_setup(void) {
       A->radius = L->radius;
       A->infinite = L->infinite;
       A->samples = 1;
+      if (L->type == YK_LIGHT_DIRECTIONAL) {
+        createCS(A->dir, &A->edu, &A->edv);
+        /* init(): worldRadius = 0.5 * (g - a).length(); infinite lights
+         * centre a disk of that radius on the scene bound */
+        v3 a = V(G.bound[0], G.bound[1], G.bound[2]), g = V(G.bound[3], G.bound[4], G.bound[5]);
+        v3 d = vsub(g, a);
+        A->world_radius = (float)(0.5 * (double)sqrtf(d.x * d.x + d.y * d.y + d.z * d.z));
+        A->epos = A->pos;
+        A->eradius = A->radius;
+        if (A->infinite) {
+          v3 sum = vadd(a, g);
+          A->epos = V(0.5f * sum.x, 0.5f * sum.y, 0.5f * sum.z);
+          A->eradius = A->world_radius;
+        }
+      }
       continue;
     }
     v3 corner = V(L->corner[0], L->corner[1], L->corner[2]);
@@ -1429,10 +1448,39 @@ static int scatter_photon(const sdmat* M, const surfpt* sp, v3 wi, v3* wo, float
   return 0;
 }
 
+/* ShirleyDisk, vector3d.cc:156-182 */
+static void shirley_disk(float r1, float r2, float* u, float* v) {
+  float phi = 0, r = 0, a = 2 * r1 - 1, b = 2 * r2 - 1;
+  if (a > -b) {
+    if (a > b) { r = a; phi = (float)(M_PI_D / 4 * (double)(b / a)); }
+    else { r = b; phi = (float)(M_PI_D / 4 * (double)(2 - a / b)); }
+  } else {
+    if (a < b) { r = -a; phi = (float)(M_PI_D / 4 * (double)(4 + b / a)); }
+    else {
+      r = -b;
+      if (b != 0) phi = (float)(M_PI_D / 4 * (double)(6 - a / b));
+      else phi = 0;
+    }
+  }
+  *u = r * fCos(phi);
+  *v = r * fSin(phi);
+}
+
 /* light_t::emitPhoton: areaLight_t (arealight.cc:98-104), pointLight_t
- * (pointlight.cc:91-97, SampleSphere sample_utils.h:54-72) */
+ * (pointlight.cc:91-97, SampleSphere sample_utils.h:54-72),
+ * directionalLight_t (directional.cc:106-116) */
 static col3 emit_photon(const struct arealight* A, float s1, float s2, float s3, float s4, v3* from, v3* dir,
                         float* ipdf) {
+  if (A->type == YK_LIGHT_DIRECTIONAL) {
+    *dir = vneg(A->dir);
+    float u, v;
+    shirley_disk(s1, s2, &u, &v);
+    v3 off = vadd(vmul(u, A->edu), vmul(v, A->edv));
+    *from = vadd(A->epos, vmul(A->eradius, off));
+    if (A->infinite) *from = vadd(*from, vmul(A->world_radius, A->dir));
+    *ipdf = (float)(M_PI_D * (double)A->eradius * (double)A->eradius);
+    return A->color;
+  }
   if (A->type == YK_LIGHT_POINT) {
     *from = A->pos;
     v3 d;
@@ -1463,17 +1511,17 @@ static float light_energy(const struct arealight* A) {
   if (A->type == YK_LIGHT_POINT) {
     col3 c4 = C(A->color.r * 4.0f, A->color.g * 4.0f, A->color.b * 4.0f);
     e = C(c4.r * (float)M_PI_D, c4.g * (float)M_PI_D, c4.b * (float)M_PI_D);
+  } else if (A->type == YK_LIGHT_DIRECTIONAL) { /* ((color * radius) * radius) * M_PI, directional.cc:33 */
+    float r = A->eradius;
+    col3 c1 = C((A->color.r * r) * r, (A->color.g * r) * r, (A->color.b * r) * r);
+    e = C(c1.r * (float)M_PI_D, c1.g * (float)M_PI_D, c1.b * (float)M_PI_D);
   } else {
     e = C(A->color.r * A->area, A->color.g * A->area, A->color.b * A->area);
   }
   return ((e.r + e.g) + e.b) * 0.333333f;
 }
 
-static int pm_supported(void) {
-  for (int l = 0; l < G.nlights; ++l)
-    if (G.al[l].type == YK_LIGHT_DIRECTIONAL) return 0;
-  return 1;
-}
+static int pm_supported(void) { return 1; }
 
 static uint64_t g_photon_rays;
 

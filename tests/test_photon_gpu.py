@@ -17,7 +17,7 @@ import pytest
 from core_amd import _abi as A
 from core_amd.scene import probe_scene
 from oracle.oracle import Oracle
-from tests.scenes import photon_scene, specular
+from tests.scenes import dirac_lights, photon_scene, specular
 
 pytestmark = pytest.mark.gpu
 
@@ -31,6 +31,8 @@ def scene(name, resx, resy):
             s, p = probe_scene("bumpy", resx, resy, 120, 61)
         elif name == "cornell":
             s, p = probe_scene("cornell_pt", resx, resy)
+        elif name == "dirac":  # area + point + infinite and finite directional lights, background
+            s, p = dirac_lights(resx, resy, "cornell_pt")
         elif name.startswith("spec"):  # mirror / glass / translucent spheres: caustic map + recursion
             s, p = specular(resx, resy, "cornell_pt", raydepth=3, caustic=name == "spec_bg")
         else:
@@ -62,6 +64,7 @@ CASES = [
     ("point", {"fg_min_pathlen": 0.5}),
     ("smooth_inst", {}),
     ("bumpy", {"photons": 30000}),
+    ("dirac", {"fg_min_pathlen": 0.5}),
     ("spec", {"caustic_photons": 20000, "caustic_radius": 0.1, "caustic_mix": 20}),
     ("spec", {"caustic_photons": 20000, "caustic_radius": 0.1, "final_gather": 0, "fg_min_pathlen": 0.5}),
     ("spec_bg", {"caustic_photons": 30000, "caustic_radius": 0.08, "fg_min_pathlen": 0.6, "fg_bounces": 3}),
