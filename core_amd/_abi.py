@@ -89,7 +89,7 @@ class yk_render_params(C.Structure):
                 ("aa_samples", C.c_int32), ("aa_passes", C.c_int32), ("filter", C.c_int32),
                 ("aa_pixelwidth", C.c_float), ("tile_size", C.c_int32),
                 ("transp_background", C.c_int32), ("aa_inc_samples", C.c_int32), ("aa_threshold", C.c_float),
-                ("photon", yk_photon_params)]
+                ("photon", yk_photon_params), ("transp_shadows", C.c_int32), ("shadow_depth", C.c_int32)]
 
     def copy(self):
         p = yk_render_params()
@@ -167,6 +167,7 @@ SIGNATURES = {
     "yk_device_stream": (P, [P]),
     "yk_trace_closest": (C.c_int, [P, P, i64, P, C.POINTER(yk_stats)]),
     "yk_trace_shadow": (C.c_int, [P, P, i64, P, C.POINTER(yk_stats)]),
+    "yk_trace_shadow_filtered": (C.c_int, [P, P, i64, P, P, i32, C.POINTER(yk_stats)]),
     "yk_render_shard": (C.c_int, [P, C.POINTER(yk_render_params), i32, i32, P, C.POINTER(yk_stats)]),
     "yk_film_resolve": (C.c_int, [P, C.POINTER(yk_render_params), P, P]),
     "yk_render_film": (C.c_int, [P, C.POINTER(yk_render_params), i32, i32, fp, C.POINTER(yk_stats)]),

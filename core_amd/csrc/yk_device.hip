@@ -97,6 +97,11 @@ struct DScene {
 
 __device__ __forceinline__ v3 ld3(const float* p) { return V3(p[0], p[1], p[2]); }
 
+struct SurfPt {
+  v3 P, N, Ng, NU, NV;
+  int mat;
+};
+
 // ============================================================ traversal
 
 // bound_t::cross (Smits), compiled form: ((a1-a0)-p)*inv evaluates as (a1-from)*inv
@@ -169,6 +174,11 @@ struct Trav {
   int node, sp;
   float Z, b1, b2;
   int prim;
+  // transparent shadows (IntersectTS): filter colour, transparent surfaces
+  // crossed, and the prims already filtered (std::set in the reference)
+  c3 filt;
+  int tdepth, nfilt, ts_max;
+  int filtered[9];
 };
 
 struct __attribute__((aligned(8))) NodePair {
@@ -190,7 +200,7 @@ __device__ __forceinline__ void exit_pb(Trav& st) {
 
 // scene_t::intersect (scene.cc:852-879) / isShadowed (scene.cc:881-902)
 // setup + tree bound test; false = miss.
-template <bool CLOSEST>
+template <bool CLOSEST, bool TS = false>
 __device__ __forceinline__ bool trav_begin(const DScene& S, Trav& st, const yk_ray& r) {
   st.d = V3(r.dir[0], r.dir[1], r.dir[2]);
   if (CLOSEST) {
@@ -199,8 +209,14 @@ __device__ __forceinline__ bool trav_begin(const DScene& S, Trav& st, const yk_r
     st.dist = (r.tmax < 0.f) ? INFINITY : r.tmax;
   } else {
     st.o = V3(r.from[0] + r.tmin * st.d.x, r.from[1] + r.tmin * st.d.y, r.from[2] + r.tmin * st.d.z);
-    st.tmin = 0.f;
+    // IntersectS accepts t >= 0; IntersectTS keeps the ray's tmin (kdtree.cc:1061)
+    st.tmin = TS ? r.tmin : 0.f;
     st.dist = (r.tmax < 0.f) ? INFINITY : r.tmax - 2.0f * r.tmin;
+  }
+  if (TS) {
+    st.filt = C3(1.f, 1.f, 1.f);
+    st.tdepth = 0;
+    st.nfilt = 0;
   }
   st.Z = st.dist;
   st.prim = -1;
@@ -228,10 +244,39 @@ __device__ __forceinline__ bool trav_begin(const DScene& S, Trav& st, const yk_r
 // (The reference's "exit == split" branch follows "exit <= split" and is
 // never taken, NaN included.)
 // Triangle test of one leaf entry; true when an any-hit query is done.
-template <bool CLOSEST>
-__device__ __forceinline__ bool leaf_test(Trav& st, uint32_t p, float4 A, float4 E1, float4 E2, bool& occluded) {
+__device__ __forceinline__ c3 mat_transparency(const DMat& M, const SurfPt& sp, v3 wo);
+__device__ __forceinline__ SurfPt make_surface(const DScene& S, v3 from, v3 dir, const yk_hit& h);
+
+template <bool CLOSEST, bool TS = false>
+__device__ __forceinline__ bool leaf_test(const DScene& S, Trav& st, uint32_t p, float4 A, float4 E1, float4 E2,
+                                          bool& occluded) {
   float th, u, v;
   if (mt_intersect(V3(A.x, A.y, A.z), V3(E1.x, E1.y, E1.z), V3(E2.x, E2.y, E2.z), st.o, st.d, th, u, v)) {
+    if (TS) {  // IntersectTS leaf body, kdtree.cc:1054-1100
+      if (!(th < st.dist && th >= st.tmin)) return false;
+      const int mat = __float_as_int(S.ng[p].w) & (kSmoothBit - 1);
+      const DMat& M = c_mats[mat];
+      if (!(M.flags & BSDF_FILTER)) {  // !isTransparent(): opaque occluder
+        occluded = true;
+        return true;
+      }
+      bool seen = false;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) seen |= (k < st.nfilt) && st.filtered[k] == (int)p;
+      if (seen) return false;  // filtered.insert(mp).second == false
+#pragma unroll
+      for (int k = 0; k < 9; ++k)
+        if (k == st.nfilt) st.filtered[k] = (int)p;
+      st.nfilt++;
+      if (st.tdepth >= st.ts_max) {
+        occluded = true;
+        return true;
+      }
+      const SurfPt sp = make_surface(S, st.o, st.d, yk_hit{(int)p, th, u, v});
+      st.filt = cmul(st.filt, mat_transparency(M, sp, st.d));
+      st.tdepth++;
+      return false;
+    }
     if (CLOSEST) {
       if (th < st.Z && th >= st.tmin) {
         st.Z = th;
@@ -251,7 +296,7 @@ __device__ __forceinline__ bool leaf_test(Trav& st, uint32_t p, float4 A, float4
 // index and vertices are loaded while the current one is tested). Used for
 // scenes with crowded leaves (hair: ~40 references per leaf), where the plain
 // loop pays two dependent memory round trips per triangle.
-template <bool CLOSEST, bool PIPE>
+template <bool CLOSEST, bool PIPE, bool TS = false>
 __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneStack& stk, unsigned& nnodes,
                                           unsigned& ntris, bool& occluded) {
   if (st.dist < st.en_t) return true;
@@ -304,7 +349,7 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
       // load past the det test: a second dependent round trip per triangle)
       asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
                    "+v"(E2.y), "+v"(E2.z));
-      if (leaf_test<CLOSEST>(st, p, A, E1, E2, occluded)) return true;
+      if (leaf_test<CLOSEST, TS>(S, st, p, A, E1, E2, occluded)) return true;
     }
   } else if (n > 0) {
     uint32_t p = (n == 1) ? w0 : S.leaf[w0];
@@ -322,7 +367,7 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
       asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
                    "+v"(E2.y), "+v"(E2.z));
       ntris++;
-      if (leaf_test<CLOSEST>(st, p, A, E1, E2, occluded)) return true;
+      if (leaf_test<CLOSEST, TS>(S, st, p, A, E1, E2, occluded)) return true;
       A = An;
       E1 = E1n;
       E2 = E2n;
@@ -373,11 +418,12 @@ struct RayCount {
   }
 };
 
-template <bool CLOSEST, int NSEG, bool PIPE>
+template <bool CLOSEST, int NSEG, bool PIPE, bool TS = false>
 __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx,
                                            RayCount rc, yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
                                            unsigned long long* __restrict__ work, unsigned long long* __restrict__ ctr,
-                                           uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
+                                           uint2* __restrict__ ovf, int ovf_depth, int refill_min,
+                                           float* __restrict__ tsf = nullptr, int ts_depth = 0) {
   __shared__ uint2 lds[kStackLds * 64];
   const int lane = threadIdx.x;
   const long long n = __builtin_amdgcn_readfirstlane((int)rc.get());
@@ -435,12 +481,18 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
         } else {
           const int r = idx ? (int)idx[q] : (int)q;
           const yk_ray ray = rays[r];
-          if (trav_begin<CLOSEST>(S, st, ray)) {
+          if (TS) st.ts_max = ts_depth;
+          if (trav_begin<CLOSEST, TS>(S, st, ray)) {
             rid = r;
           } else if (CLOSEST) {
             hits[r] = yk_hit{-1, 0.f, 0.f, 0.f};
           } else {
             occl[r] = 0;
+            if (TS) {
+              tsf[3 * (size_t)r] = 1.f;
+              tsf[3 * (size_t)r + 1] = 1.f;
+              tsf[3 * (size_t)r + 2] = 1.f;
+            }
           }
         }
       }
@@ -461,7 +513,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
     const bool runaway = ++iters > (1u << 30);
     if (rid >= 0) {
       bool occ = false;
-      bool done = trav_step<CLOSEST, PIPE>(S, st, stk, nnodes, ntris, occ);
+      bool done = trav_step<CLOSEST, PIPE, TS>(S, st, stk, nnodes, ntris, occ);
       if (runaway) {
         st.prim = -2;
         done = true;
@@ -475,6 +527,11 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
           hits[rid] = (st.prim >= 0) ? yk_hit{st.prim, st.Z, st.b1, st.b2} : yk_hit{-1, 0.f, 0.f, 0.f};
         } else {
           occl[rid] = occ ? 1 : 0;
+          if (TS) {
+            tsf[3 * (size_t)rid] = st.filt.r;
+            tsf[3 * (size_t)rid + 1] = st.filt.g;
+            tsf[3 * (size_t)rid + 2] = st.filt.b;
+          }
         }
         rid = -1;
       }
@@ -539,13 +596,18 @@ k_trace_shadow_lp(DScene S, const yk_ray* __restrict__ rays, const unsigned* __r
                   unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
   trace_body<false, 1, true>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
+// transparent shadows (scene_t::isShadowed(state, ray, maxDepth, filt),
+// scene.cc:904-928 -> IntersectTS): occlusion + filter colour per ray
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_LP_WAVES)))
+k_trace_shadow_ts(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+                  uint8_t* __restrict__ occl, float* __restrict__ tsf, int ts_depth, unsigned long long* __restrict__ work,
+                  unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
+  trace_body<false, 1, false, true>(S, rays, idx, n, nullptr, occl, work, ctr, ovf, ovf_depth, refill_min, tsf,
+                                    ts_depth);
+}
 
 // ============================================================ shading
 
-struct SurfPt {
-  v3 P, N, Ng, NU, NV;
-  int mat;
-};
 
 // scene_t::intersect tail + triangle_t::getSurface (flat shading subset)
 __device__ __forceinline__ SurfPt make_surface(const DScene& S, v3 from, v3 dir, const yk_hit& h) {
@@ -761,6 +823,18 @@ __device__ __forceinline__ void mat_specular(const DMat& M, const SurfPt& sp, v3
   }
 }
 
+// shinyDiffuseMat_t::getTransparency, shinydiffuse.cc:435-455 (only called on
+// transparent materials): accum = 1 - Kr*mirror; accum *= transparency*accum;
+// accum * (filter*diffuse + (1 - filter))
+__device__ __forceinline__ c3 mat_transparency(const DMat& M, const SurfPt& sp, v3 wo) {
+  float accum = 1.f;
+  const float Kr = mat_fresnel(M, wo, face_forward(sp.Ng, sp.N, wo));
+  if (M.flags & BSDF_SPECULAR) accum = 1.f - Kr * M.comp[0];
+  accum *= M.comp[1] * accum;
+  const float t = 1.f - M.tfilter;
+  return C3(accum * (M.tfilter * M.col[0] + t), accum * (M.tfilter * M.col[1] + t), accum * (M.tfilter * M.col[2] + t));
+}
+
 // emit: shinyDiffuseMat_t::emit (shinydiffuse.cc:251-257), lightMat_t::emit (simple.cc:54-61)
 __device__ __forceinline__ c3 mat_emit(const DMat& M, const SurfPt& sp, v3 wo, bool includeLights) {
   if (M.type == YK_MAT_LIGHT) {
@@ -906,6 +980,11 @@ struct Batch {
   uint8_t* incl;        // state.includeLights after the entry's path loop
   uint8_t* caus;        // caustic flag of the current path segment
   float* emit0;         // 3 floats: emission at the entry's hit, added at the fold
+  // transparent shadows (mcIntegrator_t::trShad): the light colour is
+  // filtered by the shadow ray before the products, so slots keep the parts
+  int ts;
+  float* s_filt;        // 3 per slot: filter colour of the shadow ray (IntersectTS)
+  float* sl_aux;        // 4 per slot: scalar factors (and the Dirac light colour)
 };
 
 struct RenderConst {
@@ -1011,6 +1090,9 @@ __device__ __forceinline__ void put_slot(const Batch& B, long long slot, uint8_t
   B.sl_contrib[3 * slot + 1] = v.g;
   B.sl_contrib[3 * slot + 2] = v.b;
 }
+__device__ __forceinline__ void put_aux(const Batch& B, long long slot, float a, float b, float c, float d) {
+  *reinterpret_cast<float4*>(B.sl_aux + 4 * slot) = make_float4(a, b, c, d);
+}
 
 // mcIntegrator_t::doLightEstimation (area light), mcintegrator.cc:73-195, split
 // at its isShadowed calls: every shadow ray it would trace is written to its
@@ -1035,6 +1117,11 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
     if (k0 < 64) traced |= 1ull << k0;
     const c3 surf = mat_eval(M, sp, wo, ldir);
     const float f = fabsf(vdot(sp.N, ldir));
+    if (B.ts) {  // lcol *= scol first (mcintegrator.cc:94): keep the parts
+      put_slot(B, slot, SL_TRACED | SL_ADDS, surf);
+      put_aux(B, slot, f, lc.r, lc.g, lc.b);
+      return 1;
+    }
     // compiled form of surfCol*lcol*|N.l|*transmitCol (transmitCol = 1):
     // R,G (lcol*surf)*f, B surf*(lcol*f)
     put_slot(B, slot, SL_TRACED | SL_ADDS,
@@ -1069,15 +1156,20 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
     const float mPdf = mat_pdf(M, sp, wo, ldir);
     // compiled form: ((surf*lcol) * (|N.l| * (1/pdf))) [* w]
     const float k = fabsf(vdot(sp.N, ldir)) * (1.0f / lpdf);
-    const c3 sl = cmul(surf, lcol);
-    c3 v;
+    float w = 1.f;
     if (mPdf > 1e-6f) {
       const float l2 = lpdf * lpdf, m2 = mPdf * mPdf;
-      const float w = l2 / (l2 + m2);
-      v = C3((sl.r * k) * w, (sl.g * k) * w, (sl.b * k) * w);
-    } else {
-      v = C3(sl.r * k, sl.g * k, sl.b * k);
+      w = l2 / (l2 + m2);
     }
+    if (B.ts) {  // ls.col *= scol first (mcintegrator.cc:130)
+      put_slot(B, slot, SL_TRACED | SL_ADDS, surf);
+      put_aux(B, slot, k, w, mPdf > 1e-6f ? 1.f : 0.f, 0.f);
+      continue;
+    }
+    const c3 sl = cmul(surf, lcol);
+    c3 v;
+    if (mPdf > 1e-6f) v = C3((sl.r * k) * w, (sl.g * k) * w, (sl.b * k) * w);
+    else v = C3(sl.r * k, sl.g * k, sl.b * k);
     put_slot(B, slot, SL_TRACED | SL_ADDS, v);
   }
   h2 = h2_start;
@@ -1106,6 +1198,11 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
     const float lPdf = 1.f / lightPdf;
     const float l2 = lPdf * lPdf, m2 = spdf * spdf;
     const float w = m2 / (l2 + m2);
+    if (B.ts) {  // lcol *= scol first (mcintegrator.cc:180)
+      put_slot(B, slot, SL_TRACED | SL_ADDS, C3(surf.r * W, surf.g * W, surf.b * W));
+      put_aux(B, slot, w, 0.f, 0.f, 0.f);
+      continue;
+    }
     // compiled form of "surfCol * lcol * w * W": R,G ((surf*W)*lcol)*w, B (surf*W)*(w*lcol)
     put_slot(B, slot, SL_TRACED | SL_ADDS,
              C3(((surf.r * W) * lcol.r) * w, ((surf.g * W) * lcol.g) * w, (surf.b * W) * (w * lcol.b)));
@@ -1242,12 +1339,33 @@ __global__ void __launch_bounds__(256) YK_SHADE_ATTR k_shade_primary(DScene S, B
 
 // Sums light li's unoccluded slot contributions in reference order:
 // (0 + invNS*ccol) + invNS*ccol2 (mcintegrator.cc:116-191); Dirac: 0 + v.
+// Contribution of an unoccluded slot under transparent shadows: the light
+// colour times the shadow ray's filter, then the reference's products.
+__device__ __forceinline__ c3 slot_value_ts(const Batch& B, long long slot, int kind, c3 lcol) {
+  const c3 a = C3(B.sl_contrib[3 * slot], B.sl_contrib[3 * slot + 1], B.sl_contrib[3 * slot + 2]);
+  const float4 x = *reinterpret_cast<const float4*>(B.sl_aux + 4 * slot);
+  const c3 sc = C3(B.s_filt[3 * slot], B.s_filt[3 * slot + 1], B.s_filt[3 * slot + 2]);
+  if (kind == 0) {  // Dirac: R,G (lcol*surf)*f, B surf*(lcol*f)
+    const c3 lc = cmul(C3(x.y, x.z, x.w), sc);
+    return C3((lc.r * a.r) * x.x, (lc.g * a.g) * x.x, a.b * (lc.b * x.x));
+  }
+  const c3 lc = cmul(lcol, sc);
+  if (kind == 1) {  // light sample: ((surf*lcol)*k) [*w]
+    const c3 sl = cmul(a, lc);
+    if (x.z != 0.f) return C3((sl.r * x.x) * x.y, (sl.g * x.x) * x.y, (sl.b * x.x) * x.y);
+    return C3(sl.r * x.x, sl.g * x.x, sl.b * x.x);
+  }
+  // BSDF (MIS) sample, a = surf*W: R,G ((surf*W)*lcol)*w, B (surf*W)*(w*lcol)
+  return C3((a.r * lc.r) * x.x, (a.g * lc.g) * x.x, a.b * (x.x * lc.b));
+}
+
 __device__ __forceinline__ c3 resolve_light(const Batch& B, long long c, int k0, int li) {
   if (c_lights[li].type != YK_LIGHT_AREA) {
     const long long slot = c * B.K + k0;
     c3 col = C3(0.f, 0.f, 0.f);
     if ((B.sl_flags[slot] & SL_ADDS) && !B.s_occl[slot])
-      col = cadd(col, C3(B.sl_contrib[3 * slot], B.sl_contrib[3 * slot + 1], B.sl_contrib[3 * slot + 2]));
+      col = cadd(col, B.ts ? slot_value_ts(B, slot, 0, col)
+                           : C3(B.sl_contrib[3 * slot], B.sl_contrib[3 * slot + 1], B.sl_contrib[3 * slot + 2]));
     return col;
   }
   const int n = c_lights[li].samples;
@@ -1256,7 +1374,8 @@ __device__ __forceinline__ c3 resolve_light(const Batch& B, long long c, int k0,
   for (int i = 0; i < 2 * n; ++i) {
     const long long slot = c * B.K + k0 + i;
     if ((B.sl_flags[slot] & SL_ADDS) && !B.s_occl[slot]) {
-      const c3 v = C3(B.sl_contrib[3 * slot], B.sl_contrib[3 * slot + 1], B.sl_contrib[3 * slot + 2]);
+      const c3 v = B.ts ? slot_value_ts(B, slot, i < n ? 1 : 2, C3(c_lights[li].color[0], c_lights[li].color[1], c_lights[li].color[2]))
+                        : C3(B.sl_contrib[3 * slot], B.sl_contrib[3 * slot + 1], B.sl_contrib[3 * slot + 2]);
       if (i < n) ccol = cadd(ccol, v);
       else ccol2 = cadd(ccol2, v);
     }
@@ -1839,6 +1958,7 @@ struct Pipe {
   DBuf<uint8_t> incl, caus;
   DBuf<float> emit0;
   DBuf<float> fgl, fglen;  // final gathering: lcol (3 per sample) and path length
+  DBuf<float> s_filt, sl_aux;  // transparent shadows
   void create() {
     HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&ev0));
@@ -1859,7 +1979,7 @@ struct Pipe {
     if (ev1) (void)hipEventDestroy(ev1);
     if (stream) (void)hipStreamDestroy(stream);
   }
-  Batch bind(long long maxc, int K, int tiles_per_batch, bool spec = false) {
+  Batch bind(long long maxc, int K, int tiles_per_batch, bool spec = false, bool ts = false) {
     soffs.ensure(maxc);
     col.ensure(3 * maxc);
     alpha.ensure(maxc);
@@ -1916,6 +2036,13 @@ struct Pipe {
     B.samples = samples.p;
     B.sxy = sxy.p;
     B.K = K;
+    if (ts) {
+      s_filt.ensure(3 * maxc * K);
+      sl_aux.ensure(4 * maxc * K);
+      B.ts = 1;
+      B.s_filt = s_filt.p;
+      B.sl_aux = sl_aux.p;
+    }
     if (spec) {
       psample.ensure(maxc);
       incl.ensure(maxc);
@@ -1951,6 +2078,7 @@ struct yk_device {
   bool spec = false;  // some material has SPECULAR|FILTER components: recursion pipeline
   bool crowded_leaves = false;  // mean references per non-empty leaf above kCrowdedLeaf: PIPE leaf loop
   int per_cu_lp[2] = {1, 1};
+  int per_cu_ts = 1;
   // node store of the specular recursion (k_finish_spec / k_spawn / k_fold)
   DBuf<float> nE, nD, nP, nrcol, nalpha, nmalpha;
   DBuf<int> nflags, nchild, noverflow;
@@ -2199,6 +2327,20 @@ void enqueue_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* id
   if (ev1) HIPCHK(hipEventRecord(ev1, P.stream));
 }
 
+// Transparent-shadow any-hit launch (k_trace_shadow_ts): occlusion + filter.
+void enqueue_trace_ts(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* idx, RayCount n, uint8_t* occ,
+                      float* filt, int max_depth, unsigned long long* work, unsigned long long* acc, hipEvent_t ev0,
+                      hipEvent_t ev1) {
+  const long long grid = (long long)d->cus * d->per_cu_ts;
+  const int ovf_depth = std::max(1, stack_depth(d) - kStackLds);
+  P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
+  if (ev0) HIPCHK(hipEventRecord(ev0, P.stream));
+  hipLaunchKernelGGL(k_trace_shadow_ts, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays, idx, n, occ, filt,
+                     max_depth, work, acc, P.ovf.p, ovf_depth, refill_min());
+  HIPCHK(hipGetLastError());
+  if (ev1) HIPCHK(hipEventRecord(ev1, P.stream));
+}
+
 // Ray-query entry points: one launch, synchronised, statistics added to st.
 template <bool CLOSEST>
 void launch_trace(yk_device* d, Pipe& P, const yk_ray* rays, long long n, yk_hit* hits, uint8_t* occ, yk_stats* st) {
@@ -2262,6 +2404,8 @@ int yk_device_open(int32_t ordinal, yk_device** out) {
   d->per_cu_lp[0] = std::max(1, blocks);
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_closest_lp, 64, 0));
   d->per_cu_lp[1] = std::max(1, blocks);
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow_ts, 64, 0));
+  d->per_cu_ts = std::max(1, blocks);
   upload_qmc();
   *out = d;
   return YK_OK;
@@ -2396,6 +2540,39 @@ int yk_trace_shadow(yk_device* d, const yk_ray* d_rays, int64_t n, uint8_t* d_oc
   HIPCHK(hipSetDevice(d->ordinal));
   yk_stats local{};
   launch_trace<false>(d, d->pipe[0], d_rays, n, nullptr, d_occ, st ? st : &local);
+  return YK_OK;
+  YK_GUARD_END
+}
+
+int yk_trace_shadow_filtered(yk_device* d, const yk_ray* d_rays, int64_t n, uint8_t* d_occ, float* d_filter,
+                             int32_t max_depth, yk_stats* st) {
+  if (!d || (n > 0 && (!d_rays || !d_occ || !d_filter)) || n < 0)
+    return set_error(YK_ERR_ARG, "yk_trace_shadow_filtered: bad arguments");
+  if (max_depth < 0 || max_depth > 8) return set_error(YK_ERR_UNSUPPORTED, "max_depth must be in [0, 8]");
+  if (!d->uploaded) return set_error(YK_ERR_STATE, "yk_trace_shadow_filtered: no scene uploaded");
+  if (n <= 0) return YK_OK;
+  if (n > 0x7FFFFFFFll - (1ll << 24)) return set_error(YK_ERR_ARG, "ray batch too large");
+  YK_GUARD_BEGIN
+  HIPCHK(hipSetDevice(d->ordinal));
+  Pipe& P = d->pipe[0];
+  unsigned long long* work = P.counters.p;
+  unsigned long long* acc = P.counters.p + 128;
+  HIPCHK(hipMemsetAsync(work, 0, 136 * sizeof(unsigned long long), P.stream));
+  enqueue_trace_ts(d, P, d_rays, nullptr, RayCount{nullptr, 0, n}, d_occ, d_filter, max_depth, work, acc, P.ev0,
+                   P.ev1);
+  unsigned long long h[4];
+  HIPCHK(hipMemcpyAsync(h, acc, sizeof h, hipMemcpyDeviceToHost, P.stream));
+  HIPCHK(hipStreamSynchronize(P.stream));
+  if (h[2]) return set_error(YK_ERR_INTERNAL, "kd-tree traversal watchdog fired");
+  if (st) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, P.ev0, P.ev1));
+    st->shadow_rays += (uint64_t)n;
+    st->shadow_nodes += h[0];
+    st->shadow_tris += h[1];
+    st->ms_shadow += ms;
+    st->shadow_launches++;
+  }
   return YK_OK;
   YK_GUARD_END
 }
@@ -2536,6 +2713,10 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   R.nsub = p->integrator == YK_INTEGRATOR_PATH ? std::max(1, p->path_samples) : 1;
   R.pm_fg = (pm && p->photon.final_gather && !p->photon.show_map) ? 1 : 0;
   R.pm_showmap = (pm && p->photon.show_map) ? 1 : 0;
+  // transparent shadows: the device keeps the filtered-prim set of a shadow
+  // ray in 9 registers, so at most 8 transparent surfaces (defaults 4-5)
+  if (p->transp_shadows && (p->shadow_depth < 0 || p->shadow_depth > 8))
+    return set_error(YK_ERR_UNSUPPORTED, "shadowDepth must be in [0, 8] with transpShad");
   if (R.pm_fg) R.nsub = std::max(1, p->photon.fg_samples);  // nSampl = max(1, nPaths / rayDivision)
   const PMConst PMC = pm ? pm_const(d, p->photon) : PMConst{};
   R.bounces = p->bounces;
@@ -2656,7 +2837,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     const int nb_here = (nbatch - pi + npipes - 1) / npipes;
     P.words.ensure((size_t)(8 + (d->spec ? 0 : words_per_batch * nb_here)));
     HIPCHK(hipMemsetAsync(P.words.p, 0, P.words.n * sizeof(unsigned long long), P.stream));
-    Bp[pi] = P.bind(maxc, K, tiles_per_batch, R.ps != 0);
+    Bp[pi] = P.bind(maxc, K, tiles_per_batch, R.ps != 0, p->transp_shadows != 0);
     if (R.pm_fg) {
       P.fgl.ensure(3 * maxc);
       P.fglen.ensure(maxc);
@@ -2708,6 +2889,8 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
       timed.push_back(Timed{pi, evn[pi], closest});
       evn[pi] += 2;
       if (closest) enqueue_trace<true>(d, P, rays, idx, n, hits, occ, work, P.words.p, e0, e1);
+      else if (B.ts)  // transparent shadows: IntersectTS, filter colour into the slot
+        enqueue_trace_ts(d, P, rays, idx, n, occ, B.s_filt, p->shadow_depth, work, P.words.p + 4, e0, e1);
       else enqueue_trace<false>(d, P, rays, idx, n, hits, occ, work, P.words.p + 4, e0, e1);
     };
     // photonIntegrator_t::integrate after the direct light: show_map /

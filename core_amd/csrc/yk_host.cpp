@@ -343,6 +343,8 @@ void yk_render_params_default(yk_render_params* p) {
   p->transp_background = 1;
   p->aa_inc_samples = 0;  // = aa_samples
   p->aa_threshold = 0.05f;
+  p->transp_shadows = 0;  // "transpShad"
+  p->shadow_depth = 5;    // "shadowDepth" (pathtracer.cc:338, photonintegr.cc:889)
   // photonIntegrator_t::factory (photonintegr.cc:884-960)
   yk_photon_params& q = p->photon;
   q.photons = 100000;

@@ -68,6 +68,17 @@ class Device:
         A.check(A.lib().yk_trace_shadow(self._p, _ptr(d_rays), n, _ptr(occ), C.byref(st)))
         return occ
 
+    def trace_shadow_filtered(self, d_rays, max_depth, stats=None):
+        """isShadowed(.., maxDepth, filt): (occluded uint8 tensor, filter (n,3) float32 tensor)"""
+        n = d_rays.shape[0]
+        occ = torch.empty((n,), dtype=torch.uint8, device=self.torch_device)
+        filt = torch.empty((n, 3), dtype=torch.float32, device=self.torch_device)
+        torch.cuda.synchronize(self.torch_device)
+        st = stats if stats is not None else A.yk_stats()
+        A.check(A.lib().yk_trace_shadow_filtered(self._p, _ptr(d_rays), n, _ptr(occ), _ptr(filt), max_depth,
+                                                 C.byref(st)))
+        return occ, filt
+
     @staticmethod
     def split_hits(hits):
         h = hits.cpu().numpy()

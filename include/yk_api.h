@@ -123,6 +123,10 @@ typedef struct yk_render_params {
                              aa_samples, scene_t::setAntialiasing scene.cc:736-742)    */
   float aa_threshold;     /* "AA_threshold" (default 0.05): adaptive resampling     */
   yk_photon_params photon; /* integrator == YK_INTEGRATOR_PHOTON                   */
+  int32_t transp_shadows;  /* "transpShad" [0]: shadow rays pass transparent materials,
+                              scene_t::isShadowed(.., maxDepth, filt) / IntersectTS    */
+  int32_t shadow_depth;    /* "shadowDepth" [5]: transparent surfaces a shadow ray may
+                              cross (mcIntegrator_t::sDepth)                           */
 } yk_render_params;
 
 /* one ray, 32 bytes: ray_t (ray.h:26-49) without time */
@@ -294,6 +298,12 @@ void* yk_device_stream(yk_device* d);
  * starts at from + tmin*dir and reaches tmax - 2*tmin (scene.cc:884-889). */
 int yk_trace_closest(yk_device* d, const yk_ray* d_rays, int64_t n, yk_hit* d_hits, yk_stats* st);
 int yk_trace_shadow(yk_device* d, const yk_ray* d_rays, int64_t n, uint8_t* d_occluded, yk_stats* st);
+/* scene_t::isShadowed(state, ray, maxDepth, filt) (scene.cc:904-928) ->
+ * triKdTree_t::IntersectTS (kdtree.cc:953-1108): transparent materials let the
+ * ray through and multiply d_filter (3 floats per ray) by getTransparency;
+ * an opaque hit, or more than max_depth (<= 8) transparent ones, occludes. */
+int yk_trace_shadow_filtered(yk_device* d, const yk_ray* d_rays, int64_t n, uint8_t* d_occluded, float* d_filter,
+                             int32_t max_depth, yk_stats* st);
 
 /* Render the tiles t with (t % nshards == shard) and accumulate the film
  * sums (R,G,B,A,weight per pixel, width*height*5 floats, pixel-major) into

@@ -46,6 +46,7 @@ def lib():
         L.orc_faure.argtypes = [C.c_int, vp]
         L.orc_photon_build.argtypes = [vp, vp, vp]
         L.orc_photon_export.argtypes = [C.c_int32, vp, C.c_int32]
+        L.orc_shadow_ts.argtypes = [vp, C.c_int64, C.c_int32, vp, vp, vp]
         L.orc_point_gather.argtypes = [vp, C.c_int32, vp, C.c_int32, vp, vp, vp]
         L.orc_point_nearest.argtypes = [vp, vp, C.c_int32, vp, vp, C.c_float]
         _lib = L
@@ -134,6 +135,17 @@ class Oracle:
         cnt = np.zeros(2, np.uint64)
         lib().orc_shadow(rays.ctypes.data, n, occ.ctypes.data, cnt.ctypes.data)
         return occ, cnt
+
+    def shadow_ts(self, rays, max_depth):
+        """transparent-shadow queries -> (occluded uint8, filter (n,3) float32, counters)"""
+        self._activate()
+        rays = np.ascontiguousarray(rays, np.float32)
+        n = len(rays)
+        occ = np.zeros(n, np.uint8)
+        filt = np.zeros((n, 3), np.float32)
+        cnt = np.zeros(2, np.uint64)
+        lib().orc_shadow_ts(rays.ctypes.data, n, max_depth, occ.ctypes.data, filt.ctypes.data, cnt.ctypes.data)
+        return occ, filt, cnt
 
     def camera_rays(self, x0, y0, w, h, spp):
         self._activate()

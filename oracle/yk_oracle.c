@@ -476,6 +476,106 @@ static int scene_shadowed(v3 from, v3 dir, float tmin, float tmax) {
   return kd_traverse(f, dir, 0.f, dis, 0, &prim, NULL, NULL, NULL, &g_nodes_s, &g_tris_s);
 }
 
+/* transparent shadows: mcIntegrator_t::trShad / sDepth (set per render) */
+static int g_trshad, g_sdepth;
+
+static col3 sd_get_transparency(int mat, const surfpt* sp, v3 wo);
+static int mat_is_transparent(int mat);
+
+/* triKdTree_t::IntersectTS (kdtree.cc:953-1108) behind scene_t::isShadowed
+ * (state, ray, maxDepth, filt) (scene.cc:904-928): the any-hit descent, but
+ * every leaf prim with tmin <= t < dist is looked at (note: the shifted ray
+ * keeps tmin, unlike IntersectS); an opaque one occludes, a transparent one
+ * not seen before multiplies filt by getTransparency -- or occludes once
+ * maxDepth of them have been crossed. */
+static int scene_shadowed_ts(v3 from0, v3 dir, float tmin, float tmax, int maxDepth, col3* filt) {
+  g_nshadow++;
+  v3 from = vadd(from0, vmul(tmin, dir));
+  float dist = (tmax < 0) ? INFINITY : tmax - 2.0f * tmin;
+  *filt = C(1.0f, 1.0f, 1.0f);
+  float a, b, t, t_hit, b1, b2;
+  if (!bound_cross(from, dir, &a, &b, dist)) return 0;
+  v3 invDir = V(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+  int depth = 0, nfilt = 0;
+  int filtered[64];
+  kdstack stack[KD_MAX_STACK + 2];
+  int currNode = 0, farChild;
+  int enPt = 0;
+  stack[enPt].t = a;
+  stack[enPt].pb = (a >= 0.0f) ? vadd(from, vmul(a, dir)) : from;
+  int exPt = 1;
+  stack[exPt].t = b;
+  stack[exPt].pb = vadd(from, vmul(b, dir));
+  stack[exPt].node = -1;
+  while (currNode != -1) {
+    if (dist < stack[enPt].t) break;
+    g_nodes_s++;
+    while ((G.nodes[2 * currNode + 1] & 3u) != 3u) {
+      int axis = (int)(G.nodes[2 * currNode + 1] & 3u);
+      float splitVal;
+      memcpy(&splitVal, &G.nodes[2 * currNode], 4);
+      int right = (int)(G.nodes[2 * currNode + 1] >> 2);
+      if (vget(stack[enPt].pb, axis) <= splitVal) {
+        if (vget(stack[exPt].pb, axis) <= splitVal) { currNode++; g_nodes_s++; continue; }
+        if (vget(stack[exPt].pb, axis) == splitVal) { currNode = right; g_nodes_s++; continue; }
+        farChild = right;
+        currNode++;
+      } else {
+        if (splitVal < vget(stack[exPt].pb, axis)) { currNode = right; g_nodes_s++; continue; }
+        farChild = currNode + 1;
+        currNode = right;
+      }
+      g_nodes_s++;
+      t = (splitVal - vget(from, axis)) * vget(invDir, axis);
+      int tmp = exPt;
+      exPt++;
+      if (exPt == enPt) exPt++;
+      static const int npAxis[2][3] = {{1, 2, 0}, {2, 0, 1}};
+      int nextAxis = npAxis[0][axis], prevAxis = npAxis[1][axis];
+      stack[exPt].prev = tmp;
+      stack[exPt].t = t;
+      stack[exPt].node = farChild;
+      vset(&stack[exPt].pb, axis, splitVal);
+      vset(&stack[exPt].pb, nextAxis, vget(from, nextAxis) + t * vget(dir, nextAxis));
+      vset(&stack[exPt].pb, prevAxis, vget(from, prevAxis) + t * vget(dir, prevAxis));
+    }
+    uint32_t w0 = G.nodes[2 * currNode], n = G.nodes[2 * currNode + 1] >> 2;
+    for (uint32_t i = 0; i < n; ++i) {
+      int p = (int)(n == 1 ? w0 : G.leaf[w0 + i]);
+      g_tris_s++;
+      if (!tri_intersect(p, from, dir, &t_hit, &b1, &b2)) continue;
+      if (!(t_hit < dist && t_hit >= tmin)) continue;
+      int mat = G.tmat[p];
+      if (!mat_is_transparent(mat)) return 1;
+      int seen = 0;
+      for (int k = 0; k < nfilt; ++k) seen |= filtered[k] == p;
+      if (seen) continue; /* filtered.insert(mp).second == false */
+      filtered[nfilt++] = p;
+      if (depth >= maxDepth) return 1;
+      /* getSurface at h = from + t_hit*dir, then getTransparency(sp, ray.dir) */
+      surfpt sp;
+      sp.P = vadd(from, vmul(t_hit, dir));
+      sp.Ng = G.ng[p];
+      sp.N = sp.Ng;
+      if (G.smooth && G.smooth[p]) {
+        const float* nv = G.vn + 9 * (size_t)p;
+        float b0 = 1.0f - (b1 + b2);
+        sp.N = vnormalize(vadd(vadd(vmul(b0, V(nv[0], nv[1], nv[2])), vmul(b1, V(nv[3], nv[4], nv[5]))),
+                               vmul(b2, V(nv[6], nv[7], nv[8]))));
+      }
+      createCS(sp.N, &sp.NU, &sp.NV);
+      sp.prim = p;
+      sp.mat = mat;
+      *filt = cmul(*filt, sd_get_transparency(mat, &sp, dir));
+      ++depth;
+    }
+    enPt = exPt;
+    currNode = stack[exPt].node;
+    exPt = stack[enPt].prev;
+  }
+  return 0;
+}
+
 /* ------------------------------------------------------------- camera -- */
 
 static void camera_setup(void) {
@@ -792,6 +892,22 @@ static void sd_get_specular(const sdmat* M, const surfpt* sp, v3 wo, int* refl, 
   }
 }
 
+/* material_t::isTransparent (material.h:124), shinyDiffuseMat_t: mIsTransparent */
+static int mat_is_transparent(int mat) { return mat_of(mat)->is_transparent; }
+
+/* shinyDiffuseMat_t::getTransparency, shinydiffuse.cc:435-455 */
+static col3 sd_get_transparency(int mat, const surfpt* sp, v3 wo) {
+  const sdmat* M = mat_of(mat);
+  float accum = 1.f;
+  v3 N = (vdot(sp->Ng, wo) < 0) ? vneg(sp->N) : sp->N;
+  float Kr = sd_fresnel(M, wo, N);
+  if (M->is_mirror) accum = 1.f - Kr * M->comp[0];
+  if (M->is_transparent) accum *= M->comp[1] * accum;
+  col3 tcol = C(M->tfilter * M->diff.r + (1.f - M->tfilter), M->tfilter * M->diff.g + (1.f - M->tfilter),
+                M->tfilter * M->diff.b + (1.f - M->tfilter));
+  return C(accum * tcol.r, accum * tcol.g, accum * tcol.b);
+}
+
 /* emit: shinyDiffuseMat_t::emit (shinydiffuse.cc:251-257), lightMat_t::emit
  * (simple.cc:54-61) */
 static col3 mat_emit(const sdmat* M, const surfpt* sp, v3 wo, int includeLights) {
@@ -970,7 +1086,10 @@ static col3 do_light_estimation(rstate* st, int li, const surfpt* sp, v3 wo, uns
     float ltmax;
     int ok = A->type == YK_LIGHT_POINT ? point_illuminate(A, sp->P, &lcol, &ldir, &ltmax)
                                        : dir_illuminate(A, sp->P, &lcol, &ldir, &ltmax);
-    if (ok && !scene_shadowed(sp->P, ldir, SHADOW_BIAS, ltmax)) {
+    col3 scol;
+    if (ok && !(g_trshad ? scene_shadowed_ts(sp->P, ldir, SHADOW_BIAS, ltmax, g_sdepth, &scol)
+                         : scene_shadowed(sp->P, ldir, SHADOW_BIAS, ltmax))) {
+      if (g_trshad) lcol = cmul(lcol, scol);
       col3 surf = sd_eval(M, sp, wo, ldir, BSDF_ALL);
       float f = fabsf(vdot(sp->N, ldir));
       /* compiled form of surfCol*lcol*|N.l|*transmitCol, transmitCol = 1:
@@ -995,8 +1114,11 @@ static col3 do_light_estimation(rstate* st, int li, const surfpt* sp, v3 wo, uns
     float ltmax, lpdf;
     col3 lcol;
     if (al_illum_sample(A, sp->P, s1, s2, &ldir, &ltmax, &lcol, &lpdf)) {
-      int shadowed = scene_shadowed(sp->P, ldir, SHADOW_BIAS, ltmax);
+      col3 scol;
+      int shadowed = g_trshad ? scene_shadowed_ts(sp->P, ldir, SHADOW_BIAS, ltmax, g_sdepth, &scol)
+                              : scene_shadowed(sp->P, ldir, SHADOW_BIAS, ltmax);
       if (!shadowed && lpdf > 1e-6f) {
+        if (g_trshad) lcol = cmul(lcol, scol); /* ls.col *= scol */
         col3 surf = sd_eval(M, sp, wo, ldir, BSDF_ALL);
         float mPdf = sd_pdf(M, sp, wo, ldir, BSDF_GLOSSY | BSDF_DIFFUSE | BSDF_DISPERSIVE | BSDF_REFLECT | BSDF_TRANSMIT);
         /* compiled form: ((surf*lcol) * (|N.l| * (1/pdf))) [* w] */
@@ -1028,8 +1150,11 @@ static col3 do_light_estimation(rstate* st, int li, const surfpt* sp, v3 wo, uns
     float bt, lightPdf;
     col3 lcol;
     if (spdf > 1e-6f && al_intersect(A, sp->P, bdir, &bt, &lcol, &lightPdf)) {
-      int shadowed = scene_shadowed(sp->P, bdir, MIN_RAYDIST, bt);
+      col3 scol;
+      int shadowed = g_trshad ? scene_shadowed_ts(sp->P, bdir, MIN_RAYDIST, bt, g_sdepth, &scol)
+                              : scene_shadowed(sp->P, bdir, MIN_RAYDIST, bt);
       if (!shadowed && lightPdf > 1e-6f) {
+        if (g_trshad) lcol = cmul(lcol, scol);
         float lPdf = 1.f / lightPdf;
         float l2 = lPdf * lPdf, m2 = spdf * spdf;
         float w = m2 / (l2 + m2);
@@ -2120,6 +2245,23 @@ int orc_shadow(const yk_ray* rays, int64_t n, uint8_t* occ, uint64_t* counters) 
   return 0;
 }
 
+/* batched transparent-shadow queries: scene_t::isShadowed(state, ray, maxDepth, filt) */
+int orc_shadow_ts(const yk_ray* rays, int64_t n, int32_t max_depth, uint8_t* occ, float* filt, uint64_t* counters) {
+  uint64_t n0 = g_nodes_s, t0 = g_tris_s, c0 = g_nshadow;
+  for (int64_t i = 0; i < n; ++i) {
+    const yk_ray* r = &rays[i];
+    col3 f;
+    occ[i] = (uint8_t)scene_shadowed_ts(V(r->from[0], r->from[1], r->from[2]), V(r->dir[0], r->dir[1], r->dir[2]),
+                                        r->tmin, r->tmax, max_depth, &f);
+    filt[3 * i] = f.r;
+    filt[3 * i + 1] = f.g;
+    filt[3 * i + 2] = f.b;
+  }
+  g_nshadow = c0;
+  if (counters) { counters[0] = g_nodes_s - n0; counters[1] = g_tris_s - t0; }
+  return 0;
+}
+
 /* camera rays of pixel (x,y) sample s, as renderTile generates them */
 int orc_camera_rays(int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t spp, yk_ray* out) {
   float d1 = (float)(1.0 / (double)(float)spp);
@@ -2165,7 +2307,10 @@ static int render_tiles(const yk_render_params* P, int shard, int nshards, float
                         uint64_t* counts) {
   if (P->aa_passes < 1) return 4;
   if (P->aa_passes > 1 && nshards != 1) return 4;
-  if (P->integrator == YK_INTEGRATOR_PHOTON && !g_pm_ready) return 3; /* preprocess() not run */ /* nextPass reads the whole film */
+  if (P->integrator == YK_INTEGRATOR_PHOTON && !g_pm_ready) return 3; /* preprocess() not run */
+  if (P->transp_shadows && (P->shadow_depth < 0 || P->shadow_depth > 32)) return 4;
+  g_trshad = P->transp_shadows != 0;
+  g_sdepth = P->shadow_depth; /* nextPass reads the whole film */
   film_t F;
   film_init(&F, P);
   g_nclosest = g_nshadow = g_nodes_c = g_tris_c = g_nodes_s = g_tris_s = 0;

@@ -154,3 +154,32 @@ def photon_scene(resx, resy, kind):
         raise ValueError(kind)
     s.build()
     return s, p
+
+
+def transparent_panes(resx, resy, integrator="cornell_pt", panes=3):
+    """Cornell box with stacked transparent panes under the light, for
+    transparent shadows (transpShad: scene_t::isShadowed(.., maxDepth, filt),
+    IntersectTS kdtree.cc:953-1108). Each pane is one quad split into many
+    triangles, so a shadow ray meets the same prim in several kd leaves (the
+    reference's `filtered` set) and crosses up to `panes` transparent
+    surfaces (shadowDepth)."""
+    s = Scene()
+    p = s.generate(integrator, resx, resy)
+    mats = [s.add_material(color=(0.9, 0.5, 0.2), diffuse_reflect=0.2, transparency=0.8, transmit_filter=0.6),
+            s.add_material(color=(0.3, 0.6, 0.9), diffuse_reflect=0.3, specular_reflect=0.2, transparency=0.7,
+                           transmit_filter=0.8, fresnel_effect=True, ior=1.4)]
+    n = 6
+    for k in range(panes):
+        y = 1.55 - 0.3 * k
+        xs = np.linspace(-0.7 + 0.1 * k, 0.6, n + 1)
+        zs = np.linspace(-0.6, 0.7 - 0.1 * k, n + 1)
+        pts = np.array([(x, y + 0.02 * x, z) for z in zs for x in xs], np.float32)
+        faces = []
+        for j in range(n):
+            for i in range(n):
+                a, b = j * (n + 1) + i, j * (n + 1) + i + 1
+                c, d = a + n + 1, b + n + 1
+                faces += [(a, b, d), (a, d, c)]
+        s.add_mesh(pts, np.asarray(faces, np.int32), mats[k % 2])
+    s.build()
+    return s, p
