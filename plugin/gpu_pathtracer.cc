@@ -335,6 +335,7 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     pm.getParam("raydepth", p.raydepth);
     pm.getParam("path_samples", p.path_samples);
     pm.getParam("bounces", p.bounces);
+    read_shadow_params(pm, p);  // pathtracer.cc:337-353
     bool bg = true;
     pm.getParam("bg_transp", bg);
     p.transp_background = bg;
@@ -347,10 +348,19 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     yk_render_params_default(&p);
     p.integrator = YK_INTEGRATOR_DIRECT;
     pm.getParam("raydepth", p.raydepth);
+    read_shadow_params(pm, p);  // directlight.cc factory
     bool bg = true;
     pm.getParam("bg_transp", bg);
     p.transp_background = bg;
     return new gpuTiledIntegrator_t(p, "DirectLight");
+  }
+  // "transpShad" / "shadowDepth" -> mcIntegrator_t::trShad / sDepth; the
+  // device keeps at most 8 filtered surfaces per shadow ray
+  static void read_shadow_params(paraMap_t& pm, yk_render_params& p) {
+    bool ts = false;
+    pm.getParam("transpShad", ts);
+    p.transp_shadows = ts;
+    pm.getParam("shadowDepth", p.shadow_depth);
   }
   // photonIntegrator_t::factory (photonintegr.cc:884-960): same parameter
   // names and defaults (yk_render_params_default)
@@ -382,7 +392,8 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     pm.getParam("bg_transp", bg);
     bool use_sss = false;
     pm.getParam("useSSS", use_sss);
-    if (transp_shad) { Y_ERROR << "PhotonMap: transparent shadows are not on the GPU path" << yendl; return nullptr; }
+    p.transp_shadows = transp_shad;
+    pm.getParam("shadowDepth", p.shadow_depth);
     if (use_sss) { Y_ERROR << "PhotonMap: SSS photons are not on the GPU path" << yendl; return nullptr; }
     p.raydepth = raydepth;
     p.transp_background = bg;
