@@ -7,6 +7,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch.multiprocessing as mp
 
 
@@ -18,15 +19,28 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, q):
+def _scene(integrator):
+    from core_amd import _abi as A
+    from core_amd.scene import probe_scene
+    s, p = probe_scene("cornell_pt", 48, 40)
+    if integrator == "photon":  # each rank runs preprocess: the maps are deterministic replicas
+        p.integrator = A.YK_INTEGRATOR_PHOTON
+        p.photon.photons = 8000
+        p.photon.fg_samples = 2
+    return s, p
+
+
+def _worker(rank, world, port, q, integrator):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from core_amd.scene import probe_scene
     from oracle.oracle import Oracle
-    s, p = probe_scene("cornell_pt", 48, 40)
-    sums, cnt = Oracle(s).render_shard(p, rank, world)
+    s, p = _scene(integrator)
+    orc = Oracle(s)
+    if integrator == "photon":
+        orc.photon_build(p)
+    sums, cnt = orc.render_shard(p, rank, world)
     film = torch.from_numpy(sums)
     dist.reduce(film, dst=0)
     rays = torch.tensor([cnt["closest"], cnt["shadow"]], dtype=torch.int64)
@@ -37,22 +51,25 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_film_reduce():
+@pytest.mark.parametrize("integrator", ["path", "photon"])
+def test_two_rank_film_reduce(integrator):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, integrator)) for r in range(world)]
     for pr in procs:
         pr.start()
     film, rays = q.get(timeout=240)
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0
-    from core_amd.scene import probe_scene
     from oracle.oracle import Oracle
-    s, p = probe_scene("cornell_pt", 48, 40)
-    _, full, cnt = Oracle(s).render(p)
+    s, p = _scene(integrator)
+    orc = Oracle(s)
+    if integrator == "photon":
+        orc.photon_build(p)
+    _, full, cnt = orc.render(p)
     assert rays[0] == cnt["closest"] and rays[1] == cnt["shadow"]
     assert np.allclose(film, full, rtol=2e-6, atol=1e-6)
     # interior pixels of a tile get contributions from one shard only: exact
