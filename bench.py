@@ -41,8 +41,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scene", default="bumpy", choices=["bumpy", "hair"],
-                    help="bumpy: the 1M-tri headline probe (configs[2]); hair: the C5 10M-tri strand scene")
+    ap.add_argument("--scene", default="bumpy", choices=["bumpy", "hair", "cornell"],
+                    help="bumpy: the 1M-tri headline probe (configs[2]); hair: the C5 10M-tri strand scene; "
+                         "cornell: configs[1] (36 tris, pass --width 1024 --height 1024 --spp 64)")
     ap.add_argument("--strands", type=int, default=200000, help="hair: strands (x50 tris each at 9 points)")
     ap.add_argument("--strand-points", type=int, default=9)
     ap.add_argument("--nu", type=int, default=1000, help="sphere segments (1000x501 -> 1,000,002 tris)")
@@ -78,6 +79,8 @@ def main():
         print(f"[bench] building {args.scene} scene + kd-tree on the host", file=sys.stderr, flush=True)
     if args.scene == "hair":
         scene, p = probe_scene("hair", args.width, args.height, args.strands, args.strand_points)
+    elif args.scene == "cornell":  # BASELINE configs[1]: path_samples 1, bounces 4, raydepth 2
+        scene, p = probe_scene("cornell_pt", args.width, args.height)
     else:
         scene, p = probe_scene("bumpy", args.width, args.height, args.nu, args.nv)
     t_build = time.perf_counter() - t_build
@@ -174,8 +177,9 @@ def main():
         cpu = cpu_baseline(scene, p, args.cpu_seconds)
 
     out = {
-        "metric": ("Mrays/s (primary+shadow), 1M-tri scene" if args.scene == "bumpy" else
-                   "Mrays/s (primary+shadow), 10M-tri hair scene (C5 shape)") +
+        "metric": {"bumpy": "Mrays/s (primary+shadow), 1M-tri scene",
+                   "hair": "Mrays/s (primary+shadow), 10M-tri hair scene (C5 shape)",
+                   "cornell": "Mrays/s (primary+shadow), Cornell box (configs[1])"}[args.scene] +
                   (", photon mapping" if pm_info is not None else ""),
         "value": round(value, 3),
         "unit": "Mrays/s",
@@ -187,14 +191,15 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": (f"synthetic: procedural displaced sphere + floor" if args.scene == "bumpy" else
-                 f"synthetic: {args.strands} curve strands x {args.strand_points} points on a sphere + floor") +
+        "data": {"bumpy": "synthetic: procedural displaced sphere + floor",
+                 "hair": f"synthetic: {args.strands} curve strands x {args.strand_points} points on a sphere + floor",
+                 "cornell": "the reference-fixture Cornell box (tests/golden/gen)"}[args.scene] +
                 f", {info.ntris} tris, kd-tree built on host ({t_build:.1f} s, not timed)",
         "config": {"workload": f"{args.scene} {info.ntris} tris, " +
                                (f"pathtracing bounces {p.bounces}, " if pm_info is None else
                                 f"photonmapping {p.photon.photons} photons, final gather {p.photon.fg_samples} paths "
                                 f"x {p.photon.fg_bounces} bounces, search {p.photon.search}, ") +
-                               f"{p.width}x{p.height}, {p.aa_samples} spp, {info.nlights} area light(s) 1 sample",
+                               f"{p.width}x{p.height}, {p.aa_samples} spp, {info.nlights} area light(s)",
                    "tris": int(info.ntris), "width": p.width, "height": p.height, "spp": p.aa_samples,
                    "parallelism": f"tiles%{world}" if world > 1 else "single",
                    "closest_rays": int(w[0]), "shadow_rays": int(w[1]),
