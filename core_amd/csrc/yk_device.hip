@@ -2095,6 +2095,7 @@ struct yk_device {
   DBuf<float4> dm_pos, dm_dir, dm_col, rm_pos, rm_dir, rm_col, cm_pos, cm_dir, cm_col;
   std::vector<float> dm_host, rm_host, cm_host;  // 9 floats per photon, photon-vector order
   int dm_paths = 0, cm_paths = 0;
+  int rm_depth = 0;  // radiance kd-tree depth (k_fg_hit keeps its lookup stack in LDS up to kLdsPStack)
   std::vector<unsigned> mat_flags;  // bsdfFlags per material
   Pipe pipe[kPipes];
   hipEvent_t gather_ev[kPipes] = {};
@@ -2911,7 +2912,8 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
           const unsigned long long* in_w = qw(isub, it);
           unsigned long long* out_w = qw(isub, it + 1);
           trace(true, Bc.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, Bc.q_hits[qin], nullptr);
-          hipLaunchKernelGGL(k_fg_hit, dim3(grid_for(n)), dim3(256), 0, P.stream, d->S, Bc, Rc, PMC, in_w, it, isub, qin,
+          hipLaunchKernelGGL(d->rm_depth <= kLdsPStack ? k_fg_hit<true> : k_fg_hit<false>, dim3(grid_for(n)), dim3(256), 0,
+                             P.stream, d->S, Bc, Rc, PMC, in_w, it, isub, qin,
                              P.fgl.p, P.fglen.p, out_w);
           HIPCHK(hipGetLastError());
           if (it < p->photon.fg_bounces) trace(false, Bc.s_rays, Bc.s_idx, RayCount{out_w, 0, 0}, nullptr, Bc.s_occl);
