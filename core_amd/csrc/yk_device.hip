@@ -564,6 +564,9 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 #ifndef YK_SHADOW_WAVES
 #define YK_SHADOW_WAVES 7
 #endif
+#ifndef YK_SHADOW_NSEG
+#define YK_SHADOW_NSEG 1
+#endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
 k_trace_closest(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                 yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
@@ -574,7 +577,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHAD
 k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false, 1, false>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+  trace_body<false, YK_SHADOW_NSEG, false>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 // crowded-leaf variants (PIPE leaf loop): one wave fewer per SIMD buys the
 // registers of the prefetched triangle without spilling
