@@ -920,6 +920,14 @@ __device__ __forceinline__ bool dirac_illum(const DLight& L, v3 P, v3& ldir, flo
 
 // ------------------------------------------------------------ queues
 
+// Queue appends: one returning atomic per 256-thread block instead of per
+// wave. Every wave of a launch appends to the same counter word, and the
+// returning atomics serialise on it; measured 1068 -> 1263 Mrays/s (photon
+// mapping, 32 gather launches of 33M threads per batch) and 2008 -> 2038
+// (path tracing).
+#ifndef YK_BLOCK_APPEND
+#define YK_BLOCK_APPEND 1
+#endif
 // Reserves m_s shadow-queue and m_b bounce-queue entries with ONE returning
 // atomic per wave: the counter word holds (bounce count << 32) | shadow
 // count. Whole-wave call; returns each lane's first index in both queues.
@@ -934,9 +942,28 @@ __device__ __forceinline__ void wave_append2(unsigned long long* counter, unsign
     if (lane >= off) incl += ((unsigned long long)hi << 32) | lo;
   }
   const unsigned long long total = shfl_u64(incl, 63);
+#if YK_BLOCK_APPEND
+  // one returning atomic per block: wave totals meet in LDS (all callers
+  // reach this point with whole blocks)
+  __shared__ unsigned long long s_tot[16];
+  __shared__ unsigned long long s_base;
+  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  if (lane == 63) s_tot[w] = total;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int k = 0; k < nw; ++k) t += s_tot[k];
+    s_base = t ? atomicAdd(counter, t) : 0ull;
+  }
+  __syncthreads();
+  unsigned long long base = s_base;
+  for (int k = 0; k < w; ++k) base += s_tot[k];
+  base += incl - m;
+#else
   unsigned long long base = 0;
   if (lane == 63 && total) base = atomicAdd(counter, total);
   base = shfl_u64(base, 63) + incl - m;
+#endif
   base_s = (unsigned)base;
   base_b = (unsigned)(base >> 32);
 }
