@@ -439,7 +439,10 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   // 4 MB L2 keeps it. A wave takes kPoolChunk-ray chunks of its own XCD's
   // segment (one atomic per chunk), then steals from the other segments.
   // Pool bounds are wave-uniform (scalar registers).
-  constexpr unsigned kPoolChunk = 64;
+#ifndef YK_POOL_CHUNK
+#define YK_POOL_CHUNK 64
+#endif
+  constexpr unsigned kPoolChunk = YK_POOL_CHUNK;
   unsigned xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
   constexpr unsigned kAll = (1u << NSEG) - 1u;
@@ -928,6 +931,16 @@ __device__ __forceinline__ bool dirac_illum(const DLight& L, v3 P, v3& ldir, flo
 #ifndef YK_BLOCK_APPEND
 #define YK_BLOCK_APPEND 1
 #endif
+// Block sizes of the kernels that append to ray queues (fewer, larger blocks
+// = fewer returning atomics on the queue word). Measured: path-tracing
+// shading at 1024 threads 2038 -> 2075 Mrays/s; the photon / final-gather
+// kernels best at 512 (1261 -> 1274; 1024: 1240).
+#ifndef YK_SHADE_BLOCK
+#define YK_SHADE_BLOCK 1024
+#endif
+#ifndef YK_APPEND_BLOCK
+#define YK_APPEND_BLOCK 512
+#endif
 // Reserves m_s shadow-queue and m_b bounce-queue entries with ONE returning
 // atomic per wave: the counter word holds (bounce count << 32) | shadow
 // count. Whole-wave call; returns each lane's first index in both queues.
@@ -1286,7 +1299,7 @@ __device__ __forceinline__ yk_ray path_first_segment(const Batch& B, const Rende
 #else
 #define YK_SHADE_ATTR
 #endif
-__global__ void __launch_bounds__(256) YK_SHADE_ATTR k_shade_primary(DScene S, Batch B, RenderConst R, long long nc,
+__global__ void __launch_bounds__(YK_SHADE_BLOCK) YK_SHADE_ATTR k_shade_primary(DScene S, Batch B, RenderConst R, long long nc,
                                                        unsigned long long* __restrict__ qword) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = c < nc;
@@ -1433,7 +1446,7 @@ __global__ void __launch_bounds__(256) k_resolve_primary(Batch B, RenderConst R,
 
 // First segment of sub-paths isub >= 1 (sub-path 0 is fused into
 // k_shade_primary).
-__global__ void __launch_bounds__(256) k_path_start(DScene S, Batch B, RenderConst R, long long nc, int isub,
+__global__ void __launch_bounds__(YK_SHADE_BLOCK) k_path_start(DScene S, Batch B, RenderConst R, long long nc, int isub,
                                                     unsigned long long* __restrict__ qword) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = c < nc;
@@ -1463,7 +1476,7 @@ __global__ void __launch_bounds__(256) k_path_start(DScene S, Batch B, RenderCon
 // (pathtracer.cc:189-298): estimateOneDirectLight shadow rays, emission,
 // and the BSDF sample of the next segment. One thread per live path (entry
 // qi of the input bounce queue, owned by camera sample c).
-__global__ void __launch_bounds__(256) YK_SHADE_ATTR k_shade_bounce(DScene S, Batch B, RenderConst R,
+__global__ void __launch_bounds__(YK_SHADE_BLOCK) YK_SHADE_ATTR k_shade_bounce(DScene S, Batch B, RenderConst R,
                                                       const unsigned long long* __restrict__ qin_word, int depth,
                                                       int isub, int qin, unsigned long long* __restrict__ qword) {
   const long long nq = (long long)(*qin_word >> 32);  // live paths (device-side count)
@@ -2934,7 +2947,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
       // final gathering (photonintegr.cc:637-790): gather path index outermost,
       // pathCol accumulated across paths in the reference's order
       for (int isub = 0; isub < (R.pm_fg ? nsub : 0); ++isub) {
-        hipLaunchKernelGGL(k_fg_start, dim3(grid_for(n)), dim3(256), 0, P.stream, d->S, Bc, Rc, n, isub, P.fgl.p,
+        hipLaunchKernelGGL(k_fg_start, dim3(grid_for(n, YK_APPEND_BLOCK)), dim3(YK_APPEND_BLOCK), 0, P.stream, d->S, Bc, Rc, n, isub, P.fgl.p,
                            qw(isub, 0));
         HIPCHK(hipGetLastError());
         int qin = 1;
@@ -2942,7 +2955,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
           const unsigned long long* in_w = qw(isub, it);
           unsigned long long* out_w = qw(isub, it + 1);
           trace(true, Bc.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, Bc.q_hits[qin], nullptr);
-          hipLaunchKernelGGL(d->rm_depth <= kLdsPStack ? k_fg_hit<true> : k_fg_hit<false>, dim3(grid_for(n)), dim3(256), 0,
+          hipLaunchKernelGGL(d->rm_depth <= kLdsPStack ? k_fg_hit<true> : k_fg_hit<false>, dim3(grid_for(n, YK_APPEND_BLOCK)), dim3(YK_APPEND_BLOCK), 0,
                              P.stream, d->S, Bc, Rc, PMC, in_w, it, isub, qin,
                              P.fgl.p, P.fglen.p, out_w);
           HIPCHK(hipGetLastError());
@@ -2971,14 +2984,14 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
         HIPCHK(hipMemsetAsync(d->spec_words.p, 0, d->spec_words.n * sizeof(unsigned long long), P.stream));
         launch = 0;
         trace(true, Bc.p_rays, nullptr, RayCount{nullptr, 0, n}, Bc.p_hits, nullptr);
-        hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(n)), dim3(256), 0, P.stream, d->S, Bc, Rc, n, qw(0, 0));
+        hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(n, YK_SHADE_BLOCK)), dim3(YK_SHADE_BLOCK), 0, P.stream, d->S, Bc, Rc, n, qw(0, 0));
         HIPCHK(hipGetLastError());
         trace(false, Bc.s_rays, Bc.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, Bc.s_occl);
         hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(n)), dim3(256), 0, P.stream, Bc, Rc, n);
         HIPCHK(hipGetLastError());
         for (int isub = 0; isub < (path ? nsub : 0); ++isub) {
           if (isub > 0) {
-            hipLaunchKernelGGL(k_path_start, dim3(grid_for(n)), dim3(256), 0, P.stream, d->S, Bc, Rc, n, isub,
+            hipLaunchKernelGGL(k_path_start, dim3(grid_for(n, YK_SHADE_BLOCK)), dim3(YK_SHADE_BLOCK), 0, P.stream, d->S, Bc, Rc, n, isub,
                                qw(isub, 0));
             HIPCHK(hipGetLastError());
           }
@@ -2987,7 +3000,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
             const unsigned long long* in_w = qw(isub, depth - 1);
             unsigned long long* out_w = qw(isub, depth);
             trace(true, Bc.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, Bc.q_hits[qin], nullptr);
-            hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(n)), dim3(256), 0, P.stream, d->S, Bc, Rc, in_w, depth,
+            hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(n, YK_SHADE_BLOCK)), dim3(YK_SHADE_BLOCK), 0, P.stream, d->S, Bc, Rc, in_w, depth,
                                isub, qin, out_w);
             HIPCHK(hipGetLastError());
             trace(false, Bc.s_rays, Bc.s_idx, RayCount{out_w, 0, 0}, nullptr, Bc.s_occl);
@@ -3031,7 +3044,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     }
     if (!d->spec) {
     trace(true, B.p_rays, nullptr, RayCount{nullptr, 0, nc}, B.p_hits, nullptr);
-    hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, d->S, B, R, nc, qw(0, 0));
+    hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(nc, YK_SHADE_BLOCK)), dim3(YK_SHADE_BLOCK), 0, P.stream, d->S, B, R, nc, qw(0, 0));
     HIPCHK(hipGetLastError());
     trace(false, B.s_rays, B.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, B.s_occl);
     hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
@@ -3041,7 +3054,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     // accumulated in the reference's order (pathtracer.cc:164-298)
     for (int isub = 0; isub < (path ? nsub : 0); ++isub) {
       if (isub > 0) {  // sub-path 0's first segment came out of k_shade_primary
-        hipLaunchKernelGGL(k_path_start, dim3(grid_for(nc)), dim3(256), 0, P.stream, d->S, B, R, nc, isub,
+        hipLaunchKernelGGL(k_path_start, dim3(grid_for(nc, YK_SHADE_BLOCK)), dim3(YK_SHADE_BLOCK), 0, P.stream, d->S, B, R, nc, isub,
                            qw(isub, 0));
         HIPCHK(hipGetLastError());
       }
@@ -3050,7 +3063,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
         const unsigned long long* in_w = qw(isub, depth - 1);
         unsigned long long* out_w = qw(isub, depth);
         trace(true, B.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, B.q_hits[qin], nullptr);
-        hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(nc)), dim3(256), 0, P.stream, d->S, B, R, in_w, depth, isub,
+        hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(nc, YK_SHADE_BLOCK)), dim3(YK_SHADE_BLOCK), 0, P.stream, d->S, B, R, in_w, depth, isub,
                            qin, out_w);
         HIPCHK(hipGetLastError());
         trace(false, B.s_rays, B.s_idx, RayCount{out_w, 0, 0}, nullptr, B.s_occl);
