@@ -45,6 +45,9 @@ def pm_params(p, **kw):
     q = p.copy()
     q.integrator = A.YK_INTEGRATOR_PHOTON
     q.aa_samples = kw.pop("spp", 2)
+    q.aa_passes = kw.pop("passes", 1)  # > 1: adaptive passes (RI_vdC / RI_S positions, nextPass flags)
+    q.aa_inc_samples = kw.pop("inc", 0)
+    q.transp_shadows = kw.pop("ts", 0)
     ph = q.photon
     ph.photons = kw.pop("photons", 20000)
     ph.fg_samples = kw.pop("fg_samples", 4)
@@ -65,6 +68,8 @@ CASES = [
     ("smooth_inst", {}),
     ("bumpy", {"photons": 30000}),
     ("dirac", {"fg_min_pathlen": 0.5}),
+    ("cornell", {"passes": 3, "inc": 1, "fg_min_pathlen": 0.5}),
+    ("spec", {"passes": 2, "caustic_photons": 10000, "caustic_radius": 0.1, "ts": 1}),
     ("spec", {"caustic_photons": 20000, "caustic_radius": 0.1, "caustic_mix": 20}),
     ("spec", {"caustic_photons": 20000, "caustic_radius": 0.1, "final_gather": 0, "fg_min_pathlen": 0.5}),
     ("spec_bg", {"caustic_photons": 30000, "caustic_radius": 0.08, "fg_min_pathlen": 0.6, "fg_bounces": 3}),
