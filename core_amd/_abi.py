@@ -19,7 +19,7 @@ YK_MESH_SMOOTH, YK_MESH_NORMALS_EXPORTED = 1, 2
 YK_INTEGRATOR_DIRECT, YK_INTEGRATOR_PATH, YK_INTEGRATOR_PHOTON = 0, 1, 2
 YK_PHOTON_MAP_DIFFUSE, YK_PHOTON_MAP_CAUSTIC, YK_PHOTON_MAP_RADIANCE = 0, 1, 2
 YK_FILTER_BOX, YK_FILTER_MITCHELL, YK_FILTER_GAUSS, YK_FILTER_LANCZOS = 0, 1, 2, 3
-YK_CAUSTIC_NONE, YK_CAUSTIC_PATH = 0, 1
+YK_CAUSTIC_NONE, YK_CAUSTIC_PATH, YK_CAUSTIC_PHOTON, YK_CAUSTIC_BOTH = 0, 1, 2, 3
 
 f3 = C.c_float * 3
 

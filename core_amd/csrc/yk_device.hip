@@ -2133,6 +2133,7 @@ struct yk_device {
   std::vector<DLight> lights_host;
   // photon maps of yk_photon_build (photonIntegrator_t::preprocess)
   bool pm_ready = false;
+  int pm_integrator = -1;  // integrator whose preprocess built the maps
   yk_photon_params pm_params{};
   DBuf<uint2> dm_nodes, rm_nodes, cm_nodes;
   DBuf<float4> dm_pos, dm_dir, dm_col, rm_pos, rm_dir, rm_col, cm_pos, cm_dir, cm_col;
@@ -2728,12 +2729,16 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
       p->integrator != YK_INTEGRATOR_PHOTON)
     return set_error(YK_ERR_ARG, "unknown integrator");
   const bool pm = p->integrator == YK_INTEGRATOR_PHOTON;
-  if (pm && !d->pm_ready) return set_error(YK_ERR_STATE, "photon mapping: call yk_photon_build first (preprocess)");
-  if (pm && std::memcmp(&p->photon, &d->pm_params, sizeof(yk_photon_params)) != 0)
+  if (p->integrator == YK_INTEGRATOR_PATH &&
+      (p->caustic_type < YK_CAUSTIC_NONE || p->caustic_type > YK_CAUSTIC_BOTH))
+    return set_error(YK_ERR_ARG, "unknown caustic_type");
+  // pathtracing with photon caustics reads the caustic map its preprocess built
+  const bool pt_cmap = p->integrator == YK_INTEGRATOR_PATH &&
+                       (p->caustic_type == YK_CAUSTIC_PHOTON || p->caustic_type == YK_CAUSTIC_BOTH);
+  if ((pm || pt_cmap) && (!d->pm_ready || d->pm_integrator != p->integrator))
+    return set_error(YK_ERR_STATE, "photon maps: call yk_photon_build for this integrator first (preprocess)");
+  if ((pm || pt_cmap) && std::memcmp(&p->photon, &d->pm_params, sizeof(yk_photon_params)) != 0)
     return set_error(YK_ERR_STATE, "photon mapping: the maps were built with different photon parameters");
-  if (p->integrator == YK_INTEGRATOR_PATH && p->caustic_type != YK_CAUSTIC_NONE &&
-      p->caustic_type != YK_CAUSTIC_PATH)
-    return set_error(YK_ERR_UNSUPPORTED, "pathtracing needs caustic_type none or path");
   if (p->integrator == YK_INTEGRATOR_PATH && (p->bounces < 1 || 4 * p->bounces + 4 >= 50))
     return set_error(YK_ERR_UNSUPPORTED, "bounces must be in [1, 11]");
   if (p->width <= 0 || p->height <= 0) return set_error(YK_ERR_ARG, "empty render area");
@@ -2762,7 +2767,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   if (p->transp_shadows && (p->shadow_depth < 0 || p->shadow_depth > 8))
     return set_error(YK_ERR_UNSUPPORTED, "shadowDepth must be in [0, 8] with transpShad");
   if (R.pm_fg) R.nsub = std::max(1, p->photon.fg_samples);  // nSampl = max(1, nPaths / rayDivision)
-  const PMConst PMC = pm ? pm_const(d, p->photon) : PMConst{};
+  const PMConst PMC = (pm || pt_cmap) ? pm_const(d, p->photon) : PMConst{};
   R.bounces = p->bounces;
   R.integrator = p->integrator;
   R.transp_bg = p->transp_background;
@@ -2771,7 +2776,8 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   for (int k = 0; k < 3; ++k) R.bg[k] = d->bg[k];
   R.d1 = F.d1;
   R.spec = d->spec ? 1 : 0;
-  R.trace_caustics = (p->integrator == YK_INTEGRATOR_PATH && p->caustic_type == YK_CAUSTIC_PATH) ? 1 : 0;
+  R.trace_caustics = (p->integrator == YK_INTEGRATOR_PATH &&
+                      (p->caustic_type == YK_CAUSTIC_PATH || p->caustic_type == YK_CAUSTIC_BOTH)) ? 1 : 0;
   R.rdepth = p->raydepth;
   R.level = 0;
   R.multipass = ps.multipass ? 1 : 0;
@@ -2968,6 +2974,11 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
       hipLaunchKernelGGL(k_pm_finish, dim3(grid_for(n, 64)), dim3(64), 0, P.stream, d->S, Bc, Rc, PMC, n);
       HIPCHK(hipGetLastError());
     };
+    auto pt_caustic = [&](const Batch& Bc, long long n) {
+      if (PMC.cmap.n == 0) return;  // !causticMap.ready()
+      hipLaunchKernelGGL(k_pt_caustic, dim3(grid_for(n, 64)), dim3(64), 0, P.stream, d->S, Bc, PMC, n);
+      HIPCHK(hipGetLastError());
+    };
     TileList TL{tiles_dev.p + (size_t)bi * tiles_per_batch, base_dev.p + (size_t)bi * (tiles_per_batch + 1),
                 (int)std::min<size_t>(tiles_per_batch, owned.size() - (size_t)bi * tiles_per_batch),
                 ps.flags ? pix_dev.p + pix_off[bi] : nullptr};
@@ -3011,6 +3022,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
           }
         }
         if (pm) pm_entries(Bc, Rc, n);
+        if (pt_cmap) pt_caustic(Bc, n);
         hipLaunchKernelGGL(k_finish_spec, dim3(grid_for(n)), dim3(256), 0, P.stream, Bc, Rc, NS, node_base, n);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_spawn, dim3(grid_for(n)), dim3(256), 0, P.stream, d->S, Bc, Rc, NS, node_base, n);
@@ -3050,6 +3062,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
     HIPCHK(hipGetLastError());
     if (pm) pm_entries(B, R, nc);
+    if (pt_cmap) pt_caustic(B, nc);
     // sub-path index outermost: pathCol is shared across sub-paths and
     // accumulated in the reference's order (pathtracer.cc:164-298)
     for (int isub = 0; isub < (path ? nsub : 0); ++isub) {

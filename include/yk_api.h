@@ -84,7 +84,12 @@ typedef struct yk_camera { /* perspectiveCam_t::factory, perspectiveCamera.cc:19
 
 enum { YK_INTEGRATOR_DIRECT = 0, YK_INTEGRATOR_PATH = 1, YK_INTEGRATOR_PHOTON = 2 };
 enum { YK_FILTER_BOX = 0, YK_FILTER_MITCHELL = 1, YK_FILTER_GAUSS = 2, YK_FILTER_LANCZOS = 3 };
-enum { YK_CAUSTIC_NONE = 0, YK_CAUSTIC_PATH = 1 };
+/* pathtracing "caustic_type" (pathtracer.cc:367-385): photon / both build a
+ * caustic photon map in preprocess (mcIntegrator_t::createCausticMap,
+ * mcintegrator.cc:197-377) from params.photon: caustic_photons ("photons"),
+ * caustic_mix ("caustic_mix"), caustic_radius ("caustic_radius") and bounces
+ * (= "caustic_depth", default 10 there); yk_photon_build builds it. */
+enum { YK_CAUSTIC_NONE = 0, YK_CAUSTIC_PATH = 1, YK_CAUSTIC_PHOTON = 2, YK_CAUSTIC_BOTH = 3 };
 
 /* photonIntegrator_t parameters (photonintegr.cc:884-960 factory; defaults
  * in brackets, set by yk_render_params_default). */

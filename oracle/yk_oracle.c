@@ -1227,19 +1227,26 @@ static void recursive_raytrace(rstate* st, const yk_render_params* P, const surf
   st->raylevel--;
 }
 
-/* pathIntegrator_t::integrate, pathtracer.cc:134-333 */
+static col3 estimate_caustic(const yk_render_params* P, const surfpt* sp, v3 wo);
+
+/* pathIntegrator_t::integrate, pathtracer.cc:134-333; photon caustics
+ * (estimateCausticPhotons after the direct light) pathtracer.cc:171 */
 static rgba pt_integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir, float tmin, float tmax) {
   col3 col = C(0, 0, 0);
   float alpha = P->transp_background ? 0.0f : 1.0f;
   surfpt sp;
-  const int traceCaustics = P->caustic_type == YK_CAUSTIC_PATH;
+  const int traceCaustics = P->caustic_type == YK_CAUSTIC_PATH || P->caustic_type == YK_CAUSTIC_BOTH;
   if (scene_intersect(from, dir, tmin, &tmax, &sp)) {
     if (st->raylevel == 0) st->includeLights = 1;
     const sdmat* M = mat_of(sp.mat);
     unsigned bsdfs = mat_flags(sp.mat);
     v3 wo = vneg(dir);
     if (bsdfs & BSDF_EMIT) col = cadd(col, mat_emit(M, &sp, wo, st->includeLights));
-    if (bsdfs & BSDF_DIFFUSE) col = cadd(col, estimate_all_direct(st, &sp, wo));
+    if (bsdfs & BSDF_DIFFUSE) {
+      col = cadd(col, estimate_all_direct(st, &sp, wo));
+      if (P->caustic_type == YK_CAUSTIC_PHOTON || P->caustic_type == YK_CAUSTIC_BOTH)
+        col = cadd(col, estimate_caustic(P, &sp, wo));
+    }
     if (bsdfs & BSDF_DIFFUSE) { /* path_flags = BSDF_DIFFUSE (no_recursive off) */
       col3 pathCol = C(0, 0, 0);
       unsigned path_flags = BSDF_DIFFUSE | BSDF_REFLECT | BSDF_TRANSMIT;
@@ -1493,7 +1500,7 @@ typedef struct {
   ptree tree;
 } pmap;
 static pmap g_dmap, g_rmap, g_cmap;
-static int g_pm_ready;
+static int g_pm_ready, g_pm_integrator; /* integrator whose preprocess built the maps */
 static int g_myseed;
 
 static void pmap_push(pmap* m, v3 pos, v3 dir, col3 c) {
@@ -1555,10 +1562,10 @@ static float cmax(col3 c) { /* color_t::maximum: std::max(R, std::max(G, B)) */
 
 /* material_t::scatterPhoton, material.cc:29-46 (pSample_t s(s1,s2,s3,BSDF_ALL,lcol,alpha)) */
 static int scatter_photon(const sdmat* M, const surfpt* sp, v3 wi, v3* wo, float s1, float s2, float s3, col3 lcol,
-                          col3 alpha, col3* color, unsigned* sflags) {
+                          col3 alpha, unsigned flags, col3* color, unsigned* sflags) {
   float W = 0.f, pdf = 0.f;
   int ok;
-  col3 scol = sd_sample(M, sp, wi, wo, s1, s2, BSDF_ALL, &pdf, &W, &ok, sflags);
+  col3 scol = sd_sample(M, sp, wi, wo, s1, s2, flags, &pdf, &W, &ok, sflags);
   if (pdf > 1.0e-6f) {
     col3 cnew = cmul(cmul(lcol, alpha), scol);
     cnew = C(cnew.r * W, cnew.g * W, cnew.b * W);
@@ -1660,6 +1667,10 @@ static uint64_t g_photon_rays;
  * chosen by pdf1D_t over their energies; the diffuse pass stores non-caustic
  * photons and draws one ourRandom() per diffuse hit for the radiance points,
  * the caustic pass stores caustic photons. */
+/* caustic_pass 2: pathIntegrator_t's caustic map, mcIntegrator_t::
+ * createCausticMap (mcintegrator.cc:197-377): sL as a division, deposit on
+ * DIFFUSE|GLOSSY, scatter only the specular / glossy / filter components,
+ * stop once a photon is neither caustic nor direct. */
 static int shoot_photons(const yk_photon_params* pp, int caustic_pass, unsigned nphotons, pmap* map, raddata** rad,
                          int* nrad, int* caprad) {
   int nL = G.nlights;
@@ -1681,7 +1692,7 @@ static int shoot_photons(const yk_photon_params* pp, int caustic_pass, unsigned 
   for (unsigned curr = 0; curr < nphotons; ++curr) {
     float s1 = RI_vdC(curr, 0), s2 = (float)scrHalton(2, curr), s3 = (float)scrHalton(3, curr),
           s4 = (float)scrHalton(4, curr);
-    float sL = (float)curr * invPhotons;
+    float sL = caustic_pass == 2 ? (float)curr / (float)nphotons : (float)curr * invPhotons;
     /* pdf1D_t::DSample, sample_utils.h:141-157 */
     int lightNum;
     if (sL == 0.f) {
@@ -1707,7 +1718,12 @@ static int shoot_photons(const yk_photon_params* pp, int caustic_pass, unsigned 
       v3 wi = vneg(dir), wo = V(0, 0, 0);
       const sdmat* M = mat_of(sp.mat);
       unsigned bsdfs = M->flags;
-      if (bsdfs & BSDF_DIFFUSE) {
+      if (caustic_pass == 2) {
+        if ((bsdfs & (BSDF_DIFFUSE | BSDF_GLOSSY)) && causticPhoton) {
+          pmap_push(map, sp.P, wi, pcol);
+          map->paths = (int)curr;
+        }
+      } else if (bsdfs & BSDF_DIFFUSE) {
         if (caustic_pass) {
           if (causticPhoton) {
             pmap_push(map, sp.P, wi, pcol);
@@ -1737,11 +1753,15 @@ static int shoot_photons(const yk_photon_params* pp, int caustic_pass, unsigned 
       float s5 = (float)scrHalton(d5, curr), s6 = (float)scrHalton(d5 + 1, curr), s7 = (float)scrHalton(d5 + 2, curr);
       col3 ncol;
       unsigned sfl = 0;
-      if (!scatter_photon(M, &sp, wi, &wo, s5, s6, s7, pcol, C(1.f, 1.f, 1.f), &ncol, &sfl)) break;
+      unsigned sflags = caustic_pass == 2
+                            ? (BSDF_SPECULAR | BSDF_REFLECT | BSDF_TRANSMIT | BSDF_GLOSSY | BSDF_FILTER | BSDF_DISPERSIVE)
+                            : BSDF_ALL;
+      if (!scatter_photon(M, &sp, wi, &wo, s5, s6, s7, pcol, C(1.f, 1.f, 1.f), sflags, &ncol, &sfl)) break;
       pcol = ncol;
       causticPhoton = ((sfl & (BSDF_GLOSSY | BSDF_SPECULAR | BSDF_DISPERSIVE)) && directPhoton) ||
                       ((sfl & (BSDF_GLOSSY | BSDF_SPECULAR | BSDF_FILTER | BSDF_DISPERSIVE)) && causticPhoton);
       directPhoton = (sfl & BSDF_FILTER) && directPhoton;
+      if (caustic_pass == 2 && !(causticPhoton || directPhoton)) break;
       from = sp.P;
       dir = wo;
       tmax = -1.0f;
@@ -1761,14 +1781,34 @@ static int shoot_photons(const yk_photon_params* pp, int caustic_pass, unsigned 
 int orc_photon_build(const yk_render_params* P, int32_t* info, uint64_t* rays) {
   const yk_photon_params* pp = &P->photon;
   if (!pm_supported()) return 4;
-  if (pp->photons <= 0 || pp->search <= 0 || G.nlights <= 0) return 1;
+  const int pt = P->integrator == YK_INTEGRATOR_PATH;
+  if (!pt && (pp->photons <= 0 || pp->search <= 0 || G.nlights <= 0)) return 1;
+  if (pt && pp->caustic_mix <= 0) return 1;
   g_pm_ready = 0;
+  g_pm_integrator = P->integrator;
   g_dmap.n = g_rmap.n = g_cmap.n = 0;
   g_dmap.paths = g_rmap.paths = g_cmap.paths = 0;
   g_myseed = pp->seed;
   uint64_t rays0 = g_nclosest;
   raddata* rad = NULL;
   int nrad = 0, caprad = 0;
+  if (pt) { /* pathIntegrator_t::preprocess -> createCausticMap */
+    /* no SPECULAR / GLOSSY component: no photon turns caustic, the map stays empty */
+    int any_spec = 0, rc = 0;
+    for (int m = 0; m < G.nmats; ++m) any_spec |= (g_sd[m].flags & (BSDF_SPECULAR | BSDF_GLOSSY)) != 0;
+    if (pp->caustic_photons > 0 && any_spec && G.nlights > 0)
+      rc = shoot_photons(pp, 2, (unsigned)pp->caustic_photons, &g_cmap, NULL, NULL, NULL);
+    if (rc) return rc;
+    if (g_cmap.n > 0) pt_build(&g_cmap.tree, &g_cmap.ph[0].pos.x, (int)(sizeof(photon) / sizeof(float)), g_cmap.n);
+    g_photon_rays = g_nclosest - rays0;
+    info[0] = info[1] = info[4] = info[5] = 0;
+    info[2] = g_cmap.n;
+    info[3] = g_cmap.paths;
+    info[6] = g_myseed;
+    *rays = g_photon_rays;
+    g_pm_ready = 1;
+    return 0;
+  }
   int rc = shoot_photons(pp, 0, (unsigned)pp->photons, &g_dmap, &rad, &nrad, &caprad);
   /* caustic pass: every light shoots caustic photons (light_t::shootsCausticP
    * defaults to true); photons become caustic only after a specular sample */
@@ -2307,7 +2347,11 @@ static int render_tiles(const yk_render_params* P, int shard, int nshards, float
                         uint64_t* counts) {
   if (P->aa_passes < 1) return 4;
   if (P->aa_passes > 1 && nshards != 1) return 4;
-  if (P->integrator == YK_INTEGRATOR_PHOTON && !g_pm_ready) return 3; /* preprocess() not run */
+  if (P->integrator == YK_INTEGRATOR_PHOTON && (!g_pm_ready || g_pm_integrator != P->integrator))
+    return 3; /* preprocess() not run */
+  if (P->integrator == YK_INTEGRATOR_PATH && (P->caustic_type == YK_CAUSTIC_PHOTON || P->caustic_type == YK_CAUSTIC_BOTH) &&
+      (!g_pm_ready || g_pm_integrator != P->integrator))
+    return 3;
   if (P->transp_shadows && (P->shadow_depth < 0 || P->shadow_depth > 32)) return 4;
   g_trshad = P->transp_shadows != 0;
   g_sdepth = P->shadow_depth; /* nextPass reads the whole film */

@@ -276,6 +276,17 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     if (yk_scene_set_camera_state(ys, &cs) != YK_OK) return fail();
     if (yk_scene_build(ys) != YK_OK) return fail();
     if (yk_device_open(0, &dev) != YK_OK || yk_device_upload(dev, ys) != YK_OK) return fail();
+    const bool pt_photons = params.integrator == YK_INTEGRATOR_PATH &&
+                            (params.caustic_type == YK_CAUSTIC_PHOTON || params.caustic_type == YK_CAUSTIC_BOTH);
+    if (pt_photons) {
+      // pathIntegrator_t::preprocess -> mcIntegrator_t::createCausticMap
+      // (pathtracer.cc:90-93, mcintegrator.cc:197-377) on the device; the
+      // caustic pass draws no ourRandom() numbers
+      yk_photon_info info{};
+      if (yk_photon_build(dev, &params, &info) != YK_OK) return fail();
+      Y_INFO << integratorName << ": " << info.caustic_photons << " caustic photons (" << info.ms_total << " ms)"
+             << yendl;
+    }
     if (params.integrator == YK_INTEGRATOR_PHOTON) {
       // photonIntegrator_t::preprocess (photonintegr.cc:126-633) on the
       // device; the radiance points draw from the global ourRandom() state
@@ -296,7 +307,10 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     int aa_inc;
     CFLOAT thr;
     scene->getAAParameters(params.aa_samples, params.aa_passes, aa_inc, thr);
-    if (params.aa_passes != 1) return unsupported("AA_passes > 1 (adaptive AA) is not on the GPU path");
+    // AA_passes > 1: the device runs nextPass's adaptive passes itself
+    // (single shard: this process renders the whole film)
+    params.aa_inc_samples = aa_inc;
+    params.aa_threshold = (float)thr;
     rgba2DImage_t* img = GET(*film, FilmImage);
     const int w = img->getWidth(), h = img->getHeight();
     params.width = w;
@@ -339,8 +353,30 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     bool bg = true;
     pm.getParam("bg_transp", bg);
     p.transp_background = bg;
+    bool use_sss = false;
+    pm.getParam("useSSS", use_sss);
+    if (use_sss) { Y_ERROR << "PathTracer: SSS photons are not on the GPU path" << yendl; return nullptr; }
     const std::string* cm = nullptr;
-    if (pm.getParam("caustic_type", cm)) p.caustic_type = (*cm == "none") ? YK_CAUSTIC_NONE : YK_CAUSTIC_PATH;
+    // pathIntegrator_t::factory (pathtracer.cc:367-385): "photon" / "both"
+    // read the caustic-map parameters with the factory's defaults
+    if (pm.getParam("caustic_type", cm)) {
+      bool use_photons = false;
+      if (*cm == "photon") { p.caustic_type = YK_CAUSTIC_PHOTON; use_photons = true; }
+      else if (*cm == "both") { p.caustic_type = YK_CAUSTIC_BOTH; use_photons = true; }
+      else if (*cm == "none") p.caustic_type = YK_CAUSTIC_NONE;
+      if (use_photons) {
+        double c_rad = 0.25;
+        int c_depth = 10, search = 100, photons = 500000;
+        pm.getParam("photons", photons);
+        pm.getParam("caustic_mix", search);
+        pm.getParam("caustic_depth", c_depth);
+        pm.getParam("caustic_radius", c_rad);
+        p.photon.caustic_photons = photons;
+        p.photon.caustic_mix = search;
+        p.photon.bounces = c_depth;
+        p.photon.caustic_radius = (float)c_rad;
+      }
+    }
     return new gpuTiledIntegrator_t(p, "PathTracer");
   }
   static integrator_t* factory_direct(paraMap_t& pm, renderEnvironment_t&) {
