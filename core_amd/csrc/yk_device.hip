@@ -1326,7 +1326,10 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) YK_SHADE_ATTR k_shade_primary(
         // photon mapping: includeLights is true at every recursion level
         // (recursiveRaytrace sets it, integrate() restores it), so its
         // emission needs no fold-time decision
-        if (R.spec && R.integrator != YK_INTEGRATOR_PHOTON) em = e;
+        // emission, and only a lightMat_t's emit() reads includeLights: other
+        // emitters add it here, before the direct light and the caustic
+        // estimate, in integrate()'s order
+        if (R.spec && R.integrator != YK_INTEGRATOR_PHOTON && M.type == YK_MAT_LIGHT) em = e;
         else col = cadd(col, e);
         // photonIntegrator_t::integrate adds emit() a second time after
         // includeLights = false (photonintegr.cc:812-831)

@@ -106,7 +106,7 @@ def dirac_lights(resx, resy, integrator="cornell_pt", with_dirac=True):
     return s, p
 
 
-def specular(resx, resy, integrator="cornell_pt", raydepth=3, caustic=False, nu=16, nv=10):
+def specular(resx, resy, integrator="cornell_pt", raydepth=3, caustic=False, nu=16, nv=10, emit=0.0):
     """Cornell box + a mirror sphere, a glass-like sphere (fresnel mirror +
     transparency with a transmit filter) and a translucent sphere:
     shinyDiffuseMat_t's specular / transmissive components and
@@ -117,7 +117,9 @@ def specular(resx, resy, integrator="cornell_pt", raydepth=3, caustic=False, nu=
                             mirror_color=(0.95, 0.9, 0.8))
     glass = s.add_material(color=(0.6, 0.8, 1.0), diffuse_reflect=0.3, specular_reflect=1.0, fresnel_effect=True,
                            ior=1.5, transparency=0.9, transmit_filter=0.6)
-    transl = s.add_material(color=(0.9, 0.7, 0.3), diffuse_reflect=0.5, translucency=0.6)
+    # emit > 0: an emitting shinydiffuse (emit() added before the direct light,
+    # whatever includeLights says)
+    transl = s.add_material(color=(0.9, 0.7, 0.3), diffuse_reflect=0.5, translucency=0.6, emit=emit)
     for (cx, cy, cz, r), m in (((-0.35, 1.42, 0.3, 0.22), mirror), ((0.4, 0.85, -0.3, 0.25), glass),
                                ((0.0, 0.22, -0.6, 0.2), transl)):
         pts, faces, nrm = uv_sphere(nu, nv, r, (cx, cy, cz))

@@ -43,10 +43,10 @@ def pt_params(p, ctype, **kw):
 _SC = {}
 
 
-def spec_scene(resx=24, resy=20, caustic=False):
-    key = (resx, resy, caustic)
+def spec_scene(resx=24, resy=20, caustic=False, emit=0.0):
+    key = (resx, resy, caustic, emit)
     if key not in _SC:
-        s, p = specular(resx, resy, "cornell_pt", raydepth=3, caustic=caustic)
+        s, p = specular(resx, resy, "cornell_pt", raydepth=3, caustic=caustic, emit=emit)
         _SC[key] = (s, p, Oracle(s))
     return _SC[key]
 
@@ -113,6 +113,9 @@ GPU_CASES = [
     ("both", {"caustic_mix": 5, "caustic_radius": 0.2, "caustic_depth": 3}),
     ("photon", {"ts": 1, "spp": 2}),
     ("both", {"passes": 2, "inc": 1, "bg": True}),
+    ("photon", {"emit": 0.7}),
+    ("none", {"emit": 0.7}),
+    ("direct", {"emit": 0.7}),
 ]
 
 
@@ -125,10 +128,19 @@ def _ids(c):
 def test_gpu_pt_photon_caustics_bit_exact(gpu_device, case):
     ctype, kw = case
     kw = dict(kw)
-    s, p0, orc = spec_scene(40, 32, caustic=kw.pop("bg", False))
-    p = pt_params(p0, A.YK_CAUSTIC_PHOTON if ctype == "photon" else A.YK_CAUSTIC_BOTH, **kw)
-    info_o = orc.photon_build(p)
+    s, p0, orc = spec_scene(40, 32, caustic=kw.pop("bg", False), emit=kw.pop("emit", 0.0))
+    ct = {"photon": A.YK_CAUSTIC_PHOTON, "both": A.YK_CAUSTIC_BOTH}.get(ctype, A.YK_CAUSTIC_NONE)
+    p = pt_params(p0, ct, **kw)
     gpu_device.upload(s)
+    if ct == A.YK_CAUSTIC_NONE:  # emitting shinydiffuse in a specular-recursion frame, no maps
+        if ctype == "direct":
+            p.integrator = A.YK_INTEGRATOR_DIRECT
+        _, sums_o, cnt = orc.render(p)
+        film = gpu_device.new_film(p)
+        gpu_device.render_shard(p, film)
+        assert (film.cpu().numpy().view(np.uint32) == sums_o.view(np.uint32)).all()
+        return
+    info_o = orc.photon_build(p)
     info = gpu_device.photon_build(p)
     assert info.caustic_photons == info_o["caustic_photons"] > 0
     assert info.caustic_paths == info_o["caustic_paths"]
