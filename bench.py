@@ -58,6 +58,9 @@ def main():
     ap.add_argument("--fg-samples", type=int, default=32, help="photon: final-gather paths per hit (default 32)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target length of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--gpu-tree", action="store_true",
+                    help="replace the reference kd-tree by the device-built binned-SAH tree (yk_device_build_tree, "
+                         "documented tie-break; not the parity default)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC HBM-traffic summary (tools/pmc_traffic.py output) to attach, if present")
     args = ap.parse_args()
@@ -88,6 +91,7 @@ def main():
     p.aa_samples = args.spp
     dev = Device(local)
     dev.upload(scene)
+    tree_info = dev.build_tree(scene) if args.gpu_tree else None
     pm_info = None
     if args.integrator == "photon":  # photonIntegrator_t::preprocess, once per scene (not timed)
         p.integrator = A.YK_INTEGRATOR_PHOTON
@@ -194,7 +198,9 @@ def main():
         "data": {"bumpy": "synthetic: procedural displaced sphere + floor",
                  "hair": f"synthetic: {args.strands} curve strands x {args.strand_points} points on a sphere + floor",
                  "cornell": "the reference-fixture Cornell box (tests/golden/gen)"}[args.scene] +
-                f", {info.ntris} tris, kd-tree built on host ({t_build:.1f} s, not timed)",
+                f", {info.ntris} tris, " + (f"kd-tree built on the device ({tree_info.ms_build:.1f} ms, not timed; "
+                                           f"the reference tree {t_build:.1f} s on host first)" if tree_info is not None
+                                           else f"kd-tree built on host ({t_build:.1f} s, not timed)"),
         "config": {"workload": f"{args.scene} {info.ntris} tris, " +
                                (f"pathtracing bounces {p.bounces}, " if pm_info is None else
                                 f"photonmapping {p.photon.photons} photons, final gather {p.photon.fg_samples} paths "

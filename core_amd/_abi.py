@@ -74,6 +74,11 @@ class yk_photon_params(C.Structure):
                 ("seed", C.c_int32)]
 
 
+class yk_tree_info(C.Structure):
+    _fields_ = [("nodes", C.c_int32), ("interior", C.c_int32), ("leaves", C.c_int32), ("empty_leaves", C.c_int32),
+                ("max_depth", C.c_int32), ("leaf_refs", C.c_int64), ("ms_build", C.c_double)]
+
+
 class yk_photon_info(C.Structure):
     _fields_ = [("diffuse_photons", C.c_int32), ("diffuse_paths", C.c_int32), ("caustic_photons", C.c_int32),
                 ("caustic_paths", C.c_int32), ("rad_candidates", C.c_int32), ("radiance_photons", C.c_int32),
@@ -174,6 +179,7 @@ SIGNATURES = {
     "yk_render": (C.c_int, [P, C.POINTER(yk_render_params), fp, C.POINTER(yk_stats)]),
     "yk_photon_build": (C.c_int, [P, C.POINTER(yk_render_params), C.POINTER(yk_photon_info)]),
     "yk_photon_export": (C.c_int, [P, i32, fp, i32, i32p]),
+    "yk_device_build_tree": (C.c_int, [P, P, i32, C.POINTER(yk_tree_info)]),
 }
 
 _lib = None

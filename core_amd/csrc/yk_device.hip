@@ -2712,6 +2712,7 @@ static FilmConst make_film(const yk_render_params* p) {
 }  // extern "C"
 
 #include "yk_photon_host.inc"
+#include "yk_kdtree_gpu.inc"
 
 // One renderPass (integrator.cc:172-224): n samples per pixel from pixel
 // sample `off`; flags (film-local bytes, host) restricts it to the pixels

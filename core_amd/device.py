@@ -108,6 +108,13 @@ class Device:
         return out
 
     # -- photon mapping ---------------------------------------------------
+    def build_tree(self, scene):
+        """Replace the uploaded reference kd-tree by the device-built binned-SAH
+        tree (yk_device_build_tree) -> yk_tree_info"""
+        info = A.yk_tree_info()
+        A.check(A.lib().yk_device_build_tree(self._p, scene._p, 0, C.byref(info)))
+        return info
+
     def photon_build(self, params):
         """photonIntegrator_t::preprocess on the device -> yk_photon_info"""
         info = A.yk_photon_info()

@@ -339,16 +339,33 @@ typedef struct yk_photon_info {
 } yk_photon_info;
 
 /* photonIntegrator_t::preprocess (photonintegr.cc:126-633): shoot the diffuse
- * photons on the device, build the photon kd-trees (kdtree::pointKdTree,
- * pkdtree.h) on the host, pre-gather the radiance photons of final gathering
- * on the device. The maps stay resident for yk_render_shard with
- * p->integrator == YK_INTEGRATOR_PHOTON. Area and point lights; shinydiffuse
- * without specular components (the caustic map stays empty). */
+ * and caustic photons on the device, build the photon kd-trees
+ * (kdtree::pointKdTree, pkdtree.h) on the host, pre-gather the radiance
+ * photons of final gathering on the device. The maps stay resident for
+ * yk_render_shard with p->integrator == YK_INTEGRATOR_PHOTON.
+ * With p->integrator == YK_INTEGRATOR_PATH it is pathIntegrator_t::preprocess
+ * for caustic_type photon / both (pathtracer.cc:76-129): only the caustic map
+ * of mcIntegrator_t::createCausticMap (mcintegrator.cc:197-377). */
 int yk_photon_build(yk_device* d, const yk_render_params* p, yk_photon_info* info);
 enum { YK_PHOTON_MAP_DIFFUSE = 0, YK_PHOTON_MAP_CAUSTIC = 1, YK_PHOTON_MAP_RADIANCE = 2 };
 /* copy a map out in photon-vector order: 9 floats per photon (pos, dir, color);
  * cap = capacity in photons; *n_out = photons in the map */
 int yk_photon_export(yk_device* d, int32_t which, float* out, int32_t cap, int32_t* n_out);
+
+/* ---- GPU kd-tree build ----
+ * Replaces triKdTree_t's CPU constructor (kdtree.cc:75-666, called from
+ * scene_t::update, scene.cc:782) for a device that already holds scene s
+ * (yk_device_upload): a binned-SAH kd-tree built level by level on the device,
+ * in the same node encoding, replacing the uploaded reference tree until the
+ * next upload. Opt-in, with a documented tie-break: hits equal those of the
+ * reference tree except for which primitive wins at exactly equal t
+ * (DESIGN.md §4 "GPU kd-tree build"). flags must be 0. */
+typedef struct yk_tree_info {
+  int32_t nodes, interior, leaves, empty_leaves, max_depth;
+  int64_t leaf_refs;
+  double ms_build; /* host wall time of the call, uploads included */
+} yk_tree_info;
+int yk_device_build_tree(yk_device* d, const yk_scene* s, int32_t flags, yk_tree_info* info);
 
 #ifdef __cplusplus
 }
