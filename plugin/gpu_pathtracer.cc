@@ -276,6 +276,11 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     if (yk_scene_set_camera_state(ys, &cs) != YK_OK) return fail();
     if (yk_scene_build(ys) != YK_OK) return fail();
     if (yk_device_open(0, &dev) != YK_OK || yk_device_upload(dev, ys) != YK_OK) return fail();
+    if (gpu_tree) {  // opt-in: replace the reference tree by the device-built one
+      yk_tree_info ti{};
+      if (yk_device_build_tree(dev, ys, 0, &ti) != YK_OK) return fail();
+      Y_INFO << integratorName << ": device kd-tree, " << ti.nodes << " nodes (" << ti.ms_build << " ms)" << yendl;
+    }
     const bool pt_photons = params.integrator == YK_INTEGRATOR_PATH &&
                             (params.caustic_type == YK_CAUSTIC_PHOTON || params.caustic_type == YK_CAUSTIC_BOTH);
     if (pt_photons) {
@@ -377,7 +382,9 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
         p.photon.caustic_radius = (float)c_rad;
       }
     }
-    return new gpuTiledIntegrator_t(p, "PathTracer");
+    auto* it = new gpuTiledIntegrator_t(p, "PathTracer");
+    pm.getParam("gpu_kdtree", it->gpu_tree);
+    return it;
   }
   static integrator_t* factory_direct(paraMap_t& pm, renderEnvironment_t&) {
     yk_render_params p;
@@ -388,7 +395,9 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     bool bg = true;
     pm.getParam("bg_transp", bg);
     p.transp_background = bg;
-    return new gpuTiledIntegrator_t(p, "DirectLight");
+    auto* it = new gpuTiledIntegrator_t(p, "DirectLight");
+    pm.getParam("gpu_kdtree", it->gpu_tree);
+    return it;
   }
   // "transpShad" / "shadowDepth" -> mcIntegrator_t::trShad / sDepth; the
   // device keeps at most 8 filtered surfaces per shadow ray
@@ -445,7 +454,9 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     q.fg_bounces = fg_bounces;
     q.fg_min_pathlen = gather_dist;
     q.show_map = show_map;
-    return new gpuTiledIntegrator_t(p, "PhotonMap");
+    auto* it = new gpuTiledIntegrator_t(p, "PhotonMap");
+    pm.getParam("gpu_kdtree", it->gpu_tree);
+    return it;
   }
 
  private:
@@ -514,6 +525,7 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
   }
 
   yk_render_params params;
+  bool gpu_tree = false;  // "gpu_kdtree": device-built tree (yk_device_build_tree), documented tie-break
   yk_scene* ys = nullptr;
   yk_device* dev = nullptr;
 };
