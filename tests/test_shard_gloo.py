@@ -22,6 +22,15 @@ def _free_port():
 def _scene(integrator):
     from core_amd import _abi as A
     from core_amd.scene import probe_scene
+    if integrator == "path_photon_caustics":  # pathtracing + caustic map (createCausticMap) per rank
+        from tests.scenes import specular
+        s, p = specular(48, 40, "cornell_pt", raydepth=3)
+        p.caustic_type = A.YK_CAUSTIC_PHOTON
+        p.path_samples = 2
+        p.photon.caustic_photons = 8000
+        p.photon.caustic_radius = 0.1
+        p.photon.caustic_mix = 20
+        return s, p
     s, p = probe_scene("cornell_pt", 48, 40)
     if integrator == "photon":  # each rank runs preprocess: the maps are deterministic replicas
         p.integrator = A.YK_INTEGRATOR_PHOTON
@@ -38,7 +47,7 @@ def _worker(rank, world, port, q, integrator):
     from oracle.oracle import Oracle
     s, p = _scene(integrator)
     orc = Oracle(s)
-    if integrator == "photon":
+    if integrator != "path":
         orc.photon_build(p)
     sums, cnt = orc.render_shard(p, rank, world)
     film = torch.from_numpy(sums)
@@ -51,7 +60,7 @@ def _worker(rank, world, port, q, integrator):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("integrator", ["path", "photon"])
+@pytest.mark.parametrize("integrator", ["path", "photon", "path_photon_caustics"])
 def test_two_rank_film_reduce(integrator):
     world = 2
     ctx = mp.get_context("spawn")
@@ -67,7 +76,7 @@ def test_two_rank_film_reduce(integrator):
     from oracle.oracle import Oracle
     s, p = _scene(integrator)
     orc = Oracle(s)
-    if integrator == "photon":
+    if integrator != "path":
         orc.photon_build(p)
     _, full, cnt = orc.render(p)
     assert rays[0] == cnt["closest"] and rays[1] == cnt["shadow"]
