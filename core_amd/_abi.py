@@ -180,6 +180,7 @@ SIGNATURES = {
     "yk_photon_build": (C.c_int, [P, C.POINTER(yk_render_params), C.POINTER(yk_photon_info)]),
     "yk_photon_export": (C.c_int, [P, i32, fp, i32, i32p]),
     "yk_device_build_tree": (C.c_int, [P, P, i32, C.POINTER(yk_tree_info)]),
+    "yk_device_export_tree": (C.c_int, [P, u32p, i64, u32p, i64, C.POINTER(i64), C.POINTER(i64)]),
 }
 
 _lib = None

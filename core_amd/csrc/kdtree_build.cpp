@@ -739,18 +739,32 @@ class ParallelSink : public TaskSink {
     return id;
   }
   void finish() {
+    close();
+    work();  // the caller helps with the remaining subtrees
+    join();
+    if (error_) std::rethrow_exception(error_);
+  }
+  // an exception in the top-level recursion unwinds past finish(): close the
+  // queue and join the workers so no joinable std::thread is destroyed
+  // (which would std::terminate before YK_GUARD can report the error)
+  ~ParallelSink() {
+    close();
+    join();
+  }
+  std::vector<std::unique_ptr<KdTree>> results_;
+
+ private:
+  void close() {
     {
       std::lock_guard<std::mutex> g(m_);
       closed_ = true;
     }
     cv_.notify_all();
-    work();  // the caller helps with the remaining subtrees
-    for (auto& w : workers_) w.join();
-    if (error_) std::rethrow_exception(error_);
   }
-  std::vector<std::unique_ptr<KdTree>> results_;
-
- private:
+  void join() {
+    for (auto& w : workers_)
+      if (w.joinable()) w.join();
+  }
   void work() {
     for (;;) {
       std::pair<uint32_t, SubtreeTask> job;

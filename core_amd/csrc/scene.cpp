@@ -2,6 +2,7 @@
 #include "scene.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -313,6 +314,8 @@ void Scene::finalize() {
   const int ntris = (int)tri_material.size();
   if (ntris == 0) throw std::invalid_argument("scene is empty");
   build_kdtree(tri_verts.data(), ntris, tree);
+  static std::atomic<uint64_t> next_generation{1};
+  generation = next_generation.fetch_add(1);
   built = true;
   build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }

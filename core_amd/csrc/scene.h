@@ -63,6 +63,7 @@ struct Scene {
   bool any_smooth = false;
   KdTree tree;
   bool built = false;
+  uint64_t generation = 0;           // unique per finalize() (process-wide), so a device can tell scenes apart
   double build_seconds = 0.0;
 
   void finalize();                   // scene_t::update: gather prims, build tree

@@ -2114,6 +2114,9 @@ struct yk_device {
   int per_cu[2] = {1, 1};  // resident trace waves per CU: [0] any-hit, [1] closest
   hipStream_t stream = nullptr;  // = pipe[0].stream (ray queries, film resolve)
   bool uploaded = false;
+  const yk_scene* uploaded_scene = nullptr;  // the scene the resident arrays came from
+  uint64_t uploaded_gen = 0;                 // its Scene::generation at upload
+  size_t nleaf = 0;                          // leaf-list entries of the resident tree
   // scene
   DBuf<float4> tris, ng;
   DBuf<float> vn;  // smooth-shading vertex normals (9 per prim), only when the scene has smooth meshes
@@ -2565,7 +2568,10 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   d->nlights = (int)S.light_states.size();
   d->ntris = nt;
   d->max_depth = S.tree.max_depth;
+  d->nleaf = S.tree.leaf_prims.size();
   d->uploaded = true;
+  d->uploaded_scene = s;
+  d->uploaded_gen = S.generation;
   return YK_OK;
   YK_GUARD_END
 }

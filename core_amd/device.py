@@ -107,13 +107,25 @@ class Device:
         A.check(A.lib().yk_render(self._p, C.byref(params), out.ctypes.data_as(A.fp), C.byref(st)))
         return out
 
-    # -- photon mapping ---------------------------------------------------
+    # -- kd-tree ------------------------------------------------------------
     def build_tree(self, scene):
         """Replace the uploaded reference kd-tree by the device-built binned-SAH
         tree (yk_device_build_tree) -> yk_tree_info"""
         info = A.yk_tree_info()
         A.check(A.lib().yk_device_build_tree(self._p, scene._p, 0, C.byref(info)))
         return info
+
+    def export_tree(self):
+        """The resident kd-tree (yk_device_export_tree): (nodes (n, 2) u32, leaf u32)"""
+        nn, nl = C.c_int64(), C.c_int64()
+        A.check(A.lib().yk_device_export_tree(self._p, None, 0, None, 0, C.byref(nn), C.byref(nl)))
+        nodes = np.zeros((nn.value, 2), np.uint32)
+        leaf = np.zeros(max(nl.value, 1), np.uint32)
+        A.check(A.lib().yk_device_export_tree(self._p, nodes.ctypes.data_as(A.u32p), nn.value,
+                                              leaf.ctypes.data_as(A.u32p), nl.value, C.byref(nn), C.byref(nl)))
+        return nodes, leaf[:nl.value]
+
+    # -- photon mapping ---------------------------------------------------
 
     def photon_build(self, params):
         """photonIntegrator_t::preprocess on the device -> yk_photon_info"""

@@ -366,6 +366,14 @@ typedef struct yk_tree_info {
   double ms_build; /* host wall time of the call, uploads included */
 } yk_tree_info;
 int yk_device_build_tree(yk_device* d, const yk_scene* s, int32_t flags, yk_tree_info* info);
+/* Copies the device's resident kd-tree (the uploaded reference tree, or the
+ * one yk_device_build_tree made) to host memory in the export encoding of
+ * yk_scene_export: 2 u32 per node (split bits / prim / leaf offset; axis |
+ * right child or count << 2), leaf lists as u32 prim ids. With nodes / leaf
+ * NULL only the counts are returned. Test and tooling hook: it lets checks
+ * aim rays at the split planes of the tree actually traversed. */
+int yk_device_export_tree(yk_device* d, uint32_t* nodes, int64_t node_cap, uint32_t* leaf, int64_t leaf_cap,
+                          int64_t* nnodes_out, int64_t* nleaf_out);
 
 #ifdef __cplusplus
 }

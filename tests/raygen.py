@@ -61,3 +61,36 @@ def edge_rays(bound, nodes, seed, n_axis=2048, n_split=2048, n_out=2048):
         tmax = -1.0 if k % 3 else float(rng.random() * np.linalg.norm(ext))
         out.append(np.r_[o, d, 0.0, tmax])
     return np.asarray(out, np.float32)
+
+
+def graze_rays(tri_verts, bound, n, seed):
+    """Rays aimed exactly at points on triangle edges (the Moller-Trumbore
+    u + v <= 1 / u >= 0 boundaries), a third of them from origins close to
+    the triangle's plane (grazing incidence): a primitive missing from a leaf
+    next to its edge shows up as a lost hit on these."""
+    rng = np.random.default_rng(seed)
+    V = np.asarray(tri_verts, np.float32).reshape(-1, 9)
+    lo, hi = np.asarray(bound[:3], np.float32), np.asarray(bound[3:], np.float32)
+    out = np.zeros((n, 8), np.float32)
+    for k in range(n):
+        t = V[rng.integers(len(V))].reshape(3, 3)
+        e = rng.integers(3)
+        a, b = t[e], t[(e + 1) % 3]
+        P = (a + np.float32(rng.random()) * (b - a)).astype(np.float32)
+        if k % 3 == 2:
+            nrm = np.cross(t[1] - t[0], t[2] - t[0])
+            nrm /= max(np.linalg.norm(nrm), 1e-30)
+            side = np.cross(nrm, b - a)
+            side /= max(np.linalg.norm(side), 1e-30)
+            o = P + side * np.float32(0.5 + rng.random()) + nrm * np.float32((rng.random() - 0.5) * 1e-3)
+        else:
+            o = lo + (hi - lo) * rng.random(3).astype(np.float32)
+        d = (P - o).astype(np.float32)
+        nd = np.float32(np.linalg.norm(d))
+        if not nd > 0:
+            d, nd = np.array([0, 1, 0], np.float32), np.float32(1)
+        out[k, 0:3] = o
+        out[k, 3:6] = d / nd
+        out[k, 6] = 0.0
+        out[k, 7] = -1.0
+    return out
