@@ -395,6 +395,201 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
   return false;
 }
 
+// ---- wave-cooperative leaf testing -------------------------------------
+// The traversal kernels are bound by VALU issue, and the per-lane leaf loop
+// ran at 17-31 % lane utilisation (a wave loops to the longest leaf among its
+// lanes while most lanes hold 0-2 references). Here each iteration is split:
+// every lane descends to its next leaf (trav_descend), then the wave tests the
+// (ray, reference) pairs of ALL its lanes' leaves together, 64 pairs per
+// round (coop_leaves), then every lane applies its leaf's outcome and pops
+// (trav_next). The outcome of a leaf is the reference's sequential leaf loop
+// (kdtree.cc:760-800 closest, 905-940 any-hit):
+//  * closest: the first reference i with the smallest t among the hits with
+//    tmin <= t < Z (Z as the leaf is entered) -- the lexicographic minimum of
+//    (t, i), found with one LDS atomic min per hit on a (t bits, i) key;
+//  * any-hit: occluded when any reference hits with 0 <= t < dist; the
+//    reference stops at the first such i and has tested i + 1 triangles,
+//    which the triangle-test counter reproduces (LDS atomic min on i).
+// Results, node and triangle-test counts are therefore those of the per-lane
+// loop, bit for bit.
+
+// Descends from st.node to a leaf (the descent of trav_step); false when the
+// ray is already finished (dist < entry t). Outputs the leaf's w0 and count.
+template <bool CLOSEST>
+__device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const LaneStack& stk, unsigned& nnodes,
+                                             uint32_t& w0, uint32_t& nref) {
+  if (st.dist < st.en_t) return false;
+  int node = st.node;
+  NodePair q = ld_pair(S.nodes, node);
+  uint2 nd = make_uint2(q.a, q.b), nx = make_uint2(q.c, q.d);
+  bool have = true;
+  nnodes++;
+  for (;;) {
+    const uint32_t ax = nd.y & 3u;
+    if (ax == 3u) break;
+    const float split = __uint_as_float(nd.x);
+    const int right = (int)(nd.y >> 2);
+    const float enp = sel3(st.en_pb, ax), exq = sel3(st.ex_pb, ax);
+    const bool left_first = enp <= split;
+    // far child pushed unless the exit stays on the near side; evaluated on
+    // wave masks (SALU) instead of per-lane 0/1 selects
+    const unsigned long long m_lf = __builtin_amdgcn_ballot_w64(left_first);
+    const unsigned long long m_c1 = __builtin_amdgcn_ballot_w64(exq <= split);
+    const unsigned long long m_c2 = __builtin_amdgcn_ballot_w64(split < exq);
+    const bool push = __builtin_amdgcn_inverse_ballot_w64((m_lf & ~m_c1) | (~m_lf & ~m_c2));
+    const int nxt = left_first ? node + 1 : right;
+    if (push) {
+      const int far_ = left_first ? right : node + 1;
+      const float t = (split - sel3(st.o, ax)) * sel3(st.inv, ax);
+      stk.push(st.sp, make_uint2(__float_as_uint(st.ex_split), st.ex_w));
+      st.sp++;
+      st.ex_t = t;
+      st.ex_split = split;
+      st.ex_w = (uint32_t)(far_ + 1) | (ax << 30);
+      exit_pb(st);
+    }
+    const bool reuse = left_first & have;
+    if (!reuse) q = ld_pair(S.nodes, nxt);
+    nd = reuse ? nx : make_uint2(q.a, q.b);
+    nx = make_uint2(q.c, q.d);
+    have = !reuse;
+    node = nxt;
+    nnodes++;
+  }
+  w0 = nd.x;
+  nref = nd.y >> 2;
+  return true;
+}
+
+// After the leaf: the closest-hit stop test, then pop (kdtree.cc:802-812).
+// True when the ray is finished.
+template <bool CLOSEST>
+__device__ __forceinline__ bool trav_next(const DScene& S, Trav& st, const LaneStack& stk) {
+  if (CLOSEST && st.prim >= 0 && st.Z <= st.ex_t) return true;
+  st.en_t = st.ex_t;
+  st.en_pb = st.ex_pb;
+  st.node = (int)(st.ex_w & 0x3FFFFFFFu) - 1;
+  if (st.node < 0) return true;
+  if ((unsigned)st.node >= S.nnodes || st.sp <= 0) {  // corrupt state: never index out of the tree
+    st.prim = -2;
+    return true;
+  }
+  st.sp--;
+  const uint2 e = stk.pop(st.sp);
+  st.ex_split = __uint_as_float(e.x);
+  st.ex_w = e.y;
+  const uint32_t code = e.y >> 30;
+  st.ex_t = (code == 3u) ? st.ex_split : (st.ex_split - sel3(st.o, code)) * sel3(st.inv, code);
+  exit_pb(st);
+  return false;
+}
+
+// total-order key of a float (for t >= 0 the raw bits; -0 is made +0 first so
+// that equal t compare equal, as the reference's t < Z does)
+__device__ __forceinline__ uint32_t ord_key(float t) {
+  const uint32_t b = __float_as_uint(t + 0.0f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+// Wave-uniform: every lane calls it; nref = 0 for lanes without a leaf to test.
+template <bool CLOSEST>
+__device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t nref, uint32_t w0, int lane,
+                                            unsigned long long* keys, float4* cand, unsigned& ntris,
+                                            bool& occluded) {
+  unsigned x = nref;  // inclusive prefix sum of the lanes' reference counts
+#ifndef YK_DPP_SCAN
+#define YK_DPP_SCAN 1
+#endif
+#if YK_DPP_SCAN
+  // DPP scan: row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15 / 31
+  // carry the row totals (out-of-row sources read 0)
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+#else
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned y = (unsigned)__shfl_up((int)x, d);
+    if (lane >= d) x += y;
+  }
+#endif
+  const unsigned pre = x - nref;
+  const unsigned total = (unsigned)__builtin_amdgcn_readlane((int)x, 63);
+  if (total == 0u) return;
+  keys[lane] = ~0ull;
+  __syncthreads();  // one wave per block: orders the LDS traffic of the phase
+  const float zlim = CLOSEST ? st.Z : st.dist;
+  for (unsigned base = 0; base < total; base += 64u) {
+    const unsigned s = base + (unsigned)lane;
+    const unsigned sc = min(s, total - 1u);
+    // owner of slot s: the last lane whose range starts at or before s
+    int own = 0;
+    unsigned pown = 0;
+#pragma unroll
+    for (int step = 32; step > 0; step >>= 1) {
+      const int c = own + step;
+      const unsigned v = (unsigned)__shfl((int)pre, c);
+      if (v <= sc) {
+        own = c;
+        pown = v;
+      }
+    }
+    const unsigned k = sc - pown;
+    const uint32_t ow0 = (uint32_t)__shfl((int)w0, own), on = (uint32_t)__shfl((int)nref, own);
+    const v3 ro = V3(__shfl(st.o.x, own), __shfl(st.o.y, own), __shfl(st.o.z, own));
+    const v3 rd = V3(__shfl(st.d.x, own), __shfl(st.d.y, own), __shfl(st.d.z, own));
+    const float rz = __shfl(zlim, own);
+    const float rtmin = CLOSEST ? __shfl(st.tmin, own) : 0.f;
+    bool valid = false;
+    unsigned long long key = 0;
+    float th = 0.f, u = 0.f, v = 0.f;
+    uint32_t p = 0;
+    if (s < total) {
+      p = (on == 1u) ? ow0 : S.leaf[ow0 + k];
+      float4 A = S.tris[3 * p], E1 = S.tris[3 * p + 1], E2 = S.tris[3 * p + 2];
+      asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
+                   "+v"(E2.y), "+v"(E2.z));
+      if (mt_intersect(V3(A.x, A.y, A.z), V3(E1.x, E1.y, E1.z), V3(E2.x, E2.y, E2.z), ro, rd, th, u, v)) {
+        valid = th < rz && th >= rtmin;
+        if (valid) {
+          if (CLOSEST) {
+            key = ((unsigned long long)ord_key(th) << 32) | k;
+            atomicMin(&keys[own], key);
+          } else {
+            atomicMin(&keys[own], (unsigned long long)k);
+          }
+        }
+      }
+    }
+    if (CLOSEST) {
+      __syncthreads();
+      if (valid && keys[own] == key) cand[own] = make_float4(th, u, v, __uint_as_float(p));
+    }
+  }
+  __syncthreads();
+  if (nref > 0u) {
+    const unsigned long long kk = keys[lane];
+    if (CLOSEST) {
+      ntris += nref;
+      if (kk != ~0ull) {
+        const float4 c = cand[lane];
+        st.Z = c.x;
+        st.b1 = c.y;
+        st.b2 = c.z;
+        st.prim = (int)__float_as_uint(c.w);
+      }
+    } else if (kk != ~0ull) {
+      occluded = true;
+      ntris += (unsigned)kk + 1u;
+    } else {
+      ntris += nref;
+    }
+  }
+}
+
 __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int src) {
   unsigned lo = __shfl((unsigned)v, src), hi = __shfl((unsigned)(v >> 32), src);
   return ((unsigned long long)hi << 32) | lo;
@@ -418,7 +613,7 @@ struct RayCount {
   }
 };
 
-template <bool CLOSEST, int NSEG, bool PIPE, bool TS = false>
+template <bool CLOSEST, int NSEG, bool PIPE, bool TS = false, bool COOP = false>
 __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx,
                                            RayCount rc, yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
                                            unsigned long long* __restrict__ work, unsigned long long* __restrict__ ctr,
@@ -450,10 +645,19 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   unsigned pool_next = 0, pool_end = 0;
   unsigned seg_done = 0;  // bit s: segment s has no chunks left
   unsigned iters = 0;     // wave watchdog: a valid tree never gets near the cap
+#ifdef YK_TRAV_STATS
+  // diagnostic build (tools/trav_bench.py only: in the render pipeline ctr[4..]
+  // are the other kernel kind's accumulators): wave iterations, active lanes per iteration, wave-level
+  // descent / leaf-loop trips (max over lanes), refills
+  unsigned long long s_it = 0, s_act = 0, s_dmax = 0, s_lmax = 0, s_refill = 0;
+#endif
   for (;;) {
     const unsigned long long want = __ballot(rid < 0 && !exhausted);
     const unsigned long long act = __ballot(rid >= 0);
     if (want != 0ull && (act == 0ull || __popcll(want) >= refill_min)) {
+#ifdef YK_TRAV_STATS
+      s_refill++;
+#endif
       const unsigned cnt = (unsigned)__popcll(want);
       const unsigned avail = pool_end - pool_next;
       unsigned cb = 0, ce = 0;  // newly grabbed chunk [cb, ce)
@@ -514,7 +718,40 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       continue;
     }
     const bool runaway = ++iters > (1u << 30);
-    if (rid >= 0) {
+#ifdef YK_TRAV_STATS
+    const unsigned n_before = nnodes, t_before = ntris;
+    s_it++;
+    s_act += (unsigned long long)__popcll(__ballot(rid >= 0));
+#endif
+    if (COOP) {
+      __shared__ unsigned long long keys[64];
+      __shared__ float4 cand[CLOSEST ? 64 : 1];
+      const bool act = rid >= 0;
+      bool live = false;
+      uint32_t w0 = 0, nref = 0;
+      if (act) live = trav_descend<CLOSEST>(S, st, stk, nnodes, w0, nref);
+      bool occ = false;
+      coop_leaves<CLOSEST>(S, st, live ? nref : 0u, w0, lane, keys, cand, ntris, occ);
+      if (act) {
+        bool done = !live || occ || trav_next<CLOSEST>(S, st, stk);
+        if (runaway) {
+          st.prim = -2;
+          done = true;
+        }
+        if (st.prim == -2) {
+          nerr++;
+          st.prim = -1;
+        }
+        if (done) {
+          if (CLOSEST) {
+            hits[rid] = (st.prim >= 0) ? yk_hit{st.prim, st.Z, st.b1, st.b2} : yk_hit{-1, 0.f, 0.f, 0.f};
+          } else {
+            occl[rid] = occ ? 1 : 0;
+          }
+          rid = -1;
+        }
+      }
+    } else if (rid >= 0) {
       bool occ = false;
       bool done = trav_step<CLOSEST, PIPE, TS>(S, st, stk, nnodes, ntris, occ);
       if (runaway) {
@@ -539,8 +776,29 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
         rid = -1;
       }
     }
+#ifdef YK_TRAV_STATS
+    {
+      unsigned dm = nnodes - n_before, lm = ntris - t_before;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        dm = max(dm, (unsigned)__shfl_xor((int)dm, off));
+        lm = max(lm, (unsigned)__shfl_xor((int)lm, off));
+      }
+      s_dmax += dm;
+      s_lmax += lm;
+    }
+#endif
     if (runaway) exhausted = true;
   }
+#ifdef YK_TRAV_STATS
+  if (lane == 0) {
+    atomicAdd(&ctr[4], s_it);
+    atomicAdd(&ctr[5], s_act);
+    atomicAdd(&ctr[6], s_dmax);
+    atomicAdd(&ctr[7], s_lmax);
+    atomicAdd(&ctr[8], s_refill);
+  }
+#endif
   // wave-reduced work counters (nodes visited, triangle tests)
   unsigned long long a = nnodes, b = ntris;
 #pragma unroll
@@ -555,32 +813,40 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   if (nerr) atomicAdd(&ctr[2], (unsigned long long)nerr);
 }
 
-// Occupancy targets and ray hand-out (measured on MI355X, 1M-tri scene): the
-// closest-hit kernel runs best at 6 waves/SIMD with per-XCD ray segments
-// (+12% from L2 locality), the any-hit kernel at 7 waves with one shared
-// segment (its smaller state leaves room for the extra waves, which the
-// segment logic's registers would take away); with an 8-deep LDS ring (4 KB
-// per wave) registers set the limit.
+// Occupancy targets and ray hand-out (measured on MI355X, 1M-tri scene): with
+// the wave-cooperative leaf phase the closest-hit kernel runs best at 5
+// waves/SIMD (102 VGPRs, no spill; 6 waves spill and lose 10 % on camera
+// rays) with per-XCD ray segments (+12% from L2 locality), the any-hit kernel
+// at 6 waves with one shared segment. Before the cooperative phase the
+// targets were 6 / 7 (tools/trav_bench.py).
 #ifndef YK_CLOSEST_WAVES
-#define YK_CLOSEST_WAVES 6
+#define YK_CLOSEST_WAVES 5
 #endif
 #ifndef YK_SHADOW_WAVES
-#define YK_SHADOW_WAVES 7
+#define YK_SHADOW_WAVES 6
 #endif
 #ifndef YK_SHADOW_NSEG
 #define YK_SHADOW_NSEG 1
+#endif
+// wave-cooperative leaf testing (coop_leaves) in the closest / any-hit kernels
+#ifndef YK_COOP
+#define YK_COOP 1
+#endif
+#ifndef YK_COOP_LP
+#define YK_COOP_LP 1
 #endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
 k_trace_closest(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                 yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                 unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<true, 8, false>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+  trace_body<true, 8, false, false, YK_COOP>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
 k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false, YK_SHADOW_NSEG, false>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+  trace_body<false, YK_SHADOW_NSEG, false, false, YK_COOP>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth,
+                                                           refill_min);
 }
 // crowded-leaf variants (PIPE leaf loop): one wave fewer per SIMD buys the
 // registers of the prefetched triangle without spilling
@@ -594,13 +860,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOS
 k_trace_closest_lp(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                    yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                    unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<true, 8, true>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+  trace_body<true, 8, true, false, YK_COOP_LP>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_LP_WAVES)))
 k_trace_shadow_lp(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                   yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                   unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false, 1, true>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+  trace_body<false, 1, true, false, YK_COOP_LP>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 // transparent shadows (scene_t::isShadowed(state, ray, maxDepth, filt),
 // scene.cc:904-928 -> IntersectTS): occlusion + filter colour per ray
@@ -2009,7 +2275,7 @@ struct Pipe {
     HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&ev0));
     HIPCHK(hipEventCreate(&ev1));
-    counters.ensure(136);
+    counters.ensure(144);
   }
   hipEvent_t event(size_t i) {
     while (evpool.size() <= i) {
@@ -2399,14 +2665,22 @@ void launch_trace(yk_device* d, Pipe& P, const yk_ray* rays, long long n, yk_hit
   if (n > 0x7FFFFFFFll - (1ll << 24)) throw std::invalid_argument("ray batch too large (max ~2^31 rays per call)");
   unsigned long long* work = P.counters.p;
   unsigned long long* acc = P.counters.p + 128;
-  HIPCHK(hipMemsetAsync(work, 0, 136 * sizeof(unsigned long long), P.stream));
+  HIPCHK(hipMemsetAsync(work, 0, 144 * sizeof(unsigned long long), P.stream));
   enqueue_trace<CLOSEST>(d, P, rays, nullptr, RayCount{nullptr, 0, n}, hits, occ, work, acc, P.ev0, P.ev1);
-  unsigned long long h[4];
+  unsigned long long h[9];
   HIPCHK(hipMemcpyAsync(h, acc, sizeof h, hipMemcpyDeviceToHost, P.stream));
   HIPCHK(hipStreamSynchronize(P.stream));
   if (h[2]) throw std::runtime_error("kd-tree traversal watchdog fired on " + std::to_string(h[2]) + " rays");
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, P.ev0, P.ev1));
+#ifdef YK_TRAV_STATS
+  std::fprintf(stderr,
+               "[trav-stats] %s rays %lld: wave iterations %llu, active lanes/iter %.2f, descent trips max %.2f / "
+               "mean-active %.2f, leaf trips max %.2f / mean-active %.2f, refills %llu (%.1f rays each)\n",
+               CLOSEST ? "closest" : "shadow", n, h[4], (double)h[5] / (double)h[4], (double)h[6] / (double)h[4],
+               (double)h[0] / (double)h[5], (double)h[7] / (double)h[4], (double)h[1] / (double)h[5], h[8],
+               (double)n / (double)h[8]);
+#endif
   if (!st) return;
   if (CLOSEST) {
     st->closest_rays += (uint64_t)n;
