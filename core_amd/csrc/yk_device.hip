@@ -190,6 +190,9 @@ __device__ __forceinline__ NodePair ld_pair(const uint2* nodes, int i) {
 
 // v[axis] for axis in 0..2 via selects (no dynamic register indexing)
 __device__ __forceinline__ float sel3(v3 v, uint32_t ax) { return ax == 0u ? v.x : (ax == 1u ? v.y : v.z); }
+// the same with the axis masks already computed (v by value: selects of
+// registers, never of addresses)
+__device__ __forceinline__ float sel3m(v3 v, bool a0, bool a1) { return a0 ? v.x : (a1 ? v.y : v.z); }
 
 // pb of the current exit: pb[code] = split, other axes from + t*dir
 __device__ __forceinline__ void exit_pb(Trav& st) {
@@ -419,17 +422,23 @@ template <bool CLOSEST>
 __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const LaneStack& stk, unsigned& nnodes,
                                              uint32_t& w0, uint32_t& nref) {
   if (st.dist < st.en_t) return false;
-  int node = st.node;
-  NodePair q = ld_pair(S.nodes, node);
+  // node indices are unsigned 32-bit offsets from the uniform node pointer
+  // (one address VALU per load: base in SGPRs, 32-bit lane offset)
+  const char* nbase = reinterpret_cast<const char*>(S.nodes);
+  uint32_t node = (uint32_t)st.node;
+  NodePair q = *reinterpret_cast<const NodePair*>(nbase + (node << 3));
   uint2 nd = make_uint2(q.a, q.b), nx = make_uint2(q.c, q.d);
   bool have = true;
   nnodes++;
-  for (;;) {
-    const uint32_t ax = nd.y & 3u;
-    if (ax == 3u) break;
+#ifndef YK_PAIR_CACHE
+#define YK_PAIR_CACHE 0  // node-pair reuse: +0 with the VALU-bound cooperative kernels (measured -1 %)
+#endif
+  uint32_t ax = nd.y & 3u;
+  while (ax != 3u) {
     const float split = __uint_as_float(nd.x);
-    const int right = (int)(nd.y >> 2);
-    const float enp = sel3(st.en_pb, ax), exq = sel3(st.ex_pb, ax);
+    const uint32_t right = nd.y >> 2;
+    const bool a0 = ax == 0u, a1 = ax == 1u;
+    const float enp = sel3m(st.en_pb, a0, a1), exq = sel3m(st.ex_pb, a0, a1);
     const bool left_first = enp <= split;
     // far child pushed unless the exit stays on the near side; evaluated on
     // wave masks (SALU) instead of per-lane 0/1 selects
@@ -437,24 +446,33 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
     const unsigned long long m_c1 = __builtin_amdgcn_ballot_w64(exq <= split);
     const unsigned long long m_c2 = __builtin_amdgcn_ballot_w64(split < exq);
     const bool push = __builtin_amdgcn_inverse_ballot_w64((m_lf & ~m_c1) | (~m_lf & ~m_c2));
-    const int nxt = left_first ? node + 1 : right;
+    const uint32_t nxt = left_first ? node + 1u : right;
     if (push) {
-      const int far_ = left_first ? right : node + 1;
-      const float t = (split - sel3(st.o, ax)) * sel3(st.inv, ax);
+      const uint32_t far_ = left_first ? right : node + 1u;
+      const float t = (split - sel3m(st.o, a0, a1)) * sel3m(st.inv, a0, a1);
       stk.push(st.sp, make_uint2(__float_as_uint(st.ex_split), st.ex_w));
       st.sp++;
       st.ex_t = t;
       st.ex_split = split;
-      st.ex_w = (uint32_t)(far_ + 1) | (ax << 30);
-      exit_pb(st);
+      st.ex_w = (far_ + 1u) | (ax << 30);
+      // exit point (exit_pb with the axis masks at hand)
+      const v3 o = st.o, d = st.d;
+      const float x = o.x + t * d.x, y = o.y + t * d.y, z = o.z + t * d.z;
+      st.ex_pb = V3(a0 ? split : x, a1 ? split : y, (a0 || a1) ? z : split);
     }
+#if YK_PAIR_CACHE
     const bool reuse = left_first & have;
-    if (!reuse) q = ld_pair(S.nodes, nxt);
+    if (!reuse) q = *reinterpret_cast<const NodePair*>(nbase + (nxt << 3));
     nd = reuse ? nx : make_uint2(q.a, q.b);
     nx = make_uint2(q.c, q.d);
     have = !reuse;
+#else
+    q = *reinterpret_cast<const NodePair*>(nbase + (nxt << 3));
+    nd = make_uint2(q.a, q.b);
+#endif
     node = nxt;
     nnodes++;
+    ax = nd.y & 3u;
   }
   w0 = nd.x;
   nref = nd.y >> 2;
