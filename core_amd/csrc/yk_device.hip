@@ -420,21 +420,34 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
 // ray is already finished (dist < entry t). Outputs the leaf's w0 and count.
 template <bool CLOSEST>
 __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const LaneStack& stk, unsigned& nnodes,
-                                             uint32_t& w0, uint32_t& nref) {
+                                             uint32_t& w0, uint32_t& nref, bool& paused) {
+  paused = false;
   if (st.dist < st.en_t) return false;
   // node indices are unsigned 32-bit offsets from the uniform node pointer
   // (one address VALU per load: base in SGPRs, 32-bit lane offset)
   const char* nbase = reinterpret_cast<const char*>(S.nodes);
   uint32_t node = (uint32_t)st.node;
-  NodePair q = *reinterpret_cast<const NodePair*>(nbase + (node << 3));
-  uint2 nd = make_uint2(q.a, q.b), nx = make_uint2(q.c, q.d);
-  bool have = true;
+  uint2 nd = *reinterpret_cast<const uint2*>(nbase + (node << 3));
   nnodes++;
-#ifndef YK_PAIR_CACHE
-#define YK_PAIR_CACHE 0  // node-pair reuse: +0 with the VALU-bound cooperative kernels (measured -1 %)
-#endif
+  // (round 1's node-pair reuse -- a left descent taking the sibling word of
+  // the previous 16-B load -- measured -1 % here: the kernels are bound by
+  // VALU issue, not by the dependent load, and the reuse costs moves)
   uint32_t ax = nd.y & 3u;
+#ifndef YK_DESC_FRAC
+#define YK_DESC_FRAC 4  // measured 2 / 3 / 4 / 8: 2477 / 2524 / 2527 / 2450 Mrays/s (off: 2344)
+#endif
+  // descent pause (YK_DESC_FRAC = f > 0): once fewer than 1/f of the lanes
+  // that started this descent are still descending, those pause at their
+  // current node and resume in the next iteration, so the wave does not loop
+  // to its longest descent while the other lanes idle
+  const unsigned started = YK_DESC_FRAC ? (unsigned)__popcll(__builtin_amdgcn_ballot_w64(true)) : 0u;
   while (ax != 3u) {
+    if (YK_DESC_FRAC && (unsigned)__popcll(__builtin_amdgcn_ballot_w64(true)) * YK_DESC_FRAC < started) {
+      paused = true;
+      st.node = (int)node;
+      nnodes--;  // counted again when the next descent reloads it
+      return true;
+    }
     const float split = __uint_as_float(nd.x);
     const uint32_t right = nd.y >> 2;
     const bool a0 = ax == 0u, a1 = ax == 1u;
@@ -460,16 +473,7 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
       const float x = o.x + t * d.x, y = o.y + t * d.y, z = o.z + t * d.z;
       st.ex_pb = V3(a0 ? split : x, a1 ? split : y, (a0 || a1) ? z : split);
     }
-#if YK_PAIR_CACHE
-    const bool reuse = left_first & have;
-    if (!reuse) q = *reinterpret_cast<const NodePair*>(nbase + (nxt << 3));
-    nd = reuse ? nx : make_uint2(q.a, q.b);
-    nx = make_uint2(q.c, q.d);
-    have = !reuse;
-#else
-    q = *reinterpret_cast<const NodePair*>(nbase + (nxt << 3));
-    nd = make_uint2(q.a, q.b);
-#endif
+    nd = *reinterpret_cast<const uint2*>(nbase + (nxt << 3));
     node = nxt;
     nnodes++;
     ax = nd.y & 3u;
@@ -747,11 +751,12 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       const bool act = rid >= 0;
       bool live = false;
       uint32_t w0 = 0, nref = 0;
-      if (act) live = trav_descend<CLOSEST>(S, st, stk, nnodes, w0, nref);
+      bool paused = false;
+      if (act) live = trav_descend<CLOSEST>(S, st, stk, nnodes, w0, nref, paused);
       bool occ = false;
-      coop_leaves<CLOSEST>(S, st, live ? nref : 0u, w0, lane, keys, cand, ntris, occ);
+      coop_leaves<CLOSEST>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, ntris, occ);
       if (act) {
-        bool done = !live || occ || trav_next<CLOSEST>(S, st, stk);
+        bool done = !live || occ || (!paused && trav_next<CLOSEST>(S, st, stk));
         if (runaway) {
           st.prim = -2;
           done = true;
