@@ -87,7 +87,7 @@ constexpr int kSmoothBit = 0x10000;  // prim interpolates vertex normals (mesh i
 struct DScene {
   const float4* tris;    // 3 float4 per prim: a, e1=b-a, e2=c-a
   const uint2* nodes;    // kd nodes (kdtree_build.h encoding)
-  const uint2* tnodes;   // the same nodes in the traversal encoding of k_flag_nodes (empty-child bits)
+  const uint4* pk;       // node packets (k_pack_nodes): 32 B per node, its word and its children's
   const float4* ltris;   // leaf-ordered triangle copies (k_gather_leaf_tris): 3 float4 per leaf-list entry
   const uint32_t* leaf;  // leaf primitive lists
   const float4* ng;      // geometric normal xyz, w = material id | kSmoothBit (int bits)
@@ -418,53 +418,34 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
 // Results, node and triangle-test counts are therefore those of the per-lane
 // loop, bit for bit.
 
-// Empty-leaf skipping (YK_SKIP_EMPTY). 43.6 % of the reference tree's leaves
-// are empty (1M probe). k_flag_nodes gives every interior node two bits that
-// say whether its left / right child is an empty leaf, so the traversal visits
-// such a leaf without loading it, and reproduces what the reference does there
-// (kdtree.cc:707-811 with nPrimitives == 0): count the node, run the
-// closest-hit exit test `hit && Z <= exit.t`, pop. In particular
-//  * an empty NEAR child whose far sibling is pushed: the near leaf's exit is
-//    the split point, and the pop makes that point the far child's entry -- so
-//    the descent tests `Z <= t_split` and `dist < t_split` (the entry test of
-//    the next iteration) and walks straight on into the far child, with the
-//    entry moved to the split point exactly as push + pop would compute it;
-//  * an empty FAR child is still pushed (its split point is the near subtree's
-//    exit, which steers that subtree's decisions) but marked (bit 29 of the
-//    entry), and trav_next pops through it: entry test, count, exit test.
-// Results and node / triangle-test counts equal the unskipped traversal's.
-// Measured on the 1M frame (tools/gpu_ab.sh, Mrays/s, off = 2497): all on
-// 2185; near walk-through only 2072; far marks only 2394; neither (the empty
-// leaf only not loaded) 2492. Lanes that keep descending past an empty leaf
-// or pop through marked entries stretch the wave's iteration while the other
-// lanes wait, which costs more than the skipped iterations save; so it is off.
-#ifndef YK_SKIP_EMPTY
-#define YK_SKIP_EMPTY 0
+// Node packets (YK_PACKETS): 32 B per node X holding X's own 8-B word and
+// those of its two children (left = X + 1, right), built by k_pack_nodes. One
+// load then serves two levels of the descent: the decision at X picks the near
+// child, whose word is already in registers, and the decision there picks the
+// next packet to load. Every lane of a wave advances two levels per memory
+// round trip, which a pair-reuse scheme (round 1: +2 %, round 2: -1 %) cannot
+// promise -- a wave waits for its slowest lane's load. 109 MB on the 1M probe.
+// (Empty-leaf skipping -- parent bits marking empty children, walked through
+// or popped through without loads -- measured 2185 / 2072 / 2394 Mrays/s
+// against 2497 without: lanes that keep going stretch the wave's iteration.)
+#ifndef YK_PACKETS
+#define YK_PACKETS 1
 #endif
-#ifndef YK_SKIP_NEAR
-#define YK_SKIP_NEAR 1  // walk through an empty near leaf into the far child
-#endif
-#ifndef YK_SKIP_FAR
-#define YK_SKIP_FAR 1  // mark empty far children and pop through them
-#endif
-constexpr bool kSkipEmpty = YK_SKIP_EMPTY != 0;
-constexpr uint32_t kEmptyMark = 1u << 29;  // stack entry: the far node is an empty leaf
-constexpr uint32_t kNodeField = kEmptyMark - 1u;
-
-// traversal node encoding (k_flag_nodes): leaves as in kdtree_build.h;
-// interior word1 = axis | left empty << 2 | right empty << 3 | right << 4
-__global__ void k_flag_nodes(const uint2* __restrict__ in, uint2* __restrict__ out, unsigned n) {
+constexpr bool kPackets = YK_PACKETS != 0;
+__global__ void k_pack_nodes(const uint2* __restrict__ nodes, uint4* __restrict__ pk, unsigned n) {
   const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint2 w = in[i];
+  const uint2 w = nodes[i];
+  uint4 p0 = make_uint4(w.x, w.y, 0u, 0u), p1 = make_uint4(0u, 0u, 0u, 0u);
   if ((w.y & 3u) != 3u) {
-    const uint32_t right = w.y >> 2;
-    // an empty leaf's word1 is 3 | 0 << 2
-    const uint32_t le = (YK_SKIP_EMPTY && in[i + 1].y == 3u) ? 4u : 0u;
-    const uint32_t re = (YK_SKIP_EMPTY && in[right].y == 3u) ? 8u : 0u;
-    w.y = (w.y & 3u) | le | re | (right << 4);
+    const uint2 l = nodes[i + 1], r = nodes[w.y >> 2];
+    p0.z = l.x;
+    p0.w = l.y;
+    p1.x = r.x;
+    p1.y = r.y;
   }
-  out[i] = w;
+  pk[2 * (size_t)i] = p0;
+  pk[2 * (size_t)i + 1] = p1;
 }
 
 // Leaf-ordered triangles (YK_LEAF_TRIS): a copy of every leaf-list entry's
@@ -489,9 +470,40 @@ __global__ void k_gather_leaf_tris(const float4* __restrict__ tris, const uint32
   out[3 * (size_t)i + 2] = tris[3 * (size_t)p + 2];
 }
 
+// One descent decision at interior node `node` (word nd, axis ax): the near /
+// far choice of kdtree.cc:711-761 plus the push of the far child (exit :=
+// split point). Returns the near child.
+__device__ __forceinline__ uint32_t desc_decide(Trav& st, const LaneStack& stk, uint2 nd, uint32_t node,
+                                                uint32_t ax) {
+  const float split = __uint_as_float(nd.x);
+  const uint32_t right = nd.y >> 2;
+  const bool a0 = ax == 0u, a1 = ax == 1u;
+  const float enp = sel3m(st.en_pb, a0, a1), exq = sel3m(st.ex_pb, a0, a1);
+  const bool left_first = enp <= split;
+  // far child pushed unless the exit stays on the near side; evaluated on
+  // wave masks (SALU) instead of per-lane 0/1 selects
+  const unsigned long long m_lf = __builtin_amdgcn_ballot_w64(left_first);
+  const unsigned long long m_c1 = __builtin_amdgcn_ballot_w64(exq <= split);
+  const unsigned long long m_c2 = __builtin_amdgcn_ballot_w64(split < exq);
+  const bool push = __builtin_amdgcn_inverse_ballot_w64((m_lf & ~m_c1) | (~m_lf & ~m_c2));
+  if (push) {
+    const uint32_t far_ = left_first ? right : node + 1u;
+    const float t = (split - sel3m(st.o, a0, a1)) * sel3m(st.inv, a0, a1);
+    stk.push(st.sp, make_uint2(__float_as_uint(st.ex_split), st.ex_w));
+    st.sp++;
+    st.ex_t = t;
+    st.ex_split = split;
+    st.ex_w = (far_ + 1u) | (ax << 30);
+    // exit point (exit_pb with the axis masks at hand)
+    const v3 o = st.o, d = st.d;
+    const float x = o.x + t * d.x, y = o.y + t * d.y, z = o.z + t * d.z;
+    st.ex_pb = V3(a0 ? split : x, a1 ? split : y, (a0 || a1) ? z : split);
+  }
+  return left_first ? node + 1u : right;
+}
+
 // Descends from st.node to a leaf (the descent of trav_step); false when the
-// ray is finished (dist < entry t, or the exit tests of a skipped empty
-// leaf). Outputs the leaf's w0 and count.
+// ray is already finished (dist < entry t). Outputs the leaf's w0 and count.
 template <bool CLOSEST>
 __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const LaneStack& stk, unsigned& nnodes,
                                              uint32_t& w0, uint32_t& nref, bool& paused) {
@@ -499,12 +511,18 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
   if (st.dist < st.en_t) return false;
   // node indices are unsigned 32-bit offsets from the uniform node pointer
   // (one address VALU per load: base in SGPRs, 32-bit lane offset)
-  const char* nbase = reinterpret_cast<const char*>(S.tnodes);
+  const char* nbase = reinterpret_cast<const char*>(kPackets ? (const void*)S.pk : (const void*)S.nodes);
   uint32_t node = (uint32_t)st.node;
-  uint2 nd = *reinterpret_cast<const uint2*>(nbase + (node << 3));
+  uint4 p0, p1;
+  uint2 nd;
+  if (kPackets) {
+    p0 = *reinterpret_cast<const uint4*>(nbase + ((size_t)node << 5));
+    p1 = *reinterpret_cast<const uint4*>(nbase + ((size_t)node << 5) + 16);
+    nd = make_uint2(p0.x, p0.y);
+  } else {
+    nd = *reinterpret_cast<const uint2*>(nbase + (node << 3));
+  }
   nnodes++;
-  // (round 1's node-pair reuse -- a left descent taking the sibling word of
-  // the previous 16-B load -- measured -1 % here)
   uint32_t ax = nd.y & 3u;
 #ifndef YK_DESC_FRAC
 #define YK_DESC_FRAC 4  // measured 2 / 3 / 4 / 8: 2477 / 2524 / 2527 / 2450 Mrays/s (off: 2344)
@@ -515,73 +533,41 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
   // to its longest descent while the other lanes idle
   const unsigned started = YK_DESC_FRAC ? (unsigned)__popcll(__builtin_amdgcn_ballot_w64(true)) : 0u;
   // wave-uniform loop: the exit test is a ballot, and lanes whose descent
-  // ended sit out the body under the exec mask (a divergent loop exit makes
-  // the compiler copy the descent's live-out registers every step)
-  bool desc = ax != 3u, fin = false;
+  // ended sit out the body under the exec mask. (A divergent loop exit makes
+  // the compiler copy the descent's live-out registers every step, 13 of ~27
+  // VALU ops; removing them measured equal: the loop waits on its loads.)
+  bool desc = ax != 3u;
   for (;;) {
     const unsigned long long m = __builtin_amdgcn_ballot_w64(desc);
     if (m == 0ull) break;
     if (YK_DESC_FRAC && (unsigned)__popcll(m) * YK_DESC_FRAC < started) break;
-    if (desc) {
-      const float split = __uint_as_float(nd.x);
-      const uint32_t right = kSkipEmpty ? nd.y >> 4 : nd.y >> 2;
-      const bool a0 = ax == 0u, a1 = ax == 1u;
-      const float enp = sel3m(st.en_pb, a0, a1), exq = sel3m(st.ex_pb, a0, a1);
-      const bool left_first = enp <= split;
-      // far child pushed unless the exit stays on the near side; evaluated on
-      // wave masks (SALU) instead of per-lane 0/1 selects
-      const unsigned long long m_lf = __builtin_amdgcn_ballot_w64(left_first);
-      const unsigned long long m_c1 = __builtin_amdgcn_ballot_w64(exq <= split);
-      const unsigned long long m_c2 = __builtin_amdgcn_ballot_w64(split < exq);
-      const bool push = __builtin_amdgcn_inverse_ballot_w64((m_lf & ~m_c1) | (~m_lf & ~m_c2));
-      const bool le = kSkipEmpty && (nd.y & 4u) != 0u, re = kSkipEmpty && (nd.y & 8u) != 0u;
-      uint32_t nxt = left_first ? node + 1u : right;
-      bool nxt_empty = left_first ? le : re;
-      if (push) {
-        const uint32_t far_ = left_first ? right : node + 1u;
-        const bool far_empty = left_first ? re : le;
-        const float t = (split - sel3m(st.o, a0, a1)) * sel3m(st.inv, a0, a1);
-        // the split point (exit_pb with the axis masks at hand)
-        const v3 o = st.o, d = st.d;
-        const float x = o.x + t * d.x, y = o.y + t * d.y, z = o.z + t * d.z;
-        const v3 spt = V3(a0 ? split : x, a1 ? split : y, (a0 || a1) ? z : split);
-        if (YK_SKIP_NEAR && nxt_empty) {
-          // empty near leaf: visited, exit test at the split point, then the
-          // far child entered there (no push / pop)
-          nnodes++;
-          if ((CLOSEST && st.prim >= 0 && st.Z <= t) || st.dist < t) {
-            fin = true;
-          } else {
-            st.en_t = t;
-            st.en_pb = spt;
-            nxt = far_;
-            nxt_empty = far_empty;
-          }
-        } else {
-          stk.push(st.sp, make_uint2(__float_as_uint(st.ex_split), st.ex_w));
-          st.sp++;
-          st.ex_t = t;
-          st.ex_split = split;
-          st.ex_w = (far_ + 1u) | ((YK_SKIP_FAR && far_empty) ? kEmptyMark : 0u) | (ax << 30);
-          st.ex_pb = spt;
-        }
-      }
-      if (fin) {
-        desc = false;
-      } else {
-        if (nxt_empty) {  // an empty leaf: known from the parent, not loaded
-          nd = make_uint2(0u, 3u);
-        } else {
-          nd = *reinterpret_cast<const uint2*>(nbase + (nxt << 3));
-        }
+    if (!desc) continue;
+    uint32_t nxt = desc_decide(st, stk, nd, node, ax);
+    if (kPackets) {
+      // the near child's word is in the packet: decide there too (unless it
+      // is a leaf), then load the packet of the node that decision picks
+      const bool left = nxt == node + 1u;
+      nd = left ? make_uint2(p0.z, p0.w) : make_uint2(p1.x, p1.y);
+      node = nxt;
+      nnodes++;
+      ax = nd.y & 3u;
+      if (ax != 3u) {
+        nxt = desc_decide(st, stk, nd, node, ax);
+        p0 = *reinterpret_cast<const uint4*>(nbase + ((size_t)nxt << 5));
+        p1 = *reinterpret_cast<const uint4*>(nbase + ((size_t)nxt << 5) + 16);
+        nd = make_uint2(p0.x, p0.y);
         node = nxt;
         nnodes++;
         ax = nd.y & 3u;
-        desc = ax != 3u;
       }
+    } else {
+      nd = *reinterpret_cast<const uint2*>(nbase + (nxt << 3));
+      node = nxt;
+      nnodes++;
+      ax = nd.y & 3u;
     }
+    desc = ax != 3u;
   }
-  if (fin) return false;
   if (desc) {  // paused: resumes at this node in the next iteration
     paused = true;
     st.node = (int)node;
@@ -593,33 +579,27 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
   return true;
 }
 
-// After the leaf: the closest-hit stop test, then pop (kdtree.cc:802-812),
-// through any marked empty far leaves (their whole iteration: entry test,
-// node count, exit test). True when the ray is finished.
+// After the leaf: the closest-hit stop test, then pop (kdtree.cc:802-812).
+// True when the ray is finished.
 template <bool CLOSEST>
-__device__ __forceinline__ bool trav_next(const DScene& S, Trav& st, const LaneStack& stk, unsigned& nnodes) {
-  for (;;) {
-    if (CLOSEST && st.prim >= 0 && st.Z <= st.ex_t) return true;
-    st.en_t = st.ex_t;
-    st.en_pb = st.ex_pb;
-    const bool empty = (st.ex_w & kEmptyMark) != 0u;
-    st.node = (int)(st.ex_w & kNodeField) - 1;
-    if (st.node < 0) return true;
-    if ((unsigned)st.node >= S.nnodes || st.sp <= 0) {  // corrupt state: never index out of the tree
-      st.prim = -2;
-      return true;
-    }
-    st.sp--;
-    const uint2 e = stk.pop(st.sp);
-    st.ex_split = __uint_as_float(e.x);
-    st.ex_w = e.y;
-    const uint32_t code = e.y >> 30;
-    st.ex_t = (code == 3u) ? st.ex_split : (st.ex_split - sel3(st.o, code)) * sel3(st.inv, code);
-    exit_pb(st);
-    if (!kSkipEmpty || !empty) return false;
-    if (st.dist < st.en_t) return true;
-    nnodes++;
+__device__ __forceinline__ bool trav_next(const DScene& S, Trav& st, const LaneStack& stk) {
+  if (CLOSEST && st.prim >= 0 && st.Z <= st.ex_t) return true;
+  st.en_t = st.ex_t;
+  st.en_pb = st.ex_pb;
+  st.node = (int)(st.ex_w & 0x3FFFFFFFu) - 1;
+  if (st.node < 0) return true;
+  if ((unsigned)st.node >= S.nnodes || st.sp <= 0) {  // corrupt state: never index out of the tree
+    st.prim = -2;
+    return true;
   }
+  st.sp--;
+  const uint2 e = stk.pop(st.sp);
+  st.ex_split = __uint_as_float(e.x);
+  st.ex_w = e.y;
+  const uint32_t code = e.y >> 30;
+  st.ex_t = (code == 3u) ? st.ex_split : (st.ex_split - sel3(st.o, code)) * sel3(st.inv, code);
+  exit_pb(st);
+  return false;
 }
 
 // total-order key of a float (for t >= 0 the raw bits; -0 is made +0 first so
@@ -879,7 +859,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       bool occ = false;
       coop_leaves<CLOSEST>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, ntris, occ);
       if (act) {
-        bool done = !live || occ || (!paused && trav_next<CLOSEST>(S, st, stk, nnodes));
+        bool done = !live || occ || (!paused && trav_next<CLOSEST>(S, st, stk));
         if (runaway) {
           st.prim = -2;
           done = true;
@@ -2533,7 +2513,7 @@ struct yk_device {
   DBuf<float4> tris, ng;
   DBuf<float> vn;  // smooth-shading vertex normals (9 per prim), only when the scene has smooth meshes
   DBuf<uint2> nodes;
-  DBuf<uint2> tnodes;  // traversal encoding (k_flag_nodes), rebuilt whenever nodes change
+  DBuf<uint4> pk;      // node packets (k_pack_nodes), rebuilt whenever nodes change
   DBuf<float4> ltris;  // leaf-ordered triangle copies, rebuilt whenever the leaf lists change
   DBuf<uint32_t> leaf;
   DScene S{};
@@ -2848,29 +2828,24 @@ void launch_trace(yk_device* d, Pipe& P, const yk_ray* rays, long long n, yk_hit
 inline unsigned grid_for(long long n, int b = 256) { return (unsigned)((n + b - 1) / b); }
 
 // Traversal copies of the resident tree: the leaf-ordered triangles
-// (k_gather_leaf_tris) and the node array in k_flag_nodes' encoding (node
-// indices must fit 28 bits in its word1 and leave bit 29 of a stack entry free).
+// (k_gather_leaf_tris) and the node packets (k_pack_nodes).
 void install_traversal(yk_device* d, size_t nn, size_t nleaf) {
+  HIPCHK(hipDeviceSynchronize());  // every copy into nodes / leaf / tris has landed
   if (kLeafTris && nleaf) {
     d->ltris.ensure(3 * nleaf);
     hipLaunchKernelGGL(k_gather_leaf_tris, dim3(grid_for((long long)nleaf)), dim3(256), 0, d->stream, d->tris.p,
                        d->leaf.p, d->ltris.p, (unsigned)nleaf);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(d->stream));
   }
   d->S.ltris = (kLeafTris && nleaf) ? d->ltris.p : nullptr;
-  if (!kSkipEmpty) {  // the plain encoding serves
-    d->S.tnodes = d->nodes.p;
-    return;
+  if (kPackets) {
+    d->pk.ensure(2 * nn);
+    hipLaunchKernelGGL(k_pack_nodes, dim3(grid_for((long long)nn)), dim3(256), 0, d->stream, d->nodes.p, d->pk.p,
+                       (unsigned)nn);
+    HIPCHK(hipGetLastError());
   }
-  if (nn >= (1u << 28)) throw std::invalid_argument("kd-tree has 2^28 nodes or more (traversal encoding limit)");
-  d->tnodes.ensure(nn + 1);
-  HIPCHK(hipMemset(d->tnodes.p + nn, 0, sizeof(uint2)));
-  hipLaunchKernelGGL(k_flag_nodes, dim3(grid_for((long long)nn)), dim3(256), 0, d->stream, d->nodes.p, d->tnodes.p,
-                     (unsigned)nn);
-  HIPCHK(hipGetLastError());
+  d->S.pk = kPackets ? d->pk.p : nullptr;
   HIPCHK(hipStreamSynchronize(d->stream));
-  d->S.tnodes = d->tnodes.p;
 }
 
 }  // namespace
