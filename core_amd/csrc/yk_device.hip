@@ -85,10 +85,10 @@ __constant__ DCam c_cam;
 
 constexpr int kSmoothBit = 0x10000;  // prim interpolates vertex normals (mesh is_smooth)
 struct DScene {
-  const float4* tris;    // 3 float4 per prim: a, e1=b-a, e2=c-a
+  const float* tris;     // triangle records (kTriWords floats per prim): a, prim id, e1=b-a, e2=c-a
   const uint2* nodes;    // kd nodes (kdtree_build.h encoding)
-  const uint4* pk;       // node packets (k_pack_nodes): 32 B per node, its word and its children's
-  const float4* ltris;   // leaf-ordered triangle copies (k_gather_leaf_tris): 3 float4 per leaf-list entry
+  const uint32_t* pk;    // node packets (k_pack_nodes): YK_PK_BYTES per node, its word and its children's
+  const float* ltris;    // leaf-ordered copies of the records (k_gather_leaf_tris), one per leaf-list entry
   const uint32_t* leaf;  // leaf primitive lists
   const float4* ng;      // geometric normal xyz, w = material id | kSmoothBit (int bits)
   const float* vn;       // 9 floats per prim: getSurface's vertex normals (smooth scenes only)
@@ -98,6 +98,29 @@ struct DScene {
 };
 
 __device__ __forceinline__ v3 ld3(const float* p) { return V3(p[0], p[1], p[2]); }
+
+// Triangle record (YK_TRI_BYTES): the Moller-Trumbore inputs a, e1 = b - a,
+// e2 = c - a (the reference's own subtractions) and the primitive id.
+//   48 B: (a, id) (e1, 0) (e2, 0) -- three aligned 16-B loads
+//   40 B: (a, id) (e1, e2.x) (e2.y, e2.z) -- 16 + 16 + 8 B loads, 17 % less
+//         footprint for the records the traversal streams through L2 / MALL
+#ifndef YK_TRI_BYTES
+#define YK_TRI_BYTES 48  // measured 48 / 40: 2752 / 2756 Mrays/s (within noise)
+#endif
+static_assert(YK_TRI_BYTES == 48 || YK_TRI_BYTES == 40, "triangle record is 40 or 48 bytes");
+constexpr unsigned kTriWords = YK_TRI_BYTES / 4;
+__device__ __forceinline__ void ld_tri(const float* rec, float4& A, float4& E1, float4& E2) {
+  A = *reinterpret_cast<const float4*>(rec);
+  if (kTriWords == 12) {
+    E1 = *reinterpret_cast<const float4*>(rec + 4);
+    E2 = *reinterpret_cast<const float4*>(rec + 8);
+  } else {
+    const float4 q = *reinterpret_cast<const float4*>(rec + 4);
+    const float2 r = *reinterpret_cast<const float2*>(rec + 8);
+    E1 = make_float4(q.x, q.y, q.z, 0.f);
+    E2 = make_float4(q.w, r.x, r.y, 0.f);
+  }
+}
 
 struct SurfPt {
   v3 P, N, Ng, NU, NV;
@@ -349,7 +372,8 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
     for (uint32_t i = 0; i < n; ++i) {
       const uint32_t p = (n == 1) ? w0 : S.leaf[w0 + i];
       ntris++;
-      float4 A = S.tris[3 * p], E1 = S.tris[3 * p + 1], E2 = S.tris[3 * p + 2];
+      float4 A, E1, E2;
+      ld_tri(S.tris + (size_t)p * kTriWords, A, E1, E2);
       // keep the three loads together (the compiler would otherwise sink A's
       // load past the det test: a second dependent round trip per triangle)
       asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
@@ -358,15 +382,14 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
     }
   } else if (n > 0) {
     uint32_t p = (n == 1) ? w0 : S.leaf[w0];
-    float4 A = S.tris[3 * p], E1 = S.tris[3 * p + 1], E2 = S.tris[3 * p + 2];
+    float4 A, E1, E2;
+    ld_tri(S.tris + (size_t)p * kTriWords, A, E1, E2);
     uint32_t pn = (n > 1) ? S.leaf[w0 + 1] : 0u;
     for (uint32_t i = 0; i < n; ++i) {
       float4 An = A, E1n = E1, E2n = E2;
       uint32_t pnn = 0u;
       if (i + 1 < n) {
-        An = S.tris[3 * pn];
-        E1n = S.tris[3 * pn + 1];
-        E2n = S.tris[3 * pn + 2];
+        ld_tri(S.tris + (size_t)pn * kTriWords, An, E1n, E2n);
       }
       if (i + 2 < n) pnn = S.leaf[w0 + i + 2];
       asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
@@ -432,20 +455,32 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
 #define YK_PACKETS 1
 #endif
 constexpr bool kPackets = YK_PACKETS != 0;
-__global__ void k_pack_nodes(const uint2* __restrict__ nodes, uint4* __restrict__ pk, unsigned n) {
+// packet stride: 32 B (two aligned 16-B loads) or 24 B (a 16-B and an 8-B
+// load; 25 % less footprint in the 256 MB Infinity Cache)
+#ifndef YK_PK_BYTES
+#define YK_PK_BYTES 24  // measured 32 / 24: 2765 / 2786 Mrays/s
+#endif
+static_assert(YK_PK_BYTES == 32 || YK_PK_BYTES == 24, "packet stride is 24 or 32 bytes");
+constexpr unsigned kPkWords = YK_PK_BYTES / 4;
+// packet of node i: p0 = (word of i, word of its left child), r = right child's word
+__device__ __forceinline__ void ld_packet(const char* base, uint32_t i, uint4& p0, uint2& r) {
+  const char* a = base + (size_t)i * YK_PK_BYTES;
+  p0 = *reinterpret_cast<const uint4*>(a);
+  r = *reinterpret_cast<const uint2*>(a + 16);
+}
+__global__ void k_pack_nodes(const uint2* __restrict__ nodes, uint32_t* __restrict__ pk, unsigned n) {
   const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint2 w = nodes[i];
-  uint4 p0 = make_uint4(w.x, w.y, 0u, 0u), p1 = make_uint4(0u, 0u, 0u, 0u);
+  uint2 l = make_uint2(0u, 0u), r = make_uint2(0u, 0u);
   if ((w.y & 3u) != 3u) {
-    const uint2 l = nodes[i + 1], r = nodes[w.y >> 2];
-    p0.z = l.x;
-    p0.w = l.y;
-    p1.x = r.x;
-    p1.y = r.y;
+    l = nodes[i + 1];
+    r = nodes[w.y >> 2];
   }
-  pk[2 * (size_t)i] = p0;
-  pk[2 * (size_t)i + 1] = p1;
+  uint32_t* o = pk + (size_t)i * kPkWords;
+  *reinterpret_cast<uint4*>(o) = make_uint4(w.x, w.y, l.x, l.y);
+  *reinterpret_cast<uint2*>(o + 4) = r;
+  if (kPkWords == 8) *reinterpret_cast<uint2*>(o + 6) = make_uint2(0u, 0u);
 }
 
 // Leaf-ordered triangles (YK_LEAF_TRIS): a copy of every leaf-list entry's
@@ -458,16 +493,15 @@ __global__ void k_pack_nodes(const uint2* __restrict__ nodes, uint4* __restrict_
 #define YK_LEAF_TRIS 1
 #endif
 constexpr bool kLeafTris = YK_LEAF_TRIS != 0;
-__global__ void k_gather_leaf_tris(const float4* __restrict__ tris, const uint32_t* __restrict__ leaf,
-                                   float4* __restrict__ out, unsigned n) {
+__global__ void k_gather_leaf_tris(const float* __restrict__ tris, const uint32_t* __restrict__ leaf,
+                                   float* __restrict__ out, unsigned n) {
   const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint32_t p = leaf[i];
-  float4 A = tris[3 * (size_t)p];
-  A.w = __uint_as_float(p);
-  out[3 * (size_t)i] = A;
-  out[3 * (size_t)i + 1] = tris[3 * (size_t)p + 1];
-  out[3 * (size_t)i + 2] = tris[3 * (size_t)p + 2];
+  const float* src = tris + (size_t)leaf[i] * kTriWords;
+  float* dst = out + (size_t)i * kTriWords;
+#pragma unroll
+  for (unsigned w = 0; w < kTriWords; w += 2)
+    *reinterpret_cast<float2*>(dst + w) = *reinterpret_cast<const float2*>(src + w);
 }
 
 // One descent decision at interior node `node` (word nd, axis ax): the near /
@@ -513,11 +547,10 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
   // (one address VALU per load: base in SGPRs, 32-bit lane offset)
   const char* nbase = reinterpret_cast<const char*>(kPackets ? (const void*)S.pk : (const void*)S.nodes);
   uint32_t node = (uint32_t)st.node;
-  uint4 p0, p1;
-  uint2 nd;
+  uint4 p0;
+  uint2 p1, nd;
   if (kPackets) {
-    p0 = *reinterpret_cast<const uint4*>(nbase + ((size_t)node << 5));
-    p1 = *reinterpret_cast<const uint4*>(nbase + ((size_t)node << 5) + 16);
+    ld_packet(nbase, node, p0, p1);
     nd = make_uint2(p0.x, p0.y);
   } else {
     nd = *reinterpret_cast<const uint2*>(nbase + (node << 3));
@@ -547,14 +580,13 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
       // the near child's word is in the packet: decide there too (unless it
       // is a leaf), then load the packet of the node that decision picks
       const bool left = nxt == node + 1u;
-      nd = left ? make_uint2(p0.z, p0.w) : make_uint2(p1.x, p1.y);
+      nd = left ? make_uint2(p0.z, p0.w) : p1;
       node = nxt;
       nnodes++;
       ax = nd.y & 3u;
       if (ax != 3u) {
         nxt = desc_decide(st, stk, nd, node, ax);
-        p0 = *reinterpret_cast<const uint4*>(nbase + ((size_t)nxt << 5));
-        p1 = *reinterpret_cast<const uint4*>(nbase + ((size_t)nxt << 5) + 16);
+        ld_packet(nbase, nxt, p0, p1);
         nd = make_uint2(p0.x, p0.y);
         node = nxt;
         nnodes++;
@@ -666,15 +698,16 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
     float th = 0.f, u = 0.f, v = 0.f;
     uint32_t p = 0;
     if (s < total) {
-      const float4* tp;
-      if (kLeafTris) {  // one load: the leaf's own triangle copy (prim id in A.w)
-        tp = (on == 1u) ? S.tris + 3 * (size_t)ow0 : S.ltris + 3 * (size_t)(ow0 + k);
+      const float* tp;
+      if (kLeafTris) {  // one load: the leaf's own record (prim id in A.w)
+        tp = (on == 1u) ? S.tris + (size_t)ow0 * kTriWords : S.ltris + (size_t)(ow0 + k) * kTriWords;
       } else {
         p = (on == 1u) ? ow0 : S.leaf[ow0 + k];
-        tp = S.tris + 3 * (size_t)p;
+        tp = S.tris + (size_t)p * kTriWords;
       }
-      float4 A = tp[0], E1 = tp[1], E2 = tp[2];
-      if (kLeafTris) p = (on == 1u) ? ow0 : __float_as_uint(A.w);
+      float4 A, E1, E2;
+      ld_tri(tp, A, E1, E2);
+      if (kLeafTris) p = __float_as_uint(A.w);
       asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
                    "+v"(E2.y), "+v"(E2.z));
       if (mt_intersect(V3(A.x, A.y, A.z), V3(E1.x, E1.y, E1.z), V3(E2.x, E2.y, E2.z), ro, rd, th, u, v)) {
@@ -2510,11 +2543,12 @@ struct yk_device {
   uint64_t uploaded_gen = 0;                 // its Scene::generation at upload
   size_t nleaf = 0;                          // leaf-list entries of the resident tree
   // scene
-  DBuf<float4> tris, ng;
+  DBuf<float> tris;  // triangle records (kTriWords floats per prim)
+  DBuf<float4> ng;
   DBuf<float> vn;  // smooth-shading vertex normals (9 per prim), only when the scene has smooth meshes
   DBuf<uint2> nodes;
-  DBuf<uint4> pk;      // node packets (k_pack_nodes), rebuilt whenever nodes change
-  DBuf<float4> ltris;  // leaf-ordered triangle copies, rebuilt whenever the leaf lists change
+  DBuf<uint32_t> pk;   // node packets (k_pack_nodes), rebuilt whenever nodes change
+  DBuf<float> ltris;  // leaf-ordered record copies, rebuilt whenever the leaf lists change
   DBuf<uint32_t> leaf;
   DScene S{};
   int ntris = 0, max_depth = 0, nlights = 0, sum_light_slots = 0;
@@ -2832,14 +2866,14 @@ inline unsigned grid_for(long long n, int b = 256) { return (unsigned)((n + b - 
 void install_traversal(yk_device* d, size_t nn, size_t nleaf) {
   HIPCHK(hipDeviceSynchronize());  // every copy into nodes / leaf / tris has landed
   if (kLeafTris && nleaf) {
-    d->ltris.ensure(3 * nleaf);
+    d->ltris.ensure(kTriWords * nleaf);
     hipLaunchKernelGGL(k_gather_leaf_tris, dim3(grid_for((long long)nleaf)), dim3(256), 0, d->stream, d->tris.p,
                        d->leaf.p, d->ltris.p, (unsigned)nleaf);
     HIPCHK(hipGetLastError());
   }
   d->S.ltris = (kLeafTris && nleaf) ? d->ltris.p : nullptr;
   if (kPackets) {
-    d->pk.ensure(2 * nn);
+    d->pk.ensure(kPkWords * nn);
     hipLaunchKernelGGL(k_pack_nodes, dim3(grid_for((long long)nn)), dim3(256), 0, d->stream, d->nodes.p, d->pk.p,
                        (unsigned)nn);
     HIPCHK(hipGetLastError());
@@ -2913,12 +2947,23 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   YK_GUARD_BEGIN
   HIPCHK(hipSetDevice(d->ordinal));
   const int nt = (int)S.tri_material.size();
-  std::vector<float4> tris((size_t)nt * 3), ng(nt);
+  std::vector<float> tris((size_t)nt * kTriWords, 0.f);
+  std::vector<float4> ng(nt);
   for (int p = 0; p < nt; ++p) {
     const float* t = &S.tri_verts[9 * (size_t)p];
-    tris[3 * p] = make_float4(t[0], t[1], t[2], 0.f);
-    tris[3 * p + 1] = make_float4(t[3] - t[0], t[4] - t[1], t[5] - t[2], 0.f);
-    tris[3 * p + 2] = make_float4(t[6] - t[0], t[7] - t[1], t[8] - t[2], 0.f);
+    float* r = &tris[(size_t)p * kTriWords];
+    const float e[6] = {t[3] - t[0], t[4] - t[1], t[5] - t[2], t[6] - t[0], t[7] - t[1], t[8] - t[2]};
+    r[0] = t[0];
+    r[1] = t[1];
+    r[2] = t[2];
+    const uint32_t pid = (uint32_t)p;
+    std::memcpy(&r[3], &pid, 4);
+    // e1 at words 4-6; e2 at 8-10 (48 B) or 7-9 (40 B)
+    const int e2at = kTriWords == 12 ? 8 : 7;
+    for (int k = 0; k < 3; ++k) {
+      r[4 + k] = e[k];
+      r[e2at + k] = e[3 + k];
+    }
     float nw;
     int m = S.tri_material[p] | (S.tri_smooth[p] ? kSmoothBit : 0);
     std::memcpy(&nw, &m, 4);
@@ -2930,7 +2975,7 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   d->nodes.ensure(nn + 1);  // + one padding node for the node-pair loads
   HIPCHK(hipMemset(d->nodes.p + nn, 0, sizeof(uint2)));
   d->leaf.ensure(std::max<size_t>(S.tree.leaf_prims.size(), 1));
-  HIPCHK(hipMemcpy(d->tris.p, tris.data(), tris.size() * sizeof(float4), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d->tris.p, tris.data(), tris.size() * sizeof(float), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d->ng.p, ng.data(), ng.size() * sizeof(float4), hipMemcpyHostToDevice));
   if (S.any_smooth) {
     d->vn.ensure(S.tri_vnormal.size());
