@@ -641,11 +641,33 @@ __device__ __forceinline__ uint32_t ord_key(float t) {
   return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
 }
 
+// Owner of a pair slot (YK_OWNER_SCAN): lanes whose reference range starts in
+// the round's 64 slots write ((range start + 1) << 8 | lane) at that slot of an LDS
+// table, and an inclusive max-scan over the table (DPP, seeded with the
+// previous round's last owner) gives every slot the lane whose range covers it
+// -- one LDS write / read and six VALU steps instead of a six-step binary
+// search of dependent cross-lane reads.
+#ifndef YK_OWNER_SCAN
+#define YK_OWNER_SCAN 1
+#endif
+constexpr bool kOwnerScan = YK_OWNER_SCAN != 0;
+__device__ __forceinline__ unsigned dpp_max_scan(unsigned x) {
+  // row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15 / 31; lanes whose
+  // source is out of range keep their value (old = x, max is idempotent)
+  x = max(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x111, 0xf, 0xf, false));
+  x = max(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x112, 0xf, 0xf, false));
+  x = max(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x114, 0xf, 0xf, false));
+  x = max(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x118, 0xf, 0xf, false));
+  x = max(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x142, 0xa, 0xf, false));
+  x = max(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x143, 0xc, 0xf, false));
+  return x;
+}
+
 // Wave-uniform: every lane calls it; nref = 0 for lanes without a leaf to test.
 template <bool CLOSEST>
 __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t nref, uint32_t w0, int lane,
-                                            unsigned long long* keys, float4* cand, unsigned& ntris,
-                                            bool& occluded) {
+                                            unsigned long long* keys, float4* cand, unsigned* otab,
+                                            unsigned& ntris, bool& occluded) {
   unsigned x = nref;  // inclusive prefix sum of the lanes' reference counts
 #ifndef YK_DPP_SCAN
 #define YK_DPP_SCAN 1
@@ -672,19 +694,33 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
   keys[lane] = ~0ull;
   __syncthreads();  // one wave per block: orders the LDS traffic of the phase
   const float zlim = CLOSEST ? st.Z : st.dist;
+  unsigned carry = 0u;  // ((start + 1) << 8 | lane) of the range covering the previous slot
   for (unsigned base = 0; base < total; base += 64u) {
     const unsigned s = base + (unsigned)lane;
     const unsigned sc = min(s, total - 1u);
     // owner of slot s: the last lane whose range starts at or before s
     int own = 0;
     unsigned pown = 0;
+    if (kOwnerScan) {  // keys hold 24-bit range starts: install_traversal caps leaves at 2^18 references
+      otab[lane] = 0u;
+      if (nref > 0u && pre >= base && pre - base < 64u) otab[pre - base] = ((pre + 1u) << 8) | (unsigned)lane;
+      __syncthreads();
+      const unsigned v = dpp_max_scan(otab[lane]);
+      // slots before the round's first range start continue the range that
+      // covered the previous round's last slot
+      const unsigned key = v ? v : carry;
+      carry = (unsigned)__builtin_amdgcn_readlane((int)key, 63);
+      own = (int)(key & 0xFFu);
+      pown = (key >> 8) - 1u;
+    } else {
 #pragma unroll
-    for (int step = 32; step > 0; step >>= 1) {
-      const int c = own + step;
-      const unsigned v = (unsigned)__shfl((int)pre, c);
-      if (v <= sc) {
-        own = c;
-        pown = v;
+      for (int step = 32; step > 0; step >>= 1) {
+        const int c = own + step;
+        const unsigned v = (unsigned)__shfl((int)pre, c);
+        if (v <= sc) {
+          own = c;
+          pown = v;
+        }
       }
     }
     const unsigned k = sc - pown;
@@ -884,13 +920,14 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
     if (COOP) {
       __shared__ unsigned long long keys[64];
       __shared__ float4 cand[CLOSEST ? 64 : 1];
+      __shared__ unsigned otab[kOwnerScan ? 64 : 1];
       const bool act = rid >= 0;
       bool live = false;
       uint32_t w0 = 0, nref = 0;
       bool paused = false;
       if (act) live = trav_descend<CLOSEST>(S, st, stk, nnodes, w0, nref, paused);
       bool occ = false;
-      coop_leaves<CLOSEST>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, ntris, occ);
+      coop_leaves<CLOSEST>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, otab, ntris, occ);
       if (act) {
         bool done = !live || occ || (!paused && trav_next<CLOSEST>(S, st, stk));
         if (runaway) {
@@ -2863,7 +2900,9 @@ inline unsigned grid_for(long long n, int b = 256) { return (unsigned)((n + b - 
 
 // Traversal copies of the resident tree: the leaf-ordered triangles
 // (k_gather_leaf_tris) and the node packets (k_pack_nodes).
-void install_traversal(yk_device* d, size_t nn, size_t nleaf) {
+void install_traversal(yk_device* d, size_t nn, size_t nleaf, uint32_t max_leaf_refs) {
+  if (kOwnerScan && max_leaf_refs >= (1u << 18))
+    throw std::invalid_argument("kd-tree leaf with 2^18 references or more (coop_leaves owner keys)");
   HIPCHK(hipDeviceSynchronize());  // every copy into nodes / leaf / tris has landed
   if (kLeafTris && nleaf) {
     d->ltris.ensure(kTriWords * nleaf);
@@ -3024,7 +3063,12 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   std::memcpy(d->S.bound, S.tree.bound, sizeof d->S.bound);
   d->S.nlights = (int)S.light_states.size();
   d->S.nnodes = (unsigned)nn;
-  install_traversal(d, nn, S.tree.leaf_prims.size());
+  {
+    uint32_t max_refs = 0;
+    for (size_t i = 0; i < nn; ++i)
+      if ((S.tree.nodes[2 * i + 1] & 3u) == 3u) max_refs = std::max(max_refs, S.tree.nodes[2 * i + 1] >> 2);
+    install_traversal(d, nn, S.tree.leaf_prims.size(), max_refs);
+  }
   {
     static const double crowd = [] {
       const char* e = std::getenv("YK_CROWDED_LEAF");
@@ -3271,14 +3315,20 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   constexpr long long kNodeBytes = 116;
   // batch = whole tiles, about YK_BATCH_SAMPLES camera samples (default 32M:
   // each trace launch ends in a tail of long rays, which large batches
-  // amortise), capped so the buffers of all pipes stay within ~64 GB of HBM
+  // amortise), capped so the buffers of all pipes stay within YK_BATCH_GB
   static const long long target_env = [] {
     const char* e = std::getenv("YK_BATCH_SAMPLES");
     const long long v = e ? std::atoll(e) : 0;
     return v > 0 ? v : (32ll << 20);
   }();
+  // HBM for the batch buffers of all pipes (YK_BATCH_GB, default 64 of the 288 GB)
+  static const long long batch_bytes = [] {
+    const char* e = std::getenv("YK_BATCH_GB");
+    const long long v = e ? std::atoll(e) : 0;
+    return (v > 0 && v <= 240 ? v : 64ll) << 30;
+  }();
   const long long bytes_per_sample = 400 + 52ll * K;
-  const long long target = std::max(1ll << 20, std::min(target_env, (64ll << 30) / kPipes / bytes_per_sample));
+  const long long target = std::max(1ll << 20, std::min(target_env, batch_bytes / kPipes / bytes_per_sample));
   const long long tile_samples = (long long)F.tile * F.tile * spp;
   if (d->spec && spec_worst * tile_samples * kNodeBytes > (48ll << 30))
     return set_error(YK_ERR_UNSUPPORTED, "raydepth too large for the tile size / spp (node store > 48 GB)");
