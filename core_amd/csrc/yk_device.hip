@@ -1403,6 +1403,11 @@ __device__ __forceinline__ bool dirac_illum(const DLight& L, v3 P, v3& ldir, flo
 #ifndef YK_APPEND_BLOCK
 #define YK_APPEND_BLOCK 512
 #endif
+// k_shade_bounce packs a block's hits onto its first threads (escaped paths
+// finish first)
+#ifndef YK_PACK_HITS
+#define YK_PACK_HITS 1
+#endif
 // Reserves m_s shadow-queue and m_b bounce-queue entries with ONE returning
 // atomic per wave: the counter word holds (bounce count << 32) | shadow
 // count. Whole-wave call; returns each lane's first index in both queues.
@@ -1945,17 +1950,17 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) YK_SHADE_ATTR k_shade_bounce(D
                                                       const unsigned long long* __restrict__ qin_word, int depth,
                                                       int isub, int qin, unsigned long long* __restrict__ qword) {
   const long long nq = (long long)(*qin_word >> 32);  // live paths (device-side count)
-  if ((long long)blockIdx.x * blockDim.x >= nq) return;  // whole block past the queue
-  const long long qi = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool valid = qi < nq;
-  const long long c = valid ? B.q_owner[qin][qi] : 0;
-  int nr = 0, kend = 0;
-  unsigned long long traced = 0;
-  bool emit_next = false;
-  yk_ray nxt;
-  if (valid) {
-    const yk_hit h = B.q_hits[qin][qi];
-    if (h.prim < 0) {
+  const long long qb = (long long)blockIdx.x * blockDim.x;
+  if (qb >= nq) return;  // whole block past the queue
+  long long qi = qb + threadIdx.x;
+  bool valid = qi < nq;
+  // Escaped paths (most first-bounce rays of an open scene) finish here; the
+  // block's hits are then packed onto its first threads, so the shading below
+  // runs on full waves instead of waves whose lanes mostly sit out.
+  {
+    const int prim = valid ? B.q_hits[qin][qi].prim : 0;
+    if (valid && prim < 0) {
+      const long long c = B.q_owner[qin][qi];
       // background: "continue" at depth 1, "break" later; a caustic segment
       // adds the background first (pathtracer.cc:279-286)
       if (R.spec && depth >= 2 && B.caus[c] && R.has_bg) {
@@ -1964,7 +1969,36 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) YK_SHADE_ATTR k_shade_bounce(D
         B.pathcol[3 * c + 2] = B.pathcol[3 * c + 2] + B.thr[3 * c + 2] * R.bg[2];
       }
       B.pstate[c] = 0;
-    } else {
+    }
+#if YK_PACK_HITS
+    __shared__ int s_q[YK_SHADE_BLOCK];
+    __shared__ int s_wn[YK_SHADE_BLOCK / 64];
+    const bool hit = valid && prim >= 0;
+    const unsigned long long hm = __ballot(hit);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) s_wn[w] = __popcll(hm);
+    __syncthreads();
+    int off = 0, tot = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
+      off += k < w ? s_wn[k] : 0;
+      tot += s_wn[k];
+    }
+    if (hit) s_q[off + __popcll(hm & ((1ull << lane) - 1ull))] = (int)threadIdx.x;
+    __syncthreads();
+    valid = (int)threadIdx.x < tot;
+    qi = qb + (valid ? s_q[threadIdx.x] : 0);
+#else
+    valid = valid && prim >= 0;
+#endif
+  }
+  const long long c = valid ? B.q_owner[qin][qi] : 0;
+  int nr = 0, kend = 0;
+  unsigned long long traced = 0;
+  bool emit_next = false;
+  yk_ray nxt;
+  if (valid) {
+    const yk_hit h = B.q_hits[qin][qi];
+    {
       const yk_ray pr = B.q_rays[qin][qi];
       const v3 from = V3(pr.from[0], pr.from[1], pr.from[2]), dir = V3(pr.dir[0], pr.dir[1], pr.dir[2]);
       const SurfPt sp = make_surface(S, from, dir, h);
