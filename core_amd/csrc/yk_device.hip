@@ -2307,6 +2307,10 @@ struct FilmConst {
 };
 
 __device__ __forceinline__ int round2int(double v) { return (int)(v + (0.5 - 1.4e-11)); }
+#ifndef YK_GATHER_GROUP
+#define YK_GATHER_GROUP 8
+#endif
+constexpr int kGatherGroup = YK_GATHER_GROUP;
 __device__ __forceinline__ int floor2int(double v) { return (int)floor(v); }
 
 // imageFilm_t::addSample as a gather (imagefilm.cc:453-511): each thread owns
@@ -2353,23 +2357,45 @@ __global__ void __launch_bounds__(256) k_film_gather(FilmConst F, const float4* 
             cbase = tb + (long long)((sy - Y) * W + (sx - X)) * F.spp;
           }
           const int ox = tx - sx, oy = ty - sy;
-          for (int s = 0; s < F.spp; ++s) {
-            const float2 dd = sxy[cbase + s];
-            const double dx = dd.x, dy = dd.y;
-            int dx0 = round2int(dx - F.filterw), dx1 = round2int(dx + F.filterw - 1.0);
-            int dy0 = round2int(dy - F.filterw), dy1 = round2int(dy + F.filterw - 1.0);
-            // film-edge clamps (cx0 - x etc.) hold by construction: tx, ty lie inside the film
-            if (ox < dx0 || ox > dx1 || oy < dy0 || oy > dy1) continue;
-            const int xi = floor2int(fabs(((double)ox - (dx - 0.5)) * F.tableScale));
-            const int yi = floor2int(fabs(((double)oy - (dy - 0.5)) * F.tableScale));
-            const float wt = F.table[yi * 16 + xi];
-            const float4 col = samples[cbase + s];
-            aR = aR + wt * col.x;
-            aG = aG + wt * col.y;
-            aB = aB + wt * col.z;
-            aA = aA + wt * col.w;
-            aW = aW + wt;
-            any = true;
+          // samples in groups of kGatherGroup: the group's positions, then the
+          // colours of the accepted ones, are loaded together (independent
+          // loads in flight instead of one dependent round trip per sample);
+          // the sums still run sample by sample in order
+          for (int s0 = 0; s0 < F.spp; s0 += kGatherGroup) {
+            float2 dd[kGatherGroup];
+#pragma unroll
+            for (int k = 0; k < kGatherGroup; ++k)
+              dd[k] = (s0 + k < F.spp) ? sxy[cbase + s0 + k] : make_float2(-8.f, -8.f);
+            float wt[kGatherGroup];
+            bool acc[kGatherGroup];
+#pragma unroll
+            for (int k = 0; k < kGatherGroup; ++k) {
+              const double dx = dd[k].x, dy = dd[k].y;
+              const int dx0 = round2int(dx - F.filterw), dx1 = round2int(dx + F.filterw - 1.0);
+              const int dy0 = round2int(dy - F.filterw), dy1 = round2int(dy + F.filterw - 1.0);
+              // film-edge clamps (cx0 - x etc.) hold by construction: tx, ty lie inside the film
+              acc[k] = s0 + k < F.spp && !(ox < dx0 || ox > dx1 || oy < dy0 || oy > dy1);
+              wt[k] = 0.f;
+              if (acc[k]) {
+                const int xi = floor2int(fabs(((double)ox - (dx - 0.5)) * F.tableScale));
+                const int yi = floor2int(fabs(((double)oy - (dy - 0.5)) * F.tableScale));
+                wt[k] = F.table[yi * 16 + xi];
+              }
+            }
+            float4 col[kGatherGroup];
+#pragma unroll
+            for (int k = 0; k < kGatherGroup; ++k)
+              col[k] = acc[k] ? samples[cbase + s0 + k] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int k = 0; k < kGatherGroup; ++k) {
+              if (!acc[k]) continue;
+              aR = aR + wt[k] * col[k].x;
+              aG = aG + wt[k] * col[k].y;
+              aB = aB + wt[k] * col[k].z;
+              aA = aA + wt[k] * col[k].w;
+              aW = aW + wt[k];
+              any = true;
+            }
           }
         }
     }
