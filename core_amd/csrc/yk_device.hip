@@ -89,8 +89,6 @@ struct DScene {
   const uint2* nodes;    // kd nodes (kdtree_build.h encoding)
   const uint32_t* pk;    // node packets (k_pack_nodes): YK_PK_BYTES per node, its word and its children's
   const float* ltris;    // leaf-ordered copies of the records (k_gather_leaf_tris), one per leaf-list entry
-  const uint32_t* chain;  // root-to-leaf chains of the non-empty leaves (k_chain_fill)
-  const uint32_t* choff;  // per node: offset of its chain in `chain` (non-empty leaves), else kNoHint
   const uint32_t* leaf;  // leaf primitive lists
   const float4* ng;      // geometric normal xyz, w = material id | kSmoothBit (int bits)
   const float* vn;       // 9 floats per prim: getSurface's vertex normals (smooth scenes only)
@@ -201,8 +199,6 @@ struct Trav {
   int node, sp;
   float Z, b1, b2;
   int prim;
-  uint32_t hint;   // chain offset of a leaf that likely holds the origin, or kNoHint
-  uint32_t hleaf;  // leaf node of the closest hit so far
   // transparent shadows (IntersectTS): filter colour, transparent surfaces
   // crossed, and the prims already filtered (std::set in the reference)
   c3 filt;
@@ -487,75 +483,6 @@ __global__ void k_pack_nodes(const uint2* __restrict__ nodes, uint32_t* __restri
   if (kPkWords == 8) *reinterpret_cast<uint2*>(o + 6) = make_uint2(0u, 0u);
 }
 
-// Hinted first descent (YK_HINTS). A shadow or bounce ray starts at the
-// surface point of its sample's last closest hit, deep inside the tree, and
-// its first descent from the root -- about half of a bounce ray's node visits
-// -- is a chain of dependent loads. Every non-empty leaf gets its root-to-leaf
-// chain (k_chain_fill): the ancestors' 8-B words root first, the leaf's word,
-// and a bit per level saying which child the path takes. The closest-hit
-// kernel records the chain of the leaf that holds each sample's hit; the
-// sample's next rays walk that chain: loads four levels at a time, all
-// independent, while the decisions run exactly as in the descent (same
-// words, same near/far tests, same pushes). Where the ray's own decision
-// leaves the chain, the ordinary descent takes over from that child -- a
-// hint is only ever slower when wrong, never different. Results and node
-// counts are those of the unhinted traversal.
-#ifndef YK_HINTS
-#define YK_HINTS 0  // measured: on 2417 / off 2817 Mrays/s (register pressure; cold chain loads replace L1-hot top levels)
-#endif
-constexpr bool kHints = YK_HINTS != 0;
-constexpr uint32_t kNoHint = 0xFFFFFFFFu;
-__global__ void k_parents(const uint2* __restrict__ nodes, unsigned n, uint32_t* __restrict__ par) {
-  const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (i == 0) par[0] = kNoHint;
-  const uint2 w = nodes[i];
-  if ((w.y & 3u) != 3u) {
-    par[i + 1] = i;
-    par[w.y >> 2] = i;
-  }
-}
-// words of the chain of node i: 4-word header + (depth + 1) node words, padded to 4 words
-__global__ void k_chain_len(const uint2* __restrict__ nodes, const uint32_t* __restrict__ par, unsigned n,
-                            uint32_t* __restrict__ len) {
-  const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint2 w = nodes[i];
-  uint32_t l = 0;
-  if ((w.y & 3u) == 3u && (w.y >> 2) > 0u) {
-    uint32_t d = 0;
-    for (uint32_t j = i; par[j] != kNoHint && d < 128u; j = par[j]) d++;
-    l = (4u + 2u * (d + 1u) + 3u) & ~3u;
-  }
-  len[i] = l;
-}
-__global__ void k_chain_fill(const uint2* __restrict__ nodes, const uint32_t* __restrict__ par,
-                             const uint32_t* __restrict__ off, unsigned n, uint32_t* __restrict__ chain) {
-  const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || off[i] == kNoHint) return;
-  uint32_t d = 0;
-  for (uint32_t j = i; par[j] != kNoHint; j = par[j]) d++;
-  uint32_t* o = chain + off[i];
-  const uint2 lw = nodes[i];
-  o[4 + 2 * d] = lw.x;
-  o[5 + 2 * d] = lw.y;
-  unsigned long long bits = 0ull;
-  uint32_t j = i, lvl = d;
-  while (lvl > 0u) {
-    const uint32_t pj = par[j];
-    lvl--;
-    const uint2 pw = nodes[pj];
-    o[4 + 2 * lvl] = pw.x;
-    o[5 + 2 * lvl] = pw.y;
-    if (j != pj + 1u) bits |= 1ull << lvl;
-    j = pj;
-  }
-  o[0] = (uint32_t)bits;
-  o[1] = (uint32_t)(bits >> 32);
-  o[2] = d;
-  o[3] = 0u;
-}
-
 // Leaf-ordered triangles (YK_LEAF_TRIS): a copy of every leaf-list entry's
 // triangle (a, e1, e2 as in S.tris) in leaf-list order, with the primitive id
 // in the first float4's w. A multi-primitive leaf's k-th test then loads
@@ -613,44 +540,9 @@ __device__ __forceinline__ uint32_t desc_decide(Trav& st, const LaneStack& stk, 
 // ray is already finished (dist < entry t). Outputs the leaf's w0 and count.
 template <bool CLOSEST>
 __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const LaneStack& stk, unsigned& nnodes,
-                                             uint32_t& w0, uint32_t& nref, bool& paused, uint32_t& leafnode) {
+                                             uint32_t& w0, uint32_t& nref, bool& paused) {
   paused = false;
   if (st.dist < st.en_t) return false;
-  if (kHints && st.hint != kNoHint) {  // hinted first descent (st.node is the root)
-    const uint32_t* ch = S.chain + st.hint;
-    st.hint = kNoHint;
-    const uint4 hd = *reinterpret_cast<const uint4*>(ch);
-    const unsigned long long bits = ((unsigned long long)hd.y << 32) | hd.x;
-    const uint32_t depth = hd.z;
-    uint32_t node = 0u;
-    bool ok = true;
-    for (uint32_t g = 0; ok && g < depth; g += 4u) {
-      const uint4 a = *reinterpret_cast<const uint4*>(ch + 4u + 2u * g);
-      const uint4 b = *reinterpret_cast<const uint4*>(ch + 8u + 2u * g);
-      const uint2 wv[4] = {make_uint2(a.x, a.y), make_uint2(a.z, a.w), make_uint2(b.x, b.y), make_uint2(b.z, b.w)};
-#pragma unroll
-      for (uint32_t j = 0; j < 4u; ++j) {
-        const uint32_t k = g + j;
-        if (ok && k < depth) {
-          const uint2 nd = wv[j];
-          nnodes++;
-          const uint32_t nxt = desc_decide(st, stk, nd, node, nd.y & 3u);
-          ok = nxt == (((bits >> k) & 1ull) ? (nd.y >> 2) : node + 1u);
-          node = nxt;
-        }
-      }
-    }
-    st.node = (int)node;
-    if (ok) {  // the chain's leaf
-      const uint2 lw = *reinterpret_cast<const uint2*>(ch + 4u + 2u * depth);
-      nnodes++;
-      w0 = lw.x;
-      nref = lw.y >> 2;
-      leafnode = node;
-      return true;
-    }
-    // the ray's own decision left the chain: the descent continues at that child
-  }
   // node indices are unsigned 32-bit offsets from the uniform node pointer
   // (one address VALU per load: base in SGPRs, 32-bit lane offset)
   const char* nbase = reinterpret_cast<const char*>(kPackets ? (const void*)S.pk : (const void*)S.nodes);
@@ -716,7 +608,6 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
   }
   w0 = nd.x;
   nref = nd.y >> 2;
-  leafnode = node;
   return true;
 }
 
@@ -776,7 +667,7 @@ __device__ __forceinline__ unsigned dpp_max_scan(unsigned x) {
 template <bool CLOSEST>
 __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t nref, uint32_t w0, int lane,
                                             unsigned long long* keys, float4* cand, unsigned* otab,
-                                            unsigned& ntris, bool& occluded, uint32_t leafnode = 0u) {
+                                            unsigned& ntris, bool& occluded) {
   unsigned x = nref;  // inclusive prefix sum of the lanes' reference counts
 #ifndef YK_DPP_SCAN
 #define YK_DPP_SCAN 1
@@ -883,7 +774,6 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
         st.b1 = c.y;
         st.b2 = c.z;
         st.prim = (int)__float_as_uint(c.w);
-        st.hleaf = leafnode;
       }
     } else if (kk != ~0ull) {
       occluded = true;
@@ -917,21 +807,11 @@ struct RayCount {
   }
 };
 
-// Hint chains of a launch (YK_HINTS): sample c(r) = owner ? owner[r] : r / div
-// of ray r reads its start hint from hints[c] (div > 0) and, for closest-hit
-// launches, stores the chain of its hit leaf there. hints == nullptr: none.
-struct HintRef {
-  uint32_t* hints;
-  const int* owner;
-  int div;  // 0: store only (camera rays start outside the tree)
-  __device__ __forceinline__ long long sample(int r) const { return owner ? owner[r] : (div > 1 ? r / div : r); }
-};
-
 template <bool CLOSEST, int NSEG, bool PIPE, bool TS = false, bool COOP = false>
 __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx,
                                            RayCount rc, yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
                                            unsigned long long* __restrict__ work, unsigned long long* __restrict__ ctr,
-                                           uint2* __restrict__ ovf, int ovf_depth, int refill_min, HintRef hr,
+                                           uint2* __restrict__ ovf, int ovf_depth, int refill_min,
                                            float* __restrict__ tsf = nullptr, int ts_depth = 0) {
   __shared__ uint2 lds[kStackLds * 64];
   const int lane = threadIdx.x;
@@ -1005,11 +885,6 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
           if (TS) st.ts_max = ts_depth;
           if (trav_begin<CLOSEST, TS>(S, st, ray)) {
             rid = r;
-            st.hint = kNoHint;
-            st.hleaf = 0u;
-            // the origin is inside the tree (entry t < 0): walk the chain of
-            // the leaf of the sample's last hit
-            if (kHints && COOP && hr.hints && hr.div > 0 && st.en_t < 0.f) st.hint = hr.hints[hr.sample(r)];
           } else if (CLOSEST) {
             hits[r] = yk_hit{-1, 0.f, 0.f, 0.f};
           } else {
@@ -1050,10 +925,9 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       bool live = false;
       uint32_t w0 = 0, nref = 0;
       bool paused = false;
-      uint32_t leafnode = 0u;
-      if (act) live = trav_descend<CLOSEST>(S, st, stk, nnodes, w0, nref, paused, leafnode);
+      if (act) live = trav_descend<CLOSEST>(S, st, stk, nnodes, w0, nref, paused);
       bool occ = false;
-      coop_leaves<CLOSEST>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, otab, ntris, occ, leafnode);
+      coop_leaves<CLOSEST>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, otab, ntris, occ);
       if (act) {
         bool done = !live || occ || (!paused && trav_next<CLOSEST>(S, st, stk));
         if (runaway) {
@@ -1067,7 +941,6 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
         if (done) {
           if (CLOSEST) {
             hits[rid] = (st.prim >= 0) ? yk_hit{st.prim, st.Z, st.b1, st.b2} : yk_hit{-1, 0.f, 0.f, 0.f};
-            if (kHints && hr.hints) hr.hints[hr.sample(rid)] = (st.prim >= 0) ? S.choff[st.hleaf] : kNoHint;
           } else {
             occl[rid] = occ ? 1 : 0;
           }
@@ -1161,17 +1034,15 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
 k_trace_closest(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                 yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
-                unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min,
-                HintRef hr) {
-  trace_body<true, 8, false, false, YK_COOP>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min, hr);
+                unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
+  trace_body<true, 8, false, false, YK_COOP>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
 k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
-               unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min,
-               HintRef hr) {
+               unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
   trace_body<false, YK_SHADOW_NSEG, false, false, YK_COOP>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth,
-                                                           refill_min, hr);
+                                                           refill_min);
 }
 // crowded-leaf variants (PIPE leaf loop): one wave fewer per SIMD buys the
 // registers of the prefetched triangle without spilling
@@ -1184,16 +1055,14 @@ k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __rest
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_LP_WAVES)))
 k_trace_closest_lp(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                    yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
-                   unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min,
-                   HintRef hr) {
-  trace_body<true, 8, true, false, YK_COOP_LP>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min, hr);
+                   unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
+  trace_body<true, 8, true, false, YK_COOP_LP>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_LP_WAVES)))
 k_trace_shadow_lp(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                   yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
-                  unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min,
-                  HintRef hr) {
-  trace_body<false, 1, true, false, YK_COOP_LP>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min, hr);
+                  unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
+  trace_body<false, 1, true, false, YK_COOP_LP>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 // transparent shadows (scene_t::isShadowed(state, ray, maxDepth, filt),
 // scene.cc:904-928 -> IntersectTS): occlusion + filter colour per ray
@@ -1201,8 +1070,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHAD
 k_trace_shadow_ts(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                   uint8_t* __restrict__ occl, float* __restrict__ tsf, int ts_depth, unsigned long long* __restrict__ work,
                   unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false, 1, false, true>(S, rays, idx, n, nullptr, occl, work, ctr, ovf, ovf_depth, refill_min, HintRef{},
-                                    tsf, ts_depth);
+  trace_body<false, 1, false, true>(S, rays, idx, n, nullptr, occl, work, ctr, ovf, ovf_depth, refill_min, tsf,
+                                    ts_depth);
 }
 
 // ============================================================ shading
@@ -1593,7 +1462,6 @@ enum : int { PS_ALIVE = 1, PS_RESOLVE = 2, PS_CONT = 4, PS_EST = 8 };
 // reads results in the reference's summation order without any sorting.
 struct Batch {
   int* prim_hit;        // PH_* flags of the camera ray
-  uint32_t* c_hint;     // hint chain of the sample's last closest hit (YK_HINTS)
   unsigned* soffs;      // samplingOffs (fnv of pixel)
   float* col;           // 3 floats: primary emission + direct light
   float* alpha;
@@ -2654,7 +2522,6 @@ struct Pipe {
   DBuf<uint8_t> sl_flags, s_occl;
   DBuf<float4> samples;
   DBuf<float2> sxy;
-  DBuf<uint32_t> c_hint;
   DBuf<unsigned> psample;
   DBuf<uint8_t> incl, caus;
   DBuf<float> emit0;
@@ -2682,7 +2549,6 @@ struct Pipe {
   }
   Batch bind(long long maxc, int K, int tiles_per_batch, bool spec = false, bool ts = false) {
     soffs.ensure(maxc);
-    c_hint.ensure(maxc);
     col.ensure(3 * maxc);
     alpha.ensure(maxc);
     prim_hit.ensure(maxc);
@@ -2713,7 +2579,6 @@ struct Pipe {
     Batch B{};
     B.prim_hit = prim_hit.p;
     B.soffs = soffs.p;
-    B.c_hint = c_hint.p;
     B.col = col.p;
     B.alpha = alpha.p;
     B.p_rays = p_rays.p;
@@ -2780,7 +2645,6 @@ struct yk_device {
   DBuf<float> vn;  // smooth-shading vertex normals (9 per prim), only when the scene has smooth meshes
   DBuf<uint2> nodes;
   DBuf<uint32_t> pk;   // node packets (k_pack_nodes), rebuilt whenever nodes change
-  DBuf<uint32_t> chain, choff;  // hint chains of the non-empty leaves and their offsets per node
   DBuf<float> ltris;  // leaf-ordered record copies, rebuilt whenever the leaf lists change
   DBuf<uint32_t> leaf;
   DScene S{};
@@ -3026,17 +2890,15 @@ int refill_min() {
 // accumulators {nodes, triangle tests, errors, rays}. ev: timing pair or null.
 template <bool CLOSEST>
 void enqueue_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* idx, RayCount n, yk_hit* hits,
-                   uint8_t* occ, unsigned long long* work, unsigned long long* acc, hipEvent_t ev0, hipEvent_t ev1,
-                   HintRef hr = HintRef{}) {
+                   uint8_t* occ, unsigned long long* work, unsigned long long* acc, hipEvent_t ev0, hipEvent_t ev1) {
   const bool lp = d->crowded_leaves;
   const long long grid = (long long)d->cus * (lp ? d->per_cu_lp[CLOSEST] : d->per_cu[CLOSEST]);
   const int ovf_depth = std::max(1, stack_depth(d) - kStackLds);
   P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
   if (ev0) HIPCHK(hipEventRecord(ev0, P.stream));
   auto kern = CLOSEST ? (lp ? k_trace_closest_lp : k_trace_closest) : (lp ? k_trace_shadow_lp : k_trace_shadow);
-  if (!d->S.chain) hr = HintRef{};
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays, idx, n, hits, occ, work, acc,
-                     P.ovf.p, ovf_depth, refill_min(), hr);
+                     P.ovf.p, ovf_depth, refill_min());
   HIPCHK(hipGetLastError());
   if (ev1) HIPCHK(hipEventRecord(ev1, P.stream));
 }
@@ -3116,37 +2978,6 @@ void install_traversal(yk_device* d, size_t nn, size_t nleaf, uint32_t max_leaf_
     HIPCHK(hipGetLastError());
   }
   d->S.pk = kPackets ? d->pk.p : nullptr;
-  d->S.chain = nullptr;
-  d->S.choff = nullptr;
-  if (kHints && nn > 1) {
-    DBuf<uint32_t> par, len;
-    par.ensure(nn + 1);
-    len.ensure(nn);
-    const unsigned g = grid_for((long long)nn);
-    hipLaunchKernelGGL(k_parents, dim3(g), dim3(256), 0, d->stream, d->nodes.p, (unsigned)nn, par.p);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_chain_len, dim3(g), dim3(256), 0, d->stream, d->nodes.p, par.p, (unsigned)nn, len.p);
-    HIPCHK(hipGetLastError());
-    std::vector<uint32_t> off(nn);
-    HIPCHK(hipMemcpyAsync(off.data(), len.p, nn * sizeof(uint32_t), hipMemcpyDeviceToHost, d->stream));
-    HIPCHK(hipStreamSynchronize(d->stream));
-    uint64_t total = 0;
-    for (size_t i = 0; i < nn; ++i) {
-      const uint32_t l = off[i];
-      off[i] = l ? (uint32_t)total : kNoHint;
-      total += l;
-      if (total >= kNoHint) throw std::invalid_argument("kd-tree hint chains exceed 2^32 words");
-    }
-    d->choff.ensure(nn);
-    d->chain.ensure((size_t)total + 16);  // + padding: the walk loads whole 4-level groups
-    HIPCHK(hipMemcpyAsync(d->choff.p, off.data(), nn * sizeof(uint32_t), hipMemcpyHostToDevice, d->stream));
-    hipLaunchKernelGGL(k_chain_fill, dim3(g), dim3(256), 0, d->stream, d->nodes.p, par.p, d->choff.p, (unsigned)nn,
-                       d->chain.p);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(d->stream));
-    d->S.chain = d->chain.p;
-    d->S.choff = d->choff.p;
-  }
   HIPCHK(hipStreamSynchronize(d->stream));
 }
 
@@ -3691,15 +3522,15 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     auto qw = [&](int isub, int depth) { return bw + isub * (bounces + 1) + depth; };
     int launch = 0;
     auto trace = [&](bool closest, const yk_ray* rays, const unsigned* idx, RayCount n, yk_hit* hits,
-                     uint8_t* occ, HintRef hr = HintRef{}) {
+                     uint8_t* occ) {
       unsigned long long* work = bw + qwords_per_batch + 128ll * launch++;
       const hipEvent_t e0 = P.event(evn[pi]), e1 = P.event(evn[pi] + 1);
       timed.push_back(Timed{pi, evn[pi], closest});
       evn[pi] += 2;
-      if (closest) enqueue_trace<true>(d, P, rays, idx, n, hits, occ, work, P.words.p, e0, e1, hr);
+      if (closest) enqueue_trace<true>(d, P, rays, idx, n, hits, occ, work, P.words.p, e0, e1);
       else if (B.ts)  // transparent shadows: IntersectTS, filter colour into the slot
         enqueue_trace_ts(d, P, rays, idx, n, occ, B.s_filt, p->shadow_depth, work, P.words.p + 4, e0, e1);
-      else enqueue_trace<false>(d, P, rays, idx, n, hits, occ, work, P.words.p + 4, e0, e1, hr);
+      else enqueue_trace<false>(d, P, rays, idx, n, hits, occ, work, P.words.p + 4, e0, e1);
     };
     // photonIntegrator_t::integrate after the direct light: show_map /
     // diffuse-map estimate, final gathering, caustics (photonintegr.cc:819-852)
@@ -3813,15 +3644,10 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
       HIPCHK(hipGetLastError());
     }
     if (!d->spec) {
-    // hint chains (YK_HINTS): camera hits store theirs per sample, shadow
-    // slots c * K + k and bounce rays of sample c start from it
-    const bool hinted = path && !B.ts;
-    const HintRef h_cam = hinted ? HintRef{B.c_hint, nullptr, 0} : HintRef{};
-    const HintRef h_shadow = hinted ? HintRef{B.c_hint, nullptr, B.K} : HintRef{};
-    trace(true, B.p_rays, nullptr, RayCount{nullptr, 0, nc}, B.p_hits, nullptr, h_cam);
+    trace(true, B.p_rays, nullptr, RayCount{nullptr, 0, nc}, B.p_hits, nullptr);
     hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(nc, YK_SHADE_BLOCK)), dim3(YK_SHADE_BLOCK), 0, P.stream, d->S, B, R, nc, qw(0, 0));
     HIPCHK(hipGetLastError());
-    trace(false, B.s_rays, B.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, B.s_occl, h_shadow);
+    trace(false, B.s_rays, B.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, B.s_occl);
     hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
     HIPCHK(hipGetLastError());
     if (pm) pm_entries(B, R, nc);
@@ -3838,12 +3664,11 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
       for (int depth = 1; depth <= bounces; ++depth) {
         const unsigned long long* in_w = qw(isub, depth - 1);
         unsigned long long* out_w = qw(isub, depth);
-        trace(true, B.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, B.q_hits[qin], nullptr,
-              hinted ? HintRef{B.c_hint, B.q_owner[qin], 1} : HintRef{});
+        trace(true, B.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, B.q_hits[qin], nullptr);
         hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(nc, YK_SHADE_BLOCK)), dim3(YK_SHADE_BLOCK), 0, P.stream, d->S, B, R, in_w, depth, isub,
                            qin, out_w);
         HIPCHK(hipGetLastError());
-        trace(false, B.s_rays, B.s_idx, RayCount{out_w, 0, 0}, nullptr, B.s_occl, h_shadow);
+        trace(false, B.s_rays, B.s_idx, RayCount{out_w, 0, 0}, nullptr, B.s_occl);
         hipLaunchKernelGGL(k_resolve_bounce, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, in_w, depth, qin);
         HIPCHK(hipGetLastError());
         qin ^= 1;
