@@ -1448,6 +1448,29 @@ __device__ __forceinline__ void wave_append2(unsigned long long* counter, unsign
   base_b = (unsigned)(base >> 32);
 }
 
+// Packs the block's threads with hit != 0 onto its first threads (in thread
+// order): returns whether this thread has an entry, and its original thread
+// index in `src`. Whole-block call; BLOCK = blockDim.x.
+template <int BLOCK>
+__device__ __forceinline__ bool pack_block(bool hit, int& src) {
+  __shared__ int s_q[BLOCK];
+  __shared__ int s_wn[BLOCK / 64];
+  const unsigned long long hm = __ballot(hit);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) s_wn[w] = __popcll(hm);
+  __syncthreads();
+  int off = 0, tot = 0;
+  for (int k = 0; k < BLOCK / 64; ++k) {
+    off += k < w ? s_wn[k] : 0;
+    tot += s_wn[k];
+  }
+  if (hit) s_q[off + __popcll(hm & ((1ull << lane) - 1ull))] = (int)threadIdx.x;
+  __syncthreads();
+  const bool valid = (int)threadIdx.x < tot;
+  src = valid ? s_q[threadIdx.x] : 0;
+  return valid;
+}
+
 // Shadow-ray slot flags
 enum : uint8_t { SL_TRACED = 1, SL_ADDS = 2 };
 // prim_hit flags
@@ -1971,22 +1994,9 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) YK_SHADE_ATTR k_shade_bounce(D
       B.pstate[c] = 0;
     }
 #if YK_PACK_HITS
-    __shared__ int s_q[YK_SHADE_BLOCK];
-    __shared__ int s_wn[YK_SHADE_BLOCK / 64];
-    const bool hit = valid && prim >= 0;
-    const unsigned long long hm = __ballot(hit);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    if (lane == 0) s_wn[w] = __popcll(hm);
-    __syncthreads();
-    int off = 0, tot = 0;
-    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
-      off += k < w ? s_wn[k] : 0;
-      tot += s_wn[k];
-    }
-    if (hit) s_q[off + __popcll(hm & ((1ull << lane) - 1ull))] = (int)threadIdx.x;
-    __syncthreads();
-    valid = (int)threadIdx.x < tot;
-    qi = qb + (valid ? s_q[threadIdx.x] : 0);
+    int src;
+    valid = pack_block<YK_SHADE_BLOCK>(valid && prim >= 0, src);
+    qi = qb + src;
 #else
     valid = valid && prim >= 0;
 #endif
