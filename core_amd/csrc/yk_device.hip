@@ -825,13 +825,22 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   // Ray hand-out. The queue is cut into NSEG (1 or 8) contiguous segments, one per XCD:
   // consecutive queue entries are spatially coherent (tile / pixel order), so
   // the rays an XCD traces touch a compact part of the tree and its private
-  // 4 MB L2 keeps it. A wave takes kPoolChunk-ray chunks of its own XCD's
-  // segment (one atomic per chunk), then steals from the other segments.
-  // Pool bounds are wave-uniform (scalar registers).
-#ifndef YK_POOL_CHUNK
-#define YK_POOL_CHUNK 64
+  // 4 MB L2 keeps it. A wave takes chunks of its own XCD's segment (one
+  // atomic per chunk), then steals from the other segments. Chunks are sized
+  // so that every wave takes about YK_POOL_CHUNKS of them, within
+  // [64, YK_POOL_CHUNK_MAX] rays: with cheap rays (the 36-tri Cornell box) a
+  // fixed 64-ray chunk made the segment counters' atomics the limit (shadow
+  // launches at 5.2 Grays/s; 256-ray chunks +52 %), while small launches keep
+  // small chunks for the tail. Pool bounds are wave-uniform (scalar registers).
+#ifndef YK_POOL_CHUNKS
+#define YK_POOL_CHUNKS 16
 #endif
-  constexpr unsigned kPoolChunk = YK_POOL_CHUNK;
+#ifndef YK_POOL_CHUNK_MAX
+#define YK_POOL_CHUNK_MAX 512
+#endif
+  const unsigned kPoolChunk = (unsigned)__builtin_amdgcn_readfirstlane((int)min(
+      (unsigned)YK_POOL_CHUNK_MAX,
+      max(64u, (unsigned)(n / ((long long)gridDim.x * YK_POOL_CHUNKS)) & ~63u)));
   unsigned xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
   constexpr unsigned kAll = (1u << NSEG) - 1u;
