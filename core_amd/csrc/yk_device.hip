@@ -95,6 +95,7 @@ struct DScene {
   float bound[6];
   int nlights;
   unsigned nnodes;  // node count, for the pop-time bounds guard
+  unsigned chunk_max;  // largest ray hand-out chunk (64 for crowded-leaf scenes, whose rays are costly)
 };
 
 __device__ __forceinline__ v3 ld3(const float* p) { return V3(p[0], p[1], p[2]); }
@@ -828,19 +829,22 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   // 4 MB L2 keeps it. A wave takes chunks of its own XCD's segment (one
   // atomic per chunk), then steals from the other segments. Chunks are sized
   // so that every wave takes about YK_POOL_CHUNKS of them, within
-  // [64, YK_POOL_CHUNK_MAX] rays: with cheap rays (the 36-tri Cornell box) a
-  // fixed 64-ray chunk made the segment counters' atomics the limit (shadow
+  // [64, S.chunk_max] rays: with cheap rays (the 36-tri Cornell box) a fixed
+  // 64-ray chunk made the segment counters' atomics the limit (shadow
   // launches at 5.2 Grays/s; 256-ray chunks +52 %), while small launches keep
-  // small chunks for the tail. Pool bounds are wave-uniform (scalar registers).
+  // small chunks for the tail. Crowded-leaf scenes (hair: 528 triangle tests
+  // per ray) keep 64-ray chunks: their rays are costly and uneven, and larger
+  // chunks measured 446 against 518 Mrays/s there. Pool bounds are
+  // wave-uniform (scalar registers).
 #ifndef YK_POOL_CHUNKS
 #define YK_POOL_CHUNKS 16
 #endif
 #ifndef YK_POOL_CHUNK_MAX
 #define YK_POOL_CHUNK_MAX 512
 #endif
-  const unsigned kPoolChunk = (unsigned)__builtin_amdgcn_readfirstlane((int)min(
-      (unsigned)YK_POOL_CHUNK_MAX,
-      max(64u, (unsigned)(n / ((long long)gridDim.x * YK_POOL_CHUNKS)) & ~63u)));
+  const unsigned kPoolChunk = (unsigned)__builtin_amdgcn_readfirstlane((int)max(
+      64u, min(min((unsigned)YK_POOL_CHUNK_MAX, S.chunk_max),
+               (unsigned)(n / ((long long)gridDim.x * YK_POOL_CHUNKS)) & ~63u)));
   unsigned xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
   constexpr unsigned kAll = (1u << NSEG) - 1u;
@@ -3156,6 +3160,7 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
     const long long filled = (long long)S.tree.stats.leaves - S.tree.stats.empty_leaves;
     const double mean = filled > 0 ? (double)S.tree.stats.leaf_prims / (double)filled : 0.0;
     d->crowded_leaves = mean > crowd;
+    d->S.chunk_max = d->crowded_leaves ? 64u : 512u;
   }
   d->nlights = (int)S.light_states.size();
   d->ntris = nt;
