@@ -1032,7 +1032,10 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 #define YK_CLOSEST_WAVES 5
 #endif
 #ifndef YK_SHADOW_WAVES
-#define YK_SHADOW_WAVES 6
+// 5: 92 VGPRs, no spill. At 6 the kernel spills 13-17 VGPRs, and small code
+// changes moved it between 2806 and 2636 Mrays/s; 5 measured 2795 on the
+// build where 6 gave 2636.
+#define YK_SHADOW_WAVES 5
 #endif
 #ifndef YK_SHADOW_NSEG
 #define YK_SHADOW_NSEG 1
