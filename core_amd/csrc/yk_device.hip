@@ -1419,6 +1419,10 @@ __device__ __forceinline__ bool dirac_illum(const DLight& L, v3 P, v3& ldir, flo
 #ifndef YK_APPEND_BLOCK
 #define YK_APPEND_BLOCK 512
 #endif
+// shadow-slot layout: k-major (slot_of) or the sample-major c * K + k
+#ifndef YK_SLOT_KMAJOR
+#define YK_SLOT_KMAJOR 1
+#endif
 // k_shade_bounce packs a block's hits onto its first threads (escaped paths
 // finish first)
 #ifndef YK_PACK_HITS
@@ -1489,14 +1493,18 @@ __device__ __forceinline__ bool pack_block(bool hit, int& src) {
 
 // Shadow-ray slot flags
 enum : uint8_t { SL_TRACED = 1, SL_ADDS = 2 };
+struct Batch;
+__device__ __forceinline__ long long slot_of(const Batch& B, long long c, int k);
 // prim_hit flags
 enum : int { PH_HIT = 1, PH_DIFFUSE = 2, PH_LIGHT = 4 };
 // path state bits
 enum : int { PS_ALIVE = 1, PS_RESOLVE = 2, PS_CONT = 4, PS_EST = 8 };
 
-// Per-batch device state. Camera sample c owns K shadow slots c*K + k:
+// Per-batch device state. Camera sample c owns K shadow slots k = 0..K-1:
 // doLightEstimation's i-th light sample is slot k0+i, its i-th BSDF (MIS)
-// sample slot k0+n+i. Shadow rays are written straight into their slot and
+// sample slot k0+n+i. Slot (c, k) is stored at k * cap + c (slot_of): the
+// lanes of a wave, consecutive samples writing the same k, then fill whole
+// cache lines (at c * K + k every lane's 32-B ray landed in its own line). Shadow rays are written straight into their slot and
 // only the slot index goes through the compacted queue, so the resolve step
 // reads results in the reference's summation order without any sorting.
 struct Batch {
@@ -1524,6 +1532,7 @@ struct Batch {
   float4* samples;      // final RGBA per camera sample
   float2* sxy;          // (dx, dy) of the sample inside its pixel
   int K;
+  long long cap;  // samples per batch: the stride of the shadow-slot arrays
   // specular recursion (recursiveRaytrace) only, see k_spawn / k_fold
   unsigned* psample;    // pixel sample index of each entry (state.pixelSample)
   uint8_t* incl;        // state.includeLights after the entry's path loop
@@ -1535,6 +1544,13 @@ struct Batch {
   float* s_filt;        // 3 per slot: filter colour of the shadow ray (IntersectTS)
   float* sl_aux;        // 4 per slot: scalar factors (and the Dirac light colour)
 };
+__device__ __forceinline__ long long slot_of(const Batch& B, long long c, int k) {
+#if YK_SLOT_KMAJOR
+  return (long long)k * B.cap + c;
+#else
+  return c * B.K + k;
+#endif
+}
 
 struct RenderConst {
   int ps;         // pixel sample index from B.psample (specular nodes, adaptive passes)
@@ -1654,7 +1670,7 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
   const DMat& M = c_mats[sp.mat];
   const c3 black = C3(0.f, 0.f, 0.f);
   if (L.type != YK_LIGHT_AREA) {  // Dirac branch, mcintegrator.cc:85-100: one shadow ray
-    const long long slot = c * B.K + k0;
+    const long long slot = slot_of(B, c, k0);
     v3 ldir;
     float ltmax;
     c3 lc;
@@ -1687,7 +1703,7 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
   const Halton h2_start = h2, h3_start = h3;  // the MIS half restarts at the same index
   for (int i = 0; i < n; ++i) {
     const float s1 = hal_next(h2), s2 = hal_next(h3);
-    const long long slot = c * B.K + k0 + i;
+    const long long slot = slot_of(B, c, k0 + i);
     v3 ldir;
     float ltmax, lpdf;
     if (!light_illum(L, sp.P, s1, s2, ldir, ltmax, lpdf)) {
@@ -1725,7 +1741,7 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
   h3 = h3_start;
   for (int i = 0; i < n; ++i) {
     const float s1 = hal_next(h2), s2 = hal_next(h3);
-    const long long slot = c * B.K + k0 + n + i;
+    const long long slot = slot_of(B, c, k0 + n + i);
     float W = 0.f, spdf = 0.f;
     bool ok;
     v3 bdir = V3(0.f, 0.f, 0.f);
@@ -1766,7 +1782,7 @@ __device__ __forceinline__ void flush_shadow(const Batch& B, long long c, int ke
   if (nr == 0) return;
   unsigned r = base;
   for (int k = 0; k < kend; ++k) {
-    const long long slot = c * B.K + k;
+    const long long slot = slot_of(B, c, k);
     const bool t = k < 64 ? ((traced >> k) & 1ull) != 0ull : (B.sl_flags[slot] & SL_TRACED) != 0;
     if (t) B.s_idx[r++] = (unsigned)slot;
   }
@@ -1913,7 +1929,7 @@ __device__ __forceinline__ c3 slot_value_ts(const Batch& B, long long slot, int 
 
 __device__ __forceinline__ c3 resolve_light(const Batch& B, long long c, int k0, int li) {
   if (c_lights[li].type != YK_LIGHT_AREA) {
-    const long long slot = c * B.K + k0;
+    const long long slot = slot_of(B, c, k0);
     c3 col = C3(0.f, 0.f, 0.f);
     if ((B.sl_flags[slot] & SL_ADDS) && !B.s_occl[slot])
       col = cadd(col, B.ts ? slot_value_ts(B, slot, 0, col)
@@ -1924,7 +1940,7 @@ __device__ __forceinline__ c3 resolve_light(const Batch& B, long long c, int k0,
   const float invNS = 1.f / (float)n;
   c3 ccol = C3(0.f, 0.f, 0.f), ccol2 = C3(0.f, 0.f, 0.f);
   for (int i = 0; i < 2 * n; ++i) {
-    const long long slot = c * B.K + k0 + i;
+    const long long slot = slot_of(B, c, k0 + i);
     if ((B.sl_flags[slot] & SL_ADDS) && !B.s_occl[slot]) {
       const c3 v = B.ts ? slot_value_ts(B, slot, i < n ? 1 : 2, C3(c_lights[li].color[0], c_lights[li].color[1], c_lights[li].color[2]))
                         : C3(B.sl_contrib[3 * slot], B.sl_contrib[3 * slot + 1], B.sl_contrib[3 * slot + 2]);
@@ -2630,6 +2646,7 @@ struct Pipe {
     B.samples = samples.p;
     B.sxy = sxy.p;
     B.K = K;
+    B.cap = maxc;
     if (ts) {
       s_filt.ensure(3 * maxc * K);
       sl_aux.ensure(4 * maxc * K);

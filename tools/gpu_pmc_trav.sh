@@ -7,7 +7,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 LIB=${1:-$PWD/tune/libyk_p1.so}
 TAG=${2:-p1}
-ARGS="--steps 1 --warmup 0 --no-cpu --spp 64"
+ARGS=${PMC_ARGS:-"--steps 1 --warmup 0 --no-cpu --spp 64"}
 O=gpurun_out/pmc_$TAG
 mkdir -p $O
 YK_LIB=$LIB timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o kt -- python3 bench.py $ARGS > $O/kt.log 2>&1
