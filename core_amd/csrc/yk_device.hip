@@ -702,7 +702,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
     // owner of slot s: the last lane whose range starts at or before s
     int own = 0;
     unsigned pown = 0;
-    if (kOwnerScan) {  // keys hold 24-bit range starts: install_traversal caps leaves at 2^18 references
+    if (kOwnerScan) {  // keys hold (range start + 1) << 8 in 32 bits: install_traversal caps leaves below 2^17 references (64 lanes x 2^17 < 2^24)
       otab[lane] = 0u;
       if (nref > 0u && pre >= base && pre - base < 64u) otab[pre - base] = ((pre + 1u) << 8) | (unsigned)lane;
       __syncthreads();
@@ -3004,8 +3004,8 @@ inline unsigned grid_for(long long n, int b = 256) { return (unsigned)((n + b - 
 // Traversal copies of the resident tree: the leaf-ordered triangles
 // (k_gather_leaf_tris) and the node packets (k_pack_nodes).
 void install_traversal(yk_device* d, size_t nn, size_t nleaf, uint32_t max_leaf_refs) {
-  if (kOwnerScan && max_leaf_refs >= (1u << 18))
-    throw std::invalid_argument("kd-tree leaf with 2^18 references or more (coop_leaves owner keys)");
+  if (kOwnerScan && max_leaf_refs >= (1u << 17))
+    throw std::invalid_argument("kd-tree leaf with 2^17 references or more (coop_leaves owner keys)");
   HIPCHK(hipDeviceSynchronize());  // every copy into nodes / leaf / tris has landed
   if (kLeafTris && nleaf) {
     d->ltris.ensure(kTriWords * nleaf);
