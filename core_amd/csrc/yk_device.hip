@@ -561,11 +561,15 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
 #ifndef YK_DESC_FRAC
 #define YK_DESC_FRAC 4  // measured 2 / 3 / 4 / 8: 2477 / 2524 / 2527 / 2450 Mrays/s (off: 2344)
 #endif
+#ifndef YK_DESC_FRAC_S
+#define YK_DESC_FRAC_S YK_DESC_FRAC  // any-hit kernel
+#endif
+  constexpr unsigned kFrac = CLOSEST ? YK_DESC_FRAC : YK_DESC_FRAC_S;
   // descent pause (YK_DESC_FRAC = f > 0): once fewer than 1/f of the lanes
   // that started this descent are still descending, those pause at their
   // current node and resume in the next iteration, so the wave does not loop
   // to its longest descent while the other lanes idle
-  const unsigned started = YK_DESC_FRAC ? (unsigned)__popcll(__builtin_amdgcn_ballot_w64(true)) : 0u;
+  const unsigned started = kFrac ? (unsigned)__popcll(__builtin_amdgcn_ballot_w64(true)) : 0u;
   // wave-uniform loop: the exit test is a ballot, and lanes whose descent
   // ended sit out the body under the exec mask. (A divergent loop exit makes
   // the compiler copy the descent's live-out registers every step, 13 of ~27
@@ -574,7 +578,7 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
   for (;;) {
     const unsigned long long m = __builtin_amdgcn_ballot_w64(desc);
     if (m == 0ull) break;
-    if (YK_DESC_FRAC && (unsigned)__popcll(m) * YK_DESC_FRAC < started) break;
+    if (kFrac && (unsigned)__popcll(m) * kFrac < started) break;
     if (!desc) continue;
     uint32_t nxt = desc_decide(st, stk, nd, node, ax);
     if (kPackets) {
