@@ -1417,6 +1417,9 @@ __device__ __forceinline__ bool dirac_illum(const DLight& L, v3 P, v3& ldir, flo
 // = fewer returning atomics on the queue word). Measured: path-tracing
 // shading at 1024 threads 2038 -> 2075 Mrays/s; the photon / final-gather
 // kernels best at 512 (1261 -> 1274; 1024: 1240).
+#ifndef YK_PRIMARY_BLOCK
+#define YK_PRIMARY_BLOCK YK_SHADE_BLOCK  // k_shade_primary's block (its own knob)
+#endif
 #ifndef YK_SHADE_BLOCK
 #define YK_SHADE_BLOCK 1024
 #endif
@@ -1825,7 +1828,7 @@ __device__ __forceinline__ yk_ray path_first_segment(const Batch& B, const Rende
 #else
 #define YK_SHADE_ATTR
 #endif
-__global__ void __launch_bounds__(YK_SHADE_BLOCK) YK_SHADE_ATTR k_shade_primary(DScene S, Batch B, RenderConst R, long long nc,
+__global__ void __launch_bounds__(YK_PRIMARY_BLOCK) YK_SHADE_ATTR k_shade_primary(DScene S, Batch B, RenderConst R, long long nc,
                                                        unsigned long long* __restrict__ qword) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = c < nc;
@@ -3632,7 +3635,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
         HIPCHK(hipMemsetAsync(d->spec_words.p, 0, d->spec_words.n * sizeof(unsigned long long), P.stream));
         launch = 0;
         trace(true, Bc.p_rays, nullptr, RayCount{nullptr, 0, n}, Bc.p_hits, nullptr);
-        hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(n, YK_SHADE_BLOCK)), dim3(YK_SHADE_BLOCK), 0, P.stream, d->S, Bc, Rc, n, qw(0, 0));
+        hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(n, YK_PRIMARY_BLOCK)), dim3(YK_PRIMARY_BLOCK), 0, P.stream, d->S, Bc, Rc, n, qw(0, 0));
         HIPCHK(hipGetLastError());
         trace(false, Bc.s_rays, Bc.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, Bc.s_occl);
         hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(n)), dim3(256), 0, P.stream, Bc, Rc, n);
@@ -3693,7 +3696,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     }
     if (!d->spec) {
     trace(true, B.p_rays, nullptr, RayCount{nullptr, 0, nc}, B.p_hits, nullptr);
-    hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(nc, YK_SHADE_BLOCK)), dim3(YK_SHADE_BLOCK), 0, P.stream, d->S, B, R, nc, qw(0, 0));
+    hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(nc, YK_PRIMARY_BLOCK)), dim3(YK_PRIMARY_BLOCK), 0, P.stream, d->S, B, R, nc, qw(0, 0));
     HIPCHK(hipGetLastError());
     trace(false, B.s_rays, B.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, B.s_occl);
     hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
