@@ -1067,10 +1067,10 @@ k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __rest
 // crowded-leaf variants (PIPE leaf loop): one wave fewer per SIMD buys the
 // registers of the prefetched triangle without spilling
 #ifndef YK_CLOSEST_LP_WAVES
-#define YK_CLOSEST_LP_WAVES 4
+#define YK_CLOSEST_LP_WAVES 5  // with the cooperative leaves (no PIPE registers): hair 533 vs 520 at 4
 #endif
 #ifndef YK_SHADOW_LP_WAVES
-#define YK_SHADOW_LP_WAVES 5
+#define YK_SHADOW_LP_WAVES 5  // 6: hair 506 vs 520
 #endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_LP_WAVES)))
 k_trace_closest_lp(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
