@@ -3187,7 +3187,7 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
     const long long filled = (long long)S.tree.stats.leaves - S.tree.stats.empty_leaves;
     const double mean = filled > 0 ? (double)S.tree.stats.leaf_prims / (double)filled : 0.0;
     d->crowded_leaves = mean > crowd;
-    d->S.chunk_max = d->crowded_leaves ? 64u : 512u;
+    d->S.chunk_max = d->crowded_leaves ? 64u : (unsigned)YK_POOL_CHUNK_MAX;
   }
   d->nlights = (int)S.light_states.size();
   d->ntris = nt;
