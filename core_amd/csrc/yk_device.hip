@@ -3011,6 +3011,8 @@ inline unsigned grid_for(long long n, int b = 256) { return (unsigned)((n + b - 
 // Traversal copies of the resident tree: the leaf-ordered triangles
 // (k_gather_leaf_tris) and the node packets (k_pack_nodes).
 void install_traversal(yk_device* d, size_t nn, size_t nleaf, uint32_t max_leaf_refs) {
+  // traversal stack entries hold (node + 1) in 30 bits
+  if (nn >= (1u << 30) - 1u) throw std::invalid_argument("kd-tree has 2^30 - 1 nodes or more");
   if (kOwnerScan && max_leaf_refs >= (1u << 17))
     throw std::invalid_argument("kd-tree leaf with 2^17 references or more (coop_leaves owner keys)");
   HIPCHK(hipDeviceSynchronize());  // every copy into nodes / leaf / tris has landed

@@ -291,6 +291,10 @@ int yk_scene_get_camera_state(const yk_scene* s, yk_camera_state* out);
 /* ---- device ---- */
 int yk_device_open(int32_t ordinal, yk_device** out);
 void yk_device_close(yk_device* d);
+/* Uploads scene s (geometry, kd-tree, materials, lights, camera) and builds
+ * the traversal's copies (node packets, leaf-ordered triangle records).
+ * YK_ERR_ARG if the kd-tree has a leaf with 2^17 or more references (the
+ * cooperative leaf test's limit) or 2^30 - 1 nodes or more (stack entries). */
 int yk_device_upload(yk_device* d, const yk_scene* s);
 int yk_device_sync(yk_device* d);
 /* hipStream_t the kernels run on, as an opaque pointer (for external timing) */
