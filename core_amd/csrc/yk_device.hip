@@ -175,21 +175,39 @@ __device__ __forceinline__ bool bound_cross(const float* bb, v3 from, v3 dir, fl
 constexpr int kStackLds = YK_STACK_LDS;  // power of two
 static_assert((kStackLds & (kStackLds - 1)) == 0, "LDS ring depth must be a power of two");
 
-struct LaneStack {
-  uint2* lds;       // [kStackLds][64]
+template <int RING>
+struct LaneStackT {
+  uint2* lds;       // [RING][64]
   uint2* ovf;       // this lane's overflow entries, contiguous (one cache line holds 8)
   int lane;
   __device__ __forceinline__ void push(int sp, uint2 e) const {
-    uint2* slot = lds + (sp & (kStackLds - 1)) * 64 + lane;
-    if (sp >= kStackLds) ovf[sp - kStackLds] = *slot;
+    uint2* slot = lds + (sp & (RING - 1)) * 64 + lane;
+    if (sp >= RING) ovf[sp - RING] = *slot;
     *slot = e;
   }
   __device__ __forceinline__ uint2 pop(int sp) const {  // sp = index of the entry to pop
-    uint2* slot = lds + (sp & (kStackLds - 1)) * 64 + lane;
+    uint2* slot = lds + (sp & (RING - 1)) * 64 + lane;
     const uint2 e = *slot;
-    if (sp >= kStackLds) *slot = ovf[sp - kStackLds];
+    if (sp >= RING) *slot = ovf[sp - RING];
     return e;
   }
+};
+using LaneStack = LaneStackT<kStackLds>;
+// Per-ray constants in LDS (YK_LDS_RAY, any-hit kernel): origin, direction
+// and inverse direction as rows [k * 64 + lane] instead of 9 VGPRs, so the
+// kernel fits 6 waves per SIMD without spilling; p == nullptr: registers.
+#ifndef YK_LDS_RAY
+#define YK_LDS_RAY 0  // measured: 6 waves (5 spills) 2708, 5 waves 2627, registers 2810 Mrays/s
+#endif
+#ifndef YK_LDS_RAY_RING
+#define YK_LDS_RAY_RING 4  // the LDS stack ring of that kernel (the rows need its LDS)
+#endif
+constexpr bool kLdsRay = YK_LDS_RAY != 0;
+struct RayLds {
+  float* p;
+  int lane;
+  __device__ __forceinline__ float at(int k, int l) const { return p[k * 64 + l]; }
+  __device__ __forceinline__ float get(int k) const { return p[k * 64 + lane]; }
 };
 struct Trav {
   v3 o, d, inv;
@@ -508,8 +526,9 @@ __global__ void k_gather_leaf_tris(const float* __restrict__ tris, const uint32_
 // One descent decision at interior node `node` (word nd, axis ax): the near /
 // far choice of kdtree.cc:711-761 plus the push of the far child (exit :=
 // split point). Returns the near child.
-__device__ __forceinline__ uint32_t desc_decide(Trav& st, const LaneStack& stk, uint2 nd, uint32_t node,
-                                                uint32_t ax) {
+template <bool LR = false, class Stk>
+__device__ __forceinline__ uint32_t desc_decide(Trav& st, const Stk& stk, uint2 nd, uint32_t node, uint32_t ax,
+                                                RayLds rl = RayLds{nullptr, 0}) {
   const float split = __uint_as_float(nd.x);
   const uint32_t right = nd.y >> 2;
   const bool a0 = ax == 0u, a1 = ax == 1u;
@@ -523,14 +542,16 @@ __device__ __forceinline__ uint32_t desc_decide(Trav& st, const LaneStack& stk, 
   const bool push = __builtin_amdgcn_inverse_ballot_w64((m_lf & ~m_c1) | (~m_lf & ~m_c2));
   if (push) {
     const uint32_t far_ = left_first ? right : node + 1u;
-    const float t = (split - sel3m(st.o, a0, a1)) * sel3m(st.inv, a0, a1);
+    const float t = LR ? (split - rl.get((int)ax)) * rl.get(6 + (int)ax)
+                       : (split - sel3m(st.o, a0, a1)) * sel3m(st.inv, a0, a1);
     stk.push(st.sp, make_uint2(__float_as_uint(st.ex_split), st.ex_w));
     st.sp++;
     st.ex_t = t;
     st.ex_split = split;
     st.ex_w = (far_ + 1u) | (ax << 30);
     // exit point (exit_pb with the axis masks at hand)
-    const v3 o = st.o, d = st.d;
+    const v3 o = LR ? V3(rl.get(0), rl.get(1), rl.get(2)) : st.o;
+    const v3 d = LR ? V3(rl.get(3), rl.get(4), rl.get(5)) : st.d;
     const float x = o.x + t * d.x, y = o.y + t * d.y, z = o.z + t * d.z;
     st.ex_pb = V3(a0 ? split : x, a1 ? split : y, (a0 || a1) ? z : split);
   }
@@ -539,9 +560,10 @@ __device__ __forceinline__ uint32_t desc_decide(Trav& st, const LaneStack& stk, 
 
 // Descends from st.node to a leaf (the descent of trav_step); false when the
 // ray is already finished (dist < entry t). Outputs the leaf's w0 and count.
-template <bool CLOSEST>
-__device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const LaneStack& stk, unsigned& nnodes,
-                                             uint32_t& w0, uint32_t& nref, bool& paused) {
+template <bool CLOSEST, bool LR = false, class Stk = LaneStack>
+__device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const Stk& stk, unsigned& nnodes,
+                                             uint32_t& w0, uint32_t& nref, bool& paused,
+                                             RayLds rl = RayLds{nullptr, 0}) {
   paused = false;
   if (st.dist < st.en_t) return false;
   // node indices are unsigned 32-bit offsets from the uniform node pointer
@@ -580,7 +602,7 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
     if (m == 0ull) break;
     if (kFrac && (unsigned)__popcll(m) * kFrac < started) break;
     if (!desc) continue;
-    uint32_t nxt = desc_decide(st, stk, nd, node, ax);
+    uint32_t nxt = desc_decide<LR>(st, stk, nd, node, ax, rl);
     if (kPackets) {
       // the near child's word is in the packet: decide there too (unless it
       // is a leaf), then load the packet of the node that decision picks
@@ -590,7 +612,7 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
       nnodes++;
       ax = nd.y & 3u;
       if (ax != 3u) {
-        nxt = desc_decide(st, stk, nd, node, ax);
+        nxt = desc_decide<LR>(st, stk, nd, node, ax, rl);
         ld_packet(nbase, nxt, p0, p1);
         nd = make_uint2(p0.x, p0.y);
         node = nxt;
@@ -618,8 +640,8 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
 
 // After the leaf: the closest-hit stop test, then pop (kdtree.cc:802-812).
 // True when the ray is finished.
-template <bool CLOSEST>
-__device__ __forceinline__ bool trav_next(const DScene& S, Trav& st, const LaneStack& stk) {
+template <bool CLOSEST, bool LR = false, class Stk = LaneStack>
+__device__ __forceinline__ bool trav_next(const DScene& S, Trav& st, const Stk& stk, RayLds rl = RayLds{nullptr, 0}) {
   if (CLOSEST && st.prim >= 0 && st.Z <= st.ex_t) return true;
   st.en_t = st.ex_t;
   st.en_pb = st.ex_pb;
@@ -634,8 +656,16 @@ __device__ __forceinline__ bool trav_next(const DScene& S, Trav& st, const LaneS
   st.ex_split = __uint_as_float(e.x);
   st.ex_w = e.y;
   const uint32_t code = e.y >> 30;
-  st.ex_t = (code == 3u) ? st.ex_split : (st.ex_split - sel3(st.o, code)) * sel3(st.inv, code);
-  exit_pb(st);
+  if (LR) {
+    const int ca = (int)min(code, 2u);  // code 3 (the initial exit) stores t itself
+    st.ex_t = (code == 3u) ? st.ex_split : (st.ex_split - rl.get(ca)) * rl.get(6 + ca);
+    const float x = rl.get(0) + st.ex_t * rl.get(3), y = rl.get(1) + st.ex_t * rl.get(4),
+                z = rl.get(2) + st.ex_t * rl.get(5);
+    st.ex_pb = V3(code == 0u ? st.ex_split : x, code == 1u ? st.ex_split : y, code == 2u ? st.ex_split : z);
+  } else {
+    st.ex_t = (code == 3u) ? st.ex_split : (st.ex_split - sel3(st.o, code)) * sel3(st.inv, code);
+    exit_pb(st);
+  }
   return false;
 }
 
@@ -669,10 +699,10 @@ __device__ __forceinline__ unsigned dpp_max_scan(unsigned x) {
 }
 
 // Wave-uniform: every lane calls it; nref = 0 for lanes without a leaf to test.
-template <bool CLOSEST>
+template <bool CLOSEST, bool LR = false>
 __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t nref, uint32_t w0, int lane,
                                             unsigned long long* keys, float4* cand, unsigned* otab,
-                                            unsigned& ntris, bool& occluded) {
+                                            unsigned& ntris, bool& occluded, RayLds rl = RayLds{nullptr, 0}) {
   unsigned x = nref;  // inclusive prefix sum of the lanes' reference counts
 #ifndef YK_DPP_SCAN
 #define YK_DPP_SCAN 1
@@ -730,8 +760,10 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
     }
     const unsigned k = sc - pown;
     const uint32_t ow0 = (uint32_t)__shfl((int)w0, own), on = (uint32_t)__shfl((int)nref, own);
-    const v3 ro = V3(__shfl(st.o.x, own), __shfl(st.o.y, own), __shfl(st.o.z, own));
-    const v3 rd = V3(__shfl(st.d.x, own), __shfl(st.d.y, own), __shfl(st.d.z, own));
+    const v3 ro = LR ? V3(rl.at(0, own), rl.at(1, own), rl.at(2, own))
+                     : V3(__shfl(st.o.x, own), __shfl(st.o.y, own), __shfl(st.o.z, own));
+    const v3 rd = LR ? V3(rl.at(3, own), rl.at(4, own), rl.at(5, own))
+                     : V3(__shfl(st.d.x, own), __shfl(st.d.y, own), __shfl(st.d.z, own));
     const float rz = __shfl(zlim, own);
     const float rtmin = CLOSEST ? __shfl(st.tmin, own) : 0.f;
     bool valid = false;
@@ -818,11 +850,15 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
                                            unsigned long long* __restrict__ work, unsigned long long* __restrict__ ctr,
                                            uint2* __restrict__ ovf, int ovf_depth, int refill_min,
                                            float* __restrict__ tsf = nullptr, int ts_depth = 0) {
-  __shared__ uint2 lds[kStackLds * 64];
+  constexpr bool LR = kLdsRay && COOP && !CLOSEST && !TS;
+  constexpr int kRing = LR ? YK_LDS_RAY_RING : kStackLds;
+  __shared__ uint2 lds[kRing * 64];
+  __shared__ float rayc[LR ? 9 * 64 : 1];
   const int lane = threadIdx.x;
+  const RayLds rl{LR ? rayc : nullptr, lane};
   const long long n = __builtin_amdgcn_readfirstlane((int)rc.get());
   if (blockIdx.x == 0 && lane == 0 && n > 0) atomicAdd(&ctr[3], (unsigned long long)n);  // rays traced
-  const LaneStack stk{lds, ovf + (size_t)(blockIdx.x * 64u + (unsigned)lane) * (unsigned)ovf_depth, lane};
+  const LaneStackT<kRing> stk{lds, ovf + (size_t)(blockIdx.x * 64u + (unsigned)lane) * (unsigned)ovf_depth, lane};
   int rid = -1;  // ray of this lane (host guarantees n < 2^31)
   bool exhausted = false;
   Trav st;
@@ -902,6 +938,17 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
           if (TS) st.ts_max = ts_depth;
           if (trav_begin<CLOSEST, TS>(S, st, ray)) {
             rid = r;
+            if (LR) {
+              rayc[0 * 64 + lane] = st.o.x;
+              rayc[1 * 64 + lane] = st.o.y;
+              rayc[2 * 64 + lane] = st.o.z;
+              rayc[3 * 64 + lane] = st.d.x;
+              rayc[4 * 64 + lane] = st.d.y;
+              rayc[5 * 64 + lane] = st.d.z;
+              rayc[6 * 64 + lane] = st.inv.x;
+              rayc[7 * 64 + lane] = st.inv.y;
+              rayc[8 * 64 + lane] = st.inv.z;
+            }
           } else if (CLOSEST) {
             hits[r] = yk_hit{-1, 0.f, 0.f, 0.f};
           } else {
@@ -934,7 +981,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
     s_it++;
     s_act += (unsigned long long)__popcll(__ballot(rid >= 0));
 #endif
-    if (COOP) {
+    if constexpr (COOP) {
       __shared__ unsigned long long keys[64];
       __shared__ float4 cand[CLOSEST ? 64 : 1];
       __shared__ unsigned otab[kOwnerScan ? 64 : 1];
@@ -942,11 +989,11 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       bool live = false;
       uint32_t w0 = 0, nref = 0;
       bool paused = false;
-      if (act) live = trav_descend<CLOSEST>(S, st, stk, nnodes, w0, nref, paused);
+      if (act) live = trav_descend<CLOSEST, LR>(S, st, stk, nnodes, w0, nref, paused, rl);
       bool occ = false;
-      coop_leaves<CLOSEST>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, otab, ntris, occ);
+      coop_leaves<CLOSEST, LR>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, otab, ntris, occ, rl);
       if (act) {
-        bool done = !live || occ || (!paused && trav_next<CLOSEST>(S, st, stk));
+        bool done = !live || occ || (!paused && trav_next<CLOSEST, LR>(S, st, stk, rl));
         if (runaway) {
           st.prim = -2;
           done = true;
@@ -2943,7 +2990,7 @@ void enqueue_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* id
                    uint8_t* occ, unsigned long long* work, unsigned long long* acc, hipEvent_t ev0, hipEvent_t ev1) {
   const bool lp = d->crowded_leaves;
   const long long grid = (long long)d->cus * (lp ? d->per_cu_lp[CLOSEST] : d->per_cu[CLOSEST]);
-  const int ovf_depth = std::max(1, stack_depth(d) - kStackLds);
+  const int ovf_depth = std::max(1, stack_depth(d) - (kLdsRay ? std::min(kStackLds, YK_LDS_RAY_RING) : kStackLds));
   P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
   if (ev0) HIPCHK(hipEventRecord(ev0, P.stream));
   auto kern = CLOSEST ? (lp ? k_trace_closest_lp : k_trace_closest) : (lp ? k_trace_shadow_lp : k_trace_shadow);
@@ -2958,7 +3005,7 @@ void enqueue_trace_ts(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned*
                       float* filt, int max_depth, unsigned long long* work, unsigned long long* acc, hipEvent_t ev0,
                       hipEvent_t ev1) {
   const long long grid = (long long)d->cus * d->per_cu_ts;
-  const int ovf_depth = std::max(1, stack_depth(d) - kStackLds);
+  const int ovf_depth = std::max(1, stack_depth(d) - (kLdsRay ? std::min(kStackLds, YK_LDS_RAY_RING) : kStackLds));
   P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
   if (ev0) HIPCHK(hipEventRecord(ev0, P.stream));
   hipLaunchKernelGGL(k_trace_shadow_ts, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays, idx, n, occ, filt,
