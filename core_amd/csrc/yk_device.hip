@@ -87,7 +87,7 @@ constexpr int kSmoothBit = 0x10000;  // prim interpolates vertex normals (mesh i
 struct DScene {
   const float* tris;     // triangle records (kTriWords floats per prim): a, prim id, e1=b-a, e2=c-a
   const uint2* nodes;    // kd nodes (kdtree_build.h encoding)
-  const uint32_t* pk;    // node packets (k_pack_nodes): YK_PK_BYTES per node, its word and its children's
+  const uint32_t* pk;    // node packets (k_pack_nodes): 24 B per node, its word and its children's
   const float* ltris;    // leaf-ordered copies of the records (k_gather_leaf_tris), one per leaf-list entry
   const uint32_t* leaf;  // leaf primitive lists
   const float4* ng;      // geometric normal xyz, w = material id | kSmoothBit (int bits)
@@ -100,27 +100,14 @@ struct DScene {
 
 __device__ __forceinline__ v3 ld3(const float* p) { return V3(p[0], p[1], p[2]); }
 
-// Triangle record (YK_TRI_BYTES): the Moller-Trumbore inputs a, e1 = b - a,
-// e2 = c - a (the reference's own subtractions) and the primitive id.
-//   48 B: (a, id) (e1, 0) (e2, 0) -- three aligned 16-B loads
-//   40 B: (a, id) (e1, e2.x) (e2.y, e2.z) -- 16 + 16 + 8 B loads, 17 % less
-//         footprint for the records the traversal streams through L2 / MALL
-#ifndef YK_TRI_BYTES
-#define YK_TRI_BYTES 48  // measured 48 / 40: 2752 / 2756 Mrays/s (within noise)
-#endif
-static_assert(YK_TRI_BYTES == 48 || YK_TRI_BYTES == 40, "triangle record is 40 or 48 bytes");
-constexpr unsigned kTriWords = YK_TRI_BYTES / 4;
+// Triangle record, 48 B: (a, prim id) (e1 = b - a, 0) (e2 = c - a, 0) -- the
+// Moller-Trumbore inputs with the reference's own subtractions, three aligned
+// 16-B loads. (A 40-B packing measured equal: 2752 / 2756 Mrays/s.)
+constexpr unsigned kTriWords = 12;
 __device__ __forceinline__ void ld_tri(const float* rec, float4& A, float4& E1, float4& E2) {
   A = *reinterpret_cast<const float4*>(rec);
-  if (kTriWords == 12) {
-    E1 = *reinterpret_cast<const float4*>(rec + 4);
-    E2 = *reinterpret_cast<const float4*>(rec + 8);
-  } else {
-    const float4 q = *reinterpret_cast<const float4*>(rec + 4);
-    const float2 r = *reinterpret_cast<const float2*>(rec + 8);
-    E1 = make_float4(q.x, q.y, q.z, 0.f);
-    E2 = make_float4(q.w, r.x, r.y, 0.f);
-  }
+  E1 = *reinterpret_cast<const float4*>(rec + 4);
+  E2 = *reinterpret_cast<const float4*>(rec + 8);
 }
 
 struct SurfPt {
@@ -169,45 +156,23 @@ __device__ __forceinline__ bool bound_cross(const float* bb, v3 from, v3 dir, fl
 // entry stores t itself. The top kStackLds entries of every lane live in an
 // LDS ring; deeper ones spill to a global overflow area (rare: a 1M-tri tree
 // has depth ~40 but a ray rarely holds more than a dozen pending exits).
-#ifndef YK_STACK_LDS
-#define YK_STACK_LDS 8
-#endif
-constexpr int kStackLds = YK_STACK_LDS;  // power of two
-static_assert((kStackLds & (kStackLds - 1)) == 0, "LDS ring depth must be a power of two");
+constexpr int kStackLds = 8;  // LDS ring depth per lane (16 measured slower: 1807 vs 2054, round 1)
 
-template <int RING>
-struct LaneStackT {
-  uint2* lds;       // [RING][64]
-  uint2* ovf;       // this lane's overflow entries, contiguous (one cache line holds 8)
+struct LaneStack {
+  uint2* lds;  // [kStackLds][64]
+  uint2* ovf;  // this lane's overflow entries, contiguous (one cache line holds 8)
   int lane;
   __device__ __forceinline__ void push(int sp, uint2 e) const {
-    uint2* slot = lds + (sp & (RING - 1)) * 64 + lane;
-    if (sp >= RING) ovf[sp - RING] = *slot;
+    uint2* slot = lds + (sp & (kStackLds - 1)) * 64 + lane;
+    if (sp >= kStackLds) ovf[sp - kStackLds] = *slot;
     *slot = e;
   }
   __device__ __forceinline__ uint2 pop(int sp) const {  // sp = index of the entry to pop
-    uint2* slot = lds + (sp & (RING - 1)) * 64 + lane;
+    uint2* slot = lds + (sp & (kStackLds - 1)) * 64 + lane;
     const uint2 e = *slot;
-    if (sp >= RING) *slot = ovf[sp - RING];
+    if (sp >= kStackLds) *slot = ovf[sp - kStackLds];
     return e;
   }
-};
-using LaneStack = LaneStackT<kStackLds>;
-// Per-ray constants in LDS (YK_LDS_RAY, any-hit kernel): origin, direction
-// and inverse direction as rows [k * 64 + lane] instead of 9 VGPRs, so the
-// kernel fits 6 waves per SIMD without spilling; p == nullptr: registers.
-#ifndef YK_LDS_RAY
-#define YK_LDS_RAY 0  // measured: 6 waves (5 spills) 2708, 5 waves 2627, registers 2810 Mrays/s
-#endif
-#ifndef YK_LDS_RAY_RING
-#define YK_LDS_RAY_RING 4  // the LDS stack ring of that kernel (the rows need its LDS)
-#endif
-constexpr bool kLdsRay = YK_LDS_RAY != 0;
-struct RayLds {
-  float* p;
-  int lane;
-  __device__ __forceinline__ float at(int k, int l) const { return p[k * 64 + l]; }
-  __device__ __forceinline__ float get(int k) const { return p[k * 64 + lane]; }
 };
 struct Trav {
   v3 o, d, inv;
@@ -339,11 +304,9 @@ __device__ __forceinline__ bool leaf_test(const DScene& S, Trav& st, uint32_t p,
   return false;
 }
 
-// PIPE: leaf loop software-pipelined one triangle ahead (the next entry's
-// index and vertices are loaded while the current one is tested). Used for
-// scenes with crowded leaves (hair: ~40 references per leaf), where the plain
-// loop pays two dependent memory round trips per triangle.
-template <bool CLOSEST, bool PIPE, bool TS = false>
+// Per-lane step (the transparent-shadow kernel, whose leaf body is
+// sequential: IntersectTS filters each transparent prim once, in leaf order).
+template <bool CLOSEST, bool TS = false>
 __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneStack& stk, unsigned& nnodes,
                                           unsigned& ntris, bool& occluded) {
   if (st.dist < st.en_t) return true;
@@ -387,40 +350,16 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
     nnodes++;
   }
   const uint32_t n = nd.y >> 2, w0 = nd.x;
-  if (!PIPE) {
-    for (uint32_t i = 0; i < n; ++i) {
-      const uint32_t p = (n == 1) ? w0 : S.leaf[w0 + i];
-      ntris++;
-      float4 A, E1, E2;
-      ld_tri(S.tris + (size_t)p * kTriWords, A, E1, E2);
-      // keep the three loads together (the compiler would otherwise sink A's
-      // load past the det test: a second dependent round trip per triangle)
-      asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
-                   "+v"(E2.y), "+v"(E2.z));
-      if (leaf_test<CLOSEST, TS>(S, st, p, A, E1, E2, occluded)) return true;
-    }
-  } else if (n > 0) {
-    uint32_t p = (n == 1) ? w0 : S.leaf[w0];
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t p = (n == 1) ? w0 : S.leaf[w0 + i];
+    ntris++;
     float4 A, E1, E2;
     ld_tri(S.tris + (size_t)p * kTriWords, A, E1, E2);
-    uint32_t pn = (n > 1) ? S.leaf[w0 + 1] : 0u;
-    for (uint32_t i = 0; i < n; ++i) {
-      float4 An = A, E1n = E1, E2n = E2;
-      uint32_t pnn = 0u;
-      if (i + 1 < n) {
-        ld_tri(S.tris + (size_t)pn * kTriWords, An, E1n, E2n);
-      }
-      if (i + 2 < n) pnn = S.leaf[w0 + i + 2];
-      asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
-                   "+v"(E2.y), "+v"(E2.z));
-      ntris++;
-      if (leaf_test<CLOSEST, TS>(S, st, p, A, E1, E2, occluded)) return true;
-      A = An;
-      E1 = E1n;
-      E2 = E2n;
-      p = pn;
-      pn = pnn;
-    }
+    // keep the three loads together (the compiler would otherwise sink A's
+    // load past the det test: a second dependent round trip per triangle)
+    asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
+                 "+v"(E2.y), "+v"(E2.z));
+    if (leaf_test<CLOSEST, TS>(S, st, p, A, E1, E2, occluded)) return true;
   }
   if (CLOSEST && st.prim >= 0 && st.Z <= st.ex_t) return true;
   // pop: entry := exit, exit := previous exit
@@ -460,30 +399,22 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
 // Results, node and triangle-test counts are therefore those of the per-lane
 // loop, bit for bit.
 
-// Node packets (YK_PACKETS): 32 B per node X holding X's own 8-B word and
-// those of its two children (left = X + 1, right), built by k_pack_nodes. One
+// Node packets: 24 B per node X holding X's own 8-B word and those of its two
+// children (left = X + 1, right), built by k_pack_nodes. One
 // load then serves two levels of the descent: the decision at X picks the near
 // child, whose word is already in registers, and the decision there picks the
 // next packet to load. Every lane of a wave advances two levels per memory
 // round trip, which a pair-reuse scheme (round 1: +2 %, round 2: -1 %) cannot
-// promise -- a wave waits for its slowest lane's load. 109 MB on the 1M probe.
+// promise -- a wave waits for its slowest lane's load. 82 MB on the 1M probe
+// (a 32-B stride, two aligned 16-B loads, measured 2765 against 2786 Mrays/s
+// for the 24-B one: 25 % less footprint in the 256 MB Infinity Cache).
 // (Empty-leaf skipping -- parent bits marking empty children, walked through
 // or popped through without loads -- measured 2185 / 2072 / 2394 Mrays/s
 // against 2497 without: lanes that keep going stretch the wave's iteration.)
-#ifndef YK_PACKETS
-#define YK_PACKETS 1
-#endif
-constexpr bool kPackets = YK_PACKETS != 0;
-// packet stride: 32 B (two aligned 16-B loads) or 24 B (a 16-B and an 8-B
-// load; 25 % less footprint in the 256 MB Infinity Cache)
-#ifndef YK_PK_BYTES
-#define YK_PK_BYTES 24  // measured 32 / 24: 2765 / 2786 Mrays/s
-#endif
-static_assert(YK_PK_BYTES == 32 || YK_PK_BYTES == 24, "packet stride is 24 or 32 bytes");
-constexpr unsigned kPkWords = YK_PK_BYTES / 4;
+constexpr unsigned kPkWords = 6;
 // packet of node i: p0 = (word of i, word of its left child), r = right child's word
 __device__ __forceinline__ void ld_packet(const char* base, uint32_t i, uint4& p0, uint2& r) {
-  const char* a = base + (size_t)i * YK_PK_BYTES;
+  const char* a = base + (size_t)i * (4 * kPkWords);
   p0 = *reinterpret_cast<const uint4*>(a);
   r = *reinterpret_cast<const uint2*>(a + 16);
 }
@@ -499,19 +430,14 @@ __global__ void k_pack_nodes(const uint2* __restrict__ nodes, uint32_t* __restri
   uint32_t* o = pk + (size_t)i * kPkWords;
   *reinterpret_cast<uint4*>(o) = make_uint4(w.x, w.y, l.x, l.y);
   *reinterpret_cast<uint2*>(o + 4) = r;
-  if (kPkWords == 8) *reinterpret_cast<uint2*>(o + 6) = make_uint2(0u, 0u);
 }
 
-// Leaf-ordered triangles (YK_LEAF_TRIS): a copy of every leaf-list entry's
+// Leaf-ordered triangles: a copy of every leaf-list entry's
 // triangle (a, e1, e2 as in S.tris) in leaf-list order, with the primitive id
 // in the first float4's w. A multi-primitive leaf's k-th test then loads
 // ltris[3 (w0 + k)] directly instead of leaf[w0 + k] and then tris[3 p]: one
 // dependent memory round trip less per test, for 48 B per leaf reference
 // (196 MB on the 1M probe, 20 GB on the 10M hair scene: HBM is 288 GB).
-#ifndef YK_LEAF_TRIS
-#define YK_LEAF_TRIS 1
-#endif
-constexpr bool kLeafTris = YK_LEAF_TRIS != 0;
 __global__ void k_gather_leaf_tris(const float* __restrict__ tris, const uint32_t* __restrict__ leaf,
                                    float* __restrict__ out, unsigned n) {
   const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -526,9 +452,8 @@ __global__ void k_gather_leaf_tris(const float* __restrict__ tris, const uint32_
 // One descent decision at interior node `node` (word nd, axis ax): the near /
 // far choice of kdtree.cc:711-761 plus the push of the far child (exit :=
 // split point). Returns the near child.
-template <bool LR = false, class Stk>
-__device__ __forceinline__ uint32_t desc_decide(Trav& st, const Stk& stk, uint2 nd, uint32_t node, uint32_t ax,
-                                                RayLds rl = RayLds{nullptr, 0}) {
+__device__ __forceinline__ uint32_t desc_decide(Trav& st, const LaneStack& stk, uint2 nd, uint32_t node,
+                                                uint32_t ax) {
   const float split = __uint_as_float(nd.x);
   const uint32_t right = nd.y >> 2;
   const bool a0 = ax == 0u, a1 = ax == 1u;
@@ -542,17 +467,14 @@ __device__ __forceinline__ uint32_t desc_decide(Trav& st, const Stk& stk, uint2 
   const bool push = __builtin_amdgcn_inverse_ballot_w64((m_lf & ~m_c1) | (~m_lf & ~m_c2));
   if (push) {
     const uint32_t far_ = left_first ? right : node + 1u;
-    const float t = LR ? (split - rl.get((int)ax)) * rl.get(6 + (int)ax)
-                       : (split - sel3m(st.o, a0, a1)) * sel3m(st.inv, a0, a1);
+    const float t = (split - sel3m(st.o, a0, a1)) * sel3m(st.inv, a0, a1);
     stk.push(st.sp, make_uint2(__float_as_uint(st.ex_split), st.ex_w));
     st.sp++;
     st.ex_t = t;
     st.ex_split = split;
     st.ex_w = (far_ + 1u) | (ax << 30);
     // exit point (exit_pb with the axis masks at hand)
-    const v3 o = LR ? V3(rl.get(0), rl.get(1), rl.get(2)) : st.o;
-    const v3 d = LR ? V3(rl.get(3), rl.get(4), rl.get(5)) : st.d;
-    const float x = o.x + t * d.x, y = o.y + t * d.y, z = o.z + t * d.z;
+    const float x = st.o.x + t * st.d.x, y = st.o.y + t * st.d.y, z = st.o.z + t * st.d.z;
     st.ex_pb = V3(a0 ? split : x, a1 ? split : y, (a0 || a1) ? z : split);
   }
   return left_first ? node + 1u : right;
@@ -560,24 +482,19 @@ __device__ __forceinline__ uint32_t desc_decide(Trav& st, const Stk& stk, uint2 
 
 // Descends from st.node to a leaf (the descent of trav_step); false when the
 // ray is already finished (dist < entry t). Outputs the leaf's w0 and count.
-template <bool CLOSEST, bool LR = false, class Stk = LaneStack>
-__device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const Stk& stk, unsigned& nnodes,
-                                             uint32_t& w0, uint32_t& nref, bool& paused,
-                                             RayLds rl = RayLds{nullptr, 0}) {
+template <bool CLOSEST>
+__device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const LaneStack& stk, unsigned& nnodes,
+                                             uint32_t& w0, uint32_t& nref, bool& paused) {
   paused = false;
   if (st.dist < st.en_t) return false;
   // node indices are unsigned 32-bit offsets from the uniform node pointer
   // (one address VALU per load: base in SGPRs, 32-bit lane offset)
-  const char* nbase = reinterpret_cast<const char*>(kPackets ? (const void*)S.pk : (const void*)S.nodes);
+  const char* nbase = reinterpret_cast<const char*>(S.pk);
   uint32_t node = (uint32_t)st.node;
   uint4 p0;
   uint2 p1, nd;
-  if (kPackets) {
-    ld_packet(nbase, node, p0, p1);
-    nd = make_uint2(p0.x, p0.y);
-  } else {
-    nd = *reinterpret_cast<const uint2*>(nbase + (node << 3));
-  }
+  ld_packet(nbase, node, p0, p1);
+  nd = make_uint2(p0.x, p0.y);
   nnodes++;
   uint32_t ax = nd.y & 3u;
 #ifndef YK_DESC_FRAC
@@ -602,25 +519,18 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const St
     if (m == 0ull) break;
     if (kFrac && (unsigned)__popcll(m) * kFrac < started) break;
     if (!desc) continue;
-    uint32_t nxt = desc_decide<LR>(st, stk, nd, node, ax, rl);
-    if (kPackets) {
-      // the near child's word is in the packet: decide there too (unless it
-      // is a leaf), then load the packet of the node that decision picks
-      const bool left = nxt == node + 1u;
-      nd = left ? make_uint2(p0.z, p0.w) : p1;
-      node = nxt;
-      nnodes++;
-      ax = nd.y & 3u;
-      if (ax != 3u) {
-        nxt = desc_decide<LR>(st, stk, nd, node, ax, rl);
-        ld_packet(nbase, nxt, p0, p1);
-        nd = make_uint2(p0.x, p0.y);
-        node = nxt;
-        nnodes++;
-        ax = nd.y & 3u;
-      }
-    } else {
-      nd = *reinterpret_cast<const uint2*>(nbase + (nxt << 3));
+    uint32_t nxt = desc_decide(st, stk, nd, node, ax);
+    // the near child's word is in the packet: decide there too (unless it is
+    // a leaf), then load the packet of the node that decision picks
+    const bool left = nxt == node + 1u;
+    nd = left ? make_uint2(p0.z, p0.w) : p1;
+    node = nxt;
+    nnodes++;
+    ax = nd.y & 3u;
+    if (ax != 3u) {
+      nxt = desc_decide(st, stk, nd, node, ax);
+      ld_packet(nbase, nxt, p0, p1);
+      nd = make_uint2(p0.x, p0.y);
       node = nxt;
       nnodes++;
       ax = nd.y & 3u;
@@ -640,8 +550,8 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const St
 
 // After the leaf: the closest-hit stop test, then pop (kdtree.cc:802-812).
 // True when the ray is finished.
-template <bool CLOSEST, bool LR = false, class Stk = LaneStack>
-__device__ __forceinline__ bool trav_next(const DScene& S, Trav& st, const Stk& stk, RayLds rl = RayLds{nullptr, 0}) {
+template <bool CLOSEST>
+__device__ __forceinline__ bool trav_next(const DScene& S, Trav& st, const LaneStack& stk) {
   if (CLOSEST && st.prim >= 0 && st.Z <= st.ex_t) return true;
   st.en_t = st.ex_t;
   st.en_pb = st.ex_pb;
@@ -656,16 +566,8 @@ __device__ __forceinline__ bool trav_next(const DScene& S, Trav& st, const Stk& 
   st.ex_split = __uint_as_float(e.x);
   st.ex_w = e.y;
   const uint32_t code = e.y >> 30;
-  if (LR) {
-    const int ca = (int)min(code, 2u);  // code 3 (the initial exit) stores t itself
-    st.ex_t = (code == 3u) ? st.ex_split : (st.ex_split - rl.get(ca)) * rl.get(6 + ca);
-    const float x = rl.get(0) + st.ex_t * rl.get(3), y = rl.get(1) + st.ex_t * rl.get(4),
-                z = rl.get(2) + st.ex_t * rl.get(5);
-    st.ex_pb = V3(code == 0u ? st.ex_split : x, code == 1u ? st.ex_split : y, code == 2u ? st.ex_split : z);
-  } else {
-    st.ex_t = (code == 3u) ? st.ex_split : (st.ex_split - sel3(st.o, code)) * sel3(st.inv, code);
-    exit_pb(st);
-  }
+  st.ex_t = (code == 3u) ? st.ex_split : (st.ex_split - sel3(st.o, code)) * sel3(st.inv, code);
+  exit_pb(st);
   return false;
 }
 
@@ -676,16 +578,13 @@ __device__ __forceinline__ uint32_t ord_key(float t) {
   return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
 }
 
-// Owner of a pair slot (YK_OWNER_SCAN): lanes whose reference range starts in
+// Owner of a pair slot: lanes whose reference range starts in
 // the round's 64 slots write ((range start + 1) << 8 | lane) at that slot of an LDS
 // table, and an inclusive max-scan over the table (DPP, seeded with the
 // previous round's last owner) gives every slot the lane whose range covers it
 // -- one LDS write / read and six VALU steps instead of a six-step binary
-// search of dependent cross-lane reads.
-#ifndef YK_OWNER_SCAN
-#define YK_OWNER_SCAN 1
-#endif
-constexpr bool kOwnerScan = YK_OWNER_SCAN != 0;
+// search of dependent cross-lane reads (measured equal; kept for the shorter
+// dependency chain).
 __device__ __forceinline__ unsigned dpp_max_scan(unsigned x) {
   // row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15 / 31; lanes whose
   // source is out of range keep their value (old = x, max is idempotent)
@@ -699,15 +598,11 @@ __device__ __forceinline__ unsigned dpp_max_scan(unsigned x) {
 }
 
 // Wave-uniform: every lane calls it; nref = 0 for lanes without a leaf to test.
-template <bool CLOSEST, bool LR = false>
+template <bool CLOSEST>
 __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t nref, uint32_t w0, int lane,
                                             unsigned long long* keys, float4* cand, unsigned* otab,
-                                            unsigned& ntris, bool& occluded, RayLds rl = RayLds{nullptr, 0}) {
+                                            unsigned& ntris, bool& occluded) {
   unsigned x = nref;  // inclusive prefix sum of the lanes' reference counts
-#ifndef YK_DPP_SCAN
-#define YK_DPP_SCAN 1
-#endif
-#if YK_DPP_SCAN
   // DPP scan: row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15 / 31
   // carry the row totals (out-of-row sources read 0)
   x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
@@ -716,13 +611,6 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
   x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
   x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
   x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
-#else
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const unsigned y = (unsigned)__shfl_up((int)x, d);
-    if (lane >= d) x += y;
-  }
-#endif
   const unsigned pre = x - nref;
   const unsigned total = (unsigned)__builtin_amdgcn_readlane((int)x, 63);
   if (total == 0u) return;
@@ -734,36 +622,22 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
     const unsigned s = base + (unsigned)lane;
     const unsigned sc = min(s, total - 1u);
     // owner of slot s: the last lane whose range starts at or before s
-    int own = 0;
-    unsigned pown = 0;
-    if (kOwnerScan) {  // keys hold (range start + 1) << 8 in 32 bits: install_traversal caps leaves below 2^17 references (64 lanes x 2^17 < 2^24)
-      otab[lane] = 0u;
-      if (nref > 0u && pre >= base && pre - base < 64u) otab[pre - base] = ((pre + 1u) << 8) | (unsigned)lane;
-      __syncthreads();
-      const unsigned v = dpp_max_scan(otab[lane]);
-      // slots before the round's first range start continue the range that
-      // covered the previous round's last slot
-      const unsigned key = v ? v : carry;
-      carry = (unsigned)__builtin_amdgcn_readlane((int)key, 63);
-      own = (int)(key & 0xFFu);
-      pown = (key >> 8) - 1u;
-    } else {
-#pragma unroll
-      for (int step = 32; step > 0; step >>= 1) {
-        const int c = own + step;
-        const unsigned v = (unsigned)__shfl((int)pre, c);
-        if (v <= sc) {
-          own = c;
-          pown = v;
-        }
-      }
-    }
+    // keys hold (range start + 1) << 8 in 32 bits: install_traversal caps
+    // leaves below 2^17 references (64 lanes x 2^17 < 2^24)
+    otab[lane] = 0u;
+    if (nref > 0u && pre >= base && pre - base < 64u) otab[pre - base] = ((pre + 1u) << 8) | (unsigned)lane;
+    __syncthreads();
+    const unsigned ov = dpp_max_scan(otab[lane]);
+    // slots before the round's first range start continue the range that
+    // covered the previous round's last slot
+    const unsigned okey = ov ? ov : carry;
+    carry = (unsigned)__builtin_amdgcn_readlane((int)okey, 63);
+    const int own = (int)(okey & 0xFFu);
+    const unsigned pown = (okey >> 8) - 1u;
     const unsigned k = sc - pown;
     const uint32_t ow0 = (uint32_t)__shfl((int)w0, own), on = (uint32_t)__shfl((int)nref, own);
-    const v3 ro = LR ? V3(rl.at(0, own), rl.at(1, own), rl.at(2, own))
-                     : V3(__shfl(st.o.x, own), __shfl(st.o.y, own), __shfl(st.o.z, own));
-    const v3 rd = LR ? V3(rl.at(3, own), rl.at(4, own), rl.at(5, own))
-                     : V3(__shfl(st.d.x, own), __shfl(st.d.y, own), __shfl(st.d.z, own));
+    const v3 ro = V3(__shfl(st.o.x, own), __shfl(st.o.y, own), __shfl(st.o.z, own));
+    const v3 rd = V3(__shfl(st.d.x, own), __shfl(st.d.y, own), __shfl(st.d.z, own));
     const float rz = __shfl(zlim, own);
     const float rtmin = CLOSEST ? __shfl(st.tmin, own) : 0.f;
     bool valid = false;
@@ -771,16 +645,11 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
     float th = 0.f, u = 0.f, v = 0.f;
     uint32_t p = 0;
     if (s < total) {
-      const float* tp;
-      if (kLeafTris) {  // one load: the leaf's own record (prim id in A.w)
-        tp = (on == 1u) ? S.tris + (size_t)ow0 * kTriWords : S.ltris + (size_t)(ow0 + k) * kTriWords;
-      } else {
-        p = (on == 1u) ? ow0 : S.leaf[ow0 + k];
-        tp = S.tris + (size_t)p * kTriWords;
-      }
+      // one load: the leaf's own record (prim id in A.w)
+      const float* tp = (on == 1u) ? S.tris + (size_t)ow0 * kTriWords : S.ltris + (size_t)(ow0 + k) * kTriWords;
       float4 A, E1, E2;
       ld_tri(tp, A, E1, E2);
-      if (kLeafTris) p = __float_as_uint(A.w);
+      p = __float_as_uint(A.w);
       asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
                    "+v"(E2.y), "+v"(E2.z));
       if (mt_intersect(V3(A.x, A.y, A.z), V3(E1.x, E1.y, E1.z), V3(E2.x, E2.y, E2.z), ro, rd, th, u, v)) {
@@ -844,21 +713,17 @@ struct RayCount {
   }
 };
 
-template <bool CLOSEST, int NSEG, bool PIPE, bool TS = false, bool COOP = false>
+template <bool CLOSEST, int NSEG, bool TS = false>
 __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx,
                                            RayCount rc, yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
                                            unsigned long long* __restrict__ work, unsigned long long* __restrict__ ctr,
                                            uint2* __restrict__ ovf, int ovf_depth, int refill_min,
                                            float* __restrict__ tsf = nullptr, int ts_depth = 0) {
-  constexpr bool LR = kLdsRay && COOP && !CLOSEST && !TS;
-  constexpr int kRing = LR ? YK_LDS_RAY_RING : kStackLds;
-  __shared__ uint2 lds[kRing * 64];
-  __shared__ float rayc[LR ? 9 * 64 : 1];
+  __shared__ uint2 lds[kStackLds * 64];
   const int lane = threadIdx.x;
-  const RayLds rl{LR ? rayc : nullptr, lane};
   const long long n = __builtin_amdgcn_readfirstlane((int)rc.get());
   if (blockIdx.x == 0 && lane == 0 && n > 0) atomicAdd(&ctr[3], (unsigned long long)n);  // rays traced
-  const LaneStackT<kRing> stk{lds, ovf + (size_t)(blockIdx.x * 64u + (unsigned)lane) * (unsigned)ovf_depth, lane};
+  const LaneStack stk{lds, ovf + (size_t)(blockIdx.x * 64u + (unsigned)lane) * (unsigned)ovf_depth, lane};
   int rid = -1;  // ray of this lane (host guarantees n < 2^31)
   bool exhausted = false;
   Trav st;
@@ -938,17 +803,6 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
           if (TS) st.ts_max = ts_depth;
           if (trav_begin<CLOSEST, TS>(S, st, ray)) {
             rid = r;
-            if (LR) {
-              rayc[0 * 64 + lane] = st.o.x;
-              rayc[1 * 64 + lane] = st.o.y;
-              rayc[2 * 64 + lane] = st.o.z;
-              rayc[3 * 64 + lane] = st.d.x;
-              rayc[4 * 64 + lane] = st.d.y;
-              rayc[5 * 64 + lane] = st.d.z;
-              rayc[6 * 64 + lane] = st.inv.x;
-              rayc[7 * 64 + lane] = st.inv.y;
-              rayc[8 * 64 + lane] = st.inv.z;
-            }
           } else if (CLOSEST) {
             hits[r] = yk_hit{-1, 0.f, 0.f, 0.f};
           } else {
@@ -981,19 +835,19 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
     s_it++;
     s_act += (unsigned long long)__popcll(__ballot(rid >= 0));
 #endif
-    if constexpr (COOP) {
+    if constexpr (!TS) {
       __shared__ unsigned long long keys[64];
       __shared__ float4 cand[CLOSEST ? 64 : 1];
-      __shared__ unsigned otab[kOwnerScan ? 64 : 1];
+      __shared__ unsigned otab[64];
       const bool act = rid >= 0;
       bool live = false;
       uint32_t w0 = 0, nref = 0;
       bool paused = false;
-      if (act) live = trav_descend<CLOSEST, LR>(S, st, stk, nnodes, w0, nref, paused, rl);
+      if (act) live = trav_descend<CLOSEST>(S, st, stk, nnodes, w0, nref, paused);
       bool occ = false;
-      coop_leaves<CLOSEST, LR>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, otab, ntris, occ, rl);
+      coop_leaves<CLOSEST>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, otab, ntris, occ);
       if (act) {
-        bool done = !live || occ || (!paused && trav_next<CLOSEST, LR>(S, st, stk, rl));
+        bool done = !live || occ || (!paused && trav_next<CLOSEST>(S, st, stk));
         if (runaway) {
           st.prim = -2;
           done = true;
@@ -1013,7 +867,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       }
     } else if (rid >= 0) {
       bool occ = false;
-      bool done = trav_step<CLOSEST, PIPE, TS>(S, st, stk, nnodes, ntris, occ);
+      bool done = trav_step<CLOSEST, TS>(S, st, stk, nnodes, ntris, occ);
       if (runaway) {
         st.prim = -2;
         done = true;
@@ -1073,71 +927,38 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   if (nerr) atomicAdd(&ctr[2], (unsigned long long)nerr);
 }
 
-// Occupancy targets and ray hand-out (measured on MI355X, 1M-tri scene): with
-// the wave-cooperative leaf phase the closest-hit kernel runs best at 5
-// waves/SIMD (102 VGPRs, no spill; 6 waves spill and lose 10 % on camera
-// rays) with per-XCD ray segments (+12% from L2 locality), the any-hit kernel
-// at 6 waves with one shared segment. Before the cooperative phase the
-// targets were 6 / 7 (tools/trav_bench.py).
+// Occupancy targets (measured on MI355X, 1M-tri scene, cooperative leaves):
+// closest-hit at 5 waves/SIMD (96 VGPRs; 6 / 4 waves measured 2644 / 2593
+// against 2810 Mrays/s) with per-XCD ray segments (+12 % from L2 locality);
+// any-hit at 5 (92 VGPRs, no spill: at 6 it spilled 13-17 VGPRs and moved
+// between 2806 and 2636 with unrelated code changes) with one shared segment
+// (per-XCD segments measured 2700 against 2719). Crowded-leaf scenes (hair)
+// run the same kernels with 64-ray hand-out chunks (DScene.chunk_max).
 #ifndef YK_CLOSEST_WAVES
 #define YK_CLOSEST_WAVES 5
 #endif
 #ifndef YK_SHADOW_WAVES
-// 5: 92 VGPRs, no spill. At 6 the kernel spills 13-17 VGPRs, and small code
-// changes moved it between 2806 and 2636 Mrays/s; 5 measured 2795 on the
-// build where 6 gave 2636.
 #define YK_SHADOW_WAVES 5
-#endif
-#ifndef YK_SHADOW_NSEG
-#define YK_SHADOW_NSEG 1
-#endif
-// wave-cooperative leaf testing (coop_leaves) in the closest / any-hit kernels
-#ifndef YK_COOP
-#define YK_COOP 1
-#endif
-#ifndef YK_COOP_LP
-#define YK_COOP_LP 1
 #endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
 k_trace_closest(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                 yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                 unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<true, 8, false, false, YK_COOP>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+  trace_body<true, 8>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
 k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false, YK_SHADOW_NSEG, false, false, YK_COOP>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth,
-                                                           refill_min);
-}
-// crowded-leaf variants (PIPE leaf loop): one wave fewer per SIMD buys the
-// registers of the prefetched triangle without spilling
-#ifndef YK_CLOSEST_LP_WAVES
-#define YK_CLOSEST_LP_WAVES 5  // with the cooperative leaves (no PIPE registers): hair 533 vs 520 at 4
-#endif
-#ifndef YK_SHADOW_LP_WAVES
-#define YK_SHADOW_LP_WAVES 5  // 6: hair 506 vs 520
-#endif
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_LP_WAVES)))
-k_trace_closest_lp(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
-                   yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
-                   unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<true, 8, true, false, YK_COOP_LP>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
-}
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_LP_WAVES)))
-k_trace_shadow_lp(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
-                  yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
-                  unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false, 1, true, false, YK_COOP_LP>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+  trace_body<false, 1>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 // transparent shadows (scene_t::isShadowed(state, ray, maxDepth, filt),
 // scene.cc:904-928 -> IntersectTS): occlusion + filter colour per ray
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_LP_WAVES)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5)))
 k_trace_shadow_ts(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                   uint8_t* __restrict__ occl, float* __restrict__ tsf, int ts_depth, unsigned long long* __restrict__ work,
                   unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false, 1, false, true>(S, rays, idx, n, nullptr, occl, work, ctr, ovf, ovf_depth, refill_min, tsf,
+  trace_body<false, 1, true>(S, rays, idx, n, nullptr, occl, work, ctr, ovf, ovf_depth, refill_min, tsf,
                                     ts_depth);
 }
 
@@ -1457,31 +1278,13 @@ __device__ __forceinline__ bool dirac_illum(const DLight& L, v3 P, v3& ldir, flo
 // returning atomics serialise on it; measured 1068 -> 1263 Mrays/s (photon
 // mapping, 32 gather launches of 33M threads per batch) and 2008 -> 2038
 // (path tracing).
-#ifndef YK_BLOCK_APPEND
-#define YK_BLOCK_APPEND 1
-#endif
 // Block sizes of the kernels that append to ray queues (fewer, larger blocks
 // = fewer returning atomics on the queue word). Measured: path-tracing
-// shading at 1024 threads 2038 -> 2075 Mrays/s; the photon / final-gather
-// kernels best at 512 (1261 -> 1274; 1024: 1240).
-#ifndef YK_PRIMARY_BLOCK
-#define YK_PRIMARY_BLOCK YK_SHADE_BLOCK  // k_shade_primary's block (its own knob)
-#endif
-#ifndef YK_SHADE_BLOCK
+// shading at 1024 threads 2038 -> 2075 Mrays/s (k_shade_primary at 512:
+// 2744 against 2811); the photon / final-gather kernels best at 512
+// (1261 -> 1274; 1024: 1240).
 #define YK_SHADE_BLOCK 1024
-#endif
-#ifndef YK_APPEND_BLOCK
 #define YK_APPEND_BLOCK 512
-#endif
-// shadow-slot layout: k-major (slot_of) or the sample-major c * K + k
-#ifndef YK_SLOT_KMAJOR
-#define YK_SLOT_KMAJOR 1
-#endif
-// k_shade_bounce packs a block's hits onto its first threads (escaped paths
-// finish first)
-#ifndef YK_PACK_HITS
-#define YK_PACK_HITS 1
-#endif
 // Reserves m_s shadow-queue and m_b bounce-queue entries with ONE returning
 // atomic per wave: the counter word holds (bounce count << 32) | shadow
 // count. Whole-wave call; returns each lane's first index in both queues.
@@ -1496,7 +1299,6 @@ __device__ __forceinline__ void wave_append2(unsigned long long* counter, unsign
     if (lane >= off) incl += ((unsigned long long)hi << 32) | lo;
   }
   const unsigned long long total = shfl_u64(incl, 63);
-#if YK_BLOCK_APPEND
   // one returning atomic per block: wave totals meet in LDS (all callers
   // reach this point with whole blocks)
   __shared__ unsigned long long s_tot[16];
@@ -1513,11 +1315,6 @@ __device__ __forceinline__ void wave_append2(unsigned long long* counter, unsign
   unsigned long long base = s_base;
   for (int k = 0; k < w; ++k) base += s_tot[k];
   base += incl - m;
-#else
-  unsigned long long base = 0;
-  if (lane == 63 && total) base = atomicAdd(counter, total);
-  base = shfl_u64(base, 63) + incl - m;
-#endif
   base_s = (unsigned)base;
   base_b = (unsigned)(base >> 32);
 }
@@ -1599,11 +1396,7 @@ struct Batch {
   float* sl_aux;        // 4 per slot: scalar factors (and the Dirac light colour)
 };
 __device__ __forceinline__ long long slot_of(const Batch& B, long long c, int k) {
-#if YK_SLOT_KMAJOR
-  return (long long)k * B.cap + c;
-#else
-  return c * B.K + k;
-#endif
+  return (long long)k * B.cap + c;  // k-major (sample-major c * K + k: C2 7810 against 8047 Mrays/s)
 }
 
 struct RenderConst {
@@ -1867,15 +1660,9 @@ __device__ __forceinline__ yk_ray path_first_segment(const Batch& B, const Rende
 // Camera-ray hit (pathtracer.cc:146-160, directlight.cc:124-135): emission
 // and the estimateAllDirectLight shadow rays; for the path tracer also the
 // first segment of sub-path 0 (appended to bounce queue 1).
-#ifndef YK_SHADE_WAVES
-#define YK_SHADE_WAVES 0  // 0: compiler's choice (128 / 122 VGPRs -> 4 waves per SIMD)
-#endif
-#if YK_SHADE_WAVES > 0
-#define YK_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(YK_SHADE_WAVES)))
-#else
-#define YK_SHADE_ATTR
-#endif
-__global__ void __launch_bounds__(YK_PRIMARY_BLOCK) YK_SHADE_ATTR k_shade_primary(DScene S, Batch B, RenderConst R, long long nc,
+// Shading kernels run at the compiler's register choice (128 / 122 VGPRs, 4
+// waves per SIMD); forcing 5 or 6 spilled 124-200 B per lane and lost 2-4 %.
+__global__ void __launch_bounds__(YK_SHADE_BLOCK) k_shade_primary(DScene S, Batch B, RenderConst R, long long nc,
                                                        unsigned long long* __restrict__ qword) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = c < nc;
@@ -2055,7 +1842,7 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) k_path_start(DScene S, Batch B
 // (pathtracer.cc:189-298): estimateOneDirectLight shadow rays, emission,
 // and the BSDF sample of the next segment. One thread per live path (entry
 // qi of the input bounce queue, owned by camera sample c).
-__global__ void __launch_bounds__(YK_SHADE_BLOCK) YK_SHADE_ATTR k_shade_bounce(DScene S, Batch B, RenderConst R,
+__global__ void __launch_bounds__(YK_SHADE_BLOCK) k_shade_bounce(DScene S, Batch B, RenderConst R,
                                                       const unsigned long long* __restrict__ qin_word, int depth,
                                                       int isub, int qin, unsigned long long* __restrict__ qword) {
   const long long nq = (long long)(*qin_word >> 32);  // live paths (device-side count)
@@ -2079,13 +1866,9 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) YK_SHADE_ATTR k_shade_bounce(D
       }
       B.pstate[c] = 0;
     }
-#if YK_PACK_HITS
     int src;
     valid = pack_block<YK_SHADE_BLOCK>(valid && prim >= 0, src);
     qi = qb + src;
-#else
-    valid = valid && prim >= 0;
-#endif
   }
   const long long c = valid ? B.q_owner[qin][qi] : 0;
   int nr = 0, kend = 0;
@@ -2403,10 +2186,7 @@ struct FilmConst {
 };
 
 __device__ __forceinline__ int round2int(double v) { return (int)(v + (0.5 - 1.4e-11)); }
-#ifndef YK_GATHER_GROUP
-#define YK_GATHER_GROUP 8
-#endif
-constexpr int kGatherGroup = YK_GATHER_GROUP;
+constexpr int kGatherGroup = 8;  // samples loaded per group (16 measured equal)
 __device__ __forceinline__ int floor2int(double v) { return (int)floor(v); }
 
 // imageFilm_t::addSample as a gather (imagefilm.cc:453-511): each thread owns
@@ -2747,8 +2527,7 @@ struct yk_device {
   DScene S{};
   int ntris = 0, max_depth = 0, nlights = 0, sum_light_slots = 0;
   bool spec = false;  // some material has SPECULAR|FILTER components: recursion pipeline
-  bool crowded_leaves = false;  // mean references per non-empty leaf above kCrowdedLeaf: PIPE leaf loop
-  int per_cu_lp[2] = {1, 1};
+  bool crowded_leaves = false;  // mean references per non-empty leaf above YK_CROWDED_LEAF: 64-ray hand-out chunks
   int per_cu_ts = 1;
   // node store of the specular recursion (k_finish_spec / k_spawn / k_fold)
   DBuf<float> nE, nD, nP, nrcol, nalpha, nmalpha;
@@ -2988,12 +2767,11 @@ int refill_min() {
 template <bool CLOSEST>
 void enqueue_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* idx, RayCount n, yk_hit* hits,
                    uint8_t* occ, unsigned long long* work, unsigned long long* acc, hipEvent_t ev0, hipEvent_t ev1) {
-  const bool lp = d->crowded_leaves;
-  const long long grid = (long long)d->cus * (lp ? d->per_cu_lp[CLOSEST] : d->per_cu[CLOSEST]);
-  const int ovf_depth = std::max(1, stack_depth(d) - (kLdsRay ? std::min(kStackLds, YK_LDS_RAY_RING) : kStackLds));
+  const long long grid = (long long)d->cus * d->per_cu[CLOSEST];
+  const int ovf_depth = std::max(1, stack_depth(d) - kStackLds);
   P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
   if (ev0) HIPCHK(hipEventRecord(ev0, P.stream));
-  auto kern = CLOSEST ? (lp ? k_trace_closest_lp : k_trace_closest) : (lp ? k_trace_shadow_lp : k_trace_shadow);
+  auto kern = CLOSEST ? k_trace_closest : k_trace_shadow;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays, idx, n, hits, occ, work, acc,
                      P.ovf.p, ovf_depth, refill_min());
   HIPCHK(hipGetLastError());
@@ -3005,7 +2783,7 @@ void enqueue_trace_ts(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned*
                       float* filt, int max_depth, unsigned long long* work, unsigned long long* acc, hipEvent_t ev0,
                       hipEvent_t ev1) {
   const long long grid = (long long)d->cus * d->per_cu_ts;
-  const int ovf_depth = std::max(1, stack_depth(d) - (kLdsRay ? std::min(kStackLds, YK_LDS_RAY_RING) : kStackLds));
+  const int ovf_depth = std::max(1, stack_depth(d) - kStackLds);
   P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
   if (ev0) HIPCHK(hipEventRecord(ev0, P.stream));
   hipLaunchKernelGGL(k_trace_shadow_ts, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays, idx, n, occ, filt,
@@ -3060,23 +2838,21 @@ inline unsigned grid_for(long long n, int b = 256) { return (unsigned)((n + b - 
 void install_traversal(yk_device* d, size_t nn, size_t nleaf, uint32_t max_leaf_refs) {
   // traversal stack entries hold (node + 1) in 30 bits
   if (nn >= (1u << 30) - 1u) throw std::invalid_argument("kd-tree has 2^30 - 1 nodes or more");
-  if (kOwnerScan && max_leaf_refs >= (1u << 17))
+  if (max_leaf_refs >= (1u << 17))
     throw std::invalid_argument("kd-tree leaf with 2^17 references or more (coop_leaves owner keys)");
   HIPCHK(hipDeviceSynchronize());  // every copy into nodes / leaf / tris has landed
-  if (kLeafTris && nleaf) {
+  if (nleaf) {
     d->ltris.ensure(kTriWords * nleaf);
     hipLaunchKernelGGL(k_gather_leaf_tris, dim3(grid_for((long long)nleaf)), dim3(256), 0, d->stream, d->tris.p,
                        d->leaf.p, d->ltris.p, (unsigned)nleaf);
     HIPCHK(hipGetLastError());
   }
-  d->S.ltris = (kLeafTris && nleaf) ? d->ltris.p : nullptr;
-  if (kPackets) {
-    d->pk.ensure(kPkWords * nn);
-    hipLaunchKernelGGL(k_pack_nodes, dim3(grid_for((long long)nn)), dim3(256), 0, d->stream, d->nodes.p, d->pk.p,
-                       (unsigned)nn);
-    HIPCHK(hipGetLastError());
-  }
-  d->S.pk = kPackets ? d->pk.p : nullptr;
+  d->S.ltris = nleaf ? d->ltris.p : nullptr;
+  d->pk.ensure(kPkWords * nn);
+  hipLaunchKernelGGL(k_pack_nodes, dim3(grid_for((long long)nn)), dim3(256), 0, d->stream, d->nodes.p, d->pk.p,
+                     (unsigned)nn);
+  HIPCHK(hipGetLastError());
+  d->S.pk = d->pk.p;
   HIPCHK(hipStreamSynchronize(d->stream));
 }
 
@@ -3106,10 +2882,6 @@ int yk_device_open(int32_t ordinal, yk_device** out) {
   d->per_cu[0] = std::max(1, blocks);
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_closest, 64, 0));
   d->per_cu[1] = std::max(1, blocks);
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow_lp, 64, 0));
-  d->per_cu_lp[0] = std::max(1, blocks);
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_closest_lp, 64, 0));
-  d->per_cu_lp[1] = std::max(1, blocks);
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow_ts, 64, 0));
   d->per_cu_ts = std::max(1, blocks);
   upload_qmc();
@@ -3156,11 +2928,9 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
     r[2] = t[2];
     const uint32_t pid = (uint32_t)p;
     std::memcpy(&r[3], &pid, 4);
-    // e1 at words 4-6; e2 at 8-10 (48 B) or 7-9 (40 B)
-    const int e2at = kTriWords == 12 ? 8 : 7;
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 3; ++k) {  // e1 at words 4-6, e2 at 8-10
       r[4 + k] = e[k];
-      r[e2at + k] = e[3 + k];
+      r[8 + k] = e[3 + k];
     }
     float nw;
     int m = S.tri_material[p] | (S.tri_smooth[p] ? kSmoothBit : 0);
@@ -3684,7 +3454,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
         HIPCHK(hipMemsetAsync(d->spec_words.p, 0, d->spec_words.n * sizeof(unsigned long long), P.stream));
         launch = 0;
         trace(true, Bc.p_rays, nullptr, RayCount{nullptr, 0, n}, Bc.p_hits, nullptr);
-        hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(n, YK_PRIMARY_BLOCK)), dim3(YK_PRIMARY_BLOCK), 0, P.stream, d->S, Bc, Rc, n, qw(0, 0));
+        hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(n, YK_SHADE_BLOCK)), dim3(YK_SHADE_BLOCK), 0, P.stream, d->S, Bc, Rc, n, qw(0, 0));
         HIPCHK(hipGetLastError());
         trace(false, Bc.s_rays, Bc.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, Bc.s_occl);
         hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(n)), dim3(256), 0, P.stream, Bc, Rc, n);
@@ -3745,7 +3515,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     }
     if (!d->spec) {
     trace(true, B.p_rays, nullptr, RayCount{nullptr, 0, nc}, B.p_hits, nullptr);
-    hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(nc, YK_PRIMARY_BLOCK)), dim3(YK_PRIMARY_BLOCK), 0, P.stream, d->S, B, R, nc, qw(0, 0));
+    hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(nc, YK_SHADE_BLOCK)), dim3(YK_SHADE_BLOCK), 0, P.stream, d->S, B, R, nc, qw(0, 0));
     HIPCHK(hipGetLastError());
     trace(false, B.s_rays, B.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, B.s_occl);
     hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
