@@ -598,7 +598,12 @@ __device__ __forceinline__ unsigned dpp_max_scan(unsigned x) {
 }
 
 // Wave-uniform: every lane calls it; nref = 0 for lanes without a leaf to test.
-template <bool CLOSEST>
+// BIG: trees with a leaf of 2^17 references or more (degenerate or heavily
+// overlapping geometry at maxDepth), whose absolute range starts overflow the
+// 24-bit owner keys: the keys then hold the start relative to the round and
+// the owner's start is read from its lane (one cross-lane read more per
+// round; measured 0.7 % slower, so only such trees run it).
+template <bool CLOSEST, bool BIG = false>
 __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t nref, uint32_t w0, int lane,
                                             unsigned long long* keys, float4* cand, unsigned* otab,
                                             unsigned& ntris, bool& occluded) {
@@ -622,10 +627,11 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
     const unsigned s = base + (unsigned)lane;
     const unsigned sc = min(s, total - 1u);
     // owner of slot s: the last lane whose range starts at or before s
-    // keys hold (range start + 1) << 8 in 32 bits: install_traversal caps
-    // leaves below 2^17 references (64 lanes x 2^17 < 2^24)
+    // keys hold (range start + 1) << 8 in 32 bits: without BIG every leaf has
+    // fewer than 2^17 references (64 lanes x 2^17 < 2^24)
     otab[lane] = 0u;
-    if (nref > 0u && pre >= base && pre - base < 64u) otab[pre - base] = ((pre + 1u) << 8) | (unsigned)lane;
+    if (nref > 0u && pre >= base && pre - base < 64u)
+      otab[pre - base] = ((BIG ? pre - base + 1u : pre + 1u) << 8) | (unsigned)lane;
     __syncthreads();
     const unsigned ov = dpp_max_scan(otab[lane]);
     // slots before the round's first range start continue the range that
@@ -633,7 +639,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
     const unsigned okey = ov ? ov : carry;
     carry = (unsigned)__builtin_amdgcn_readlane((int)okey, 63);
     const int own = (int)(okey & 0xFFu);
-    const unsigned pown = (okey >> 8) - 1u;
+    const unsigned pown = BIG ? (unsigned)__shfl((int)pre, own) : (okey >> 8) - 1u;
     const unsigned k = sc - pown;
     const uint32_t ow0 = (uint32_t)__shfl((int)w0, own), on = (uint32_t)__shfl((int)nref, own);
     const v3 ro = V3(__shfl(st.o.x, own), __shfl(st.o.y, own), __shfl(st.o.z, own));
@@ -713,7 +719,7 @@ struct RayCount {
   }
 };
 
-template <bool CLOSEST, int NSEG, bool TS = false>
+template <bool CLOSEST, int NSEG, bool TS = false, bool BIG = false>
 __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx,
                                            RayCount rc, yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
                                            unsigned long long* __restrict__ work, unsigned long long* __restrict__ ctr,
@@ -845,7 +851,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       bool paused = false;
       if (act) live = trav_descend<CLOSEST>(S, st, stk, nnodes, w0, nref, paused);
       bool occ = false;
-      coop_leaves<CLOSEST>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, otab, ntris, occ);
+      coop_leaves<CLOSEST, BIG>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, otab, ntris, occ);
       if (act) {
         bool done = !live || occ || (!paused && trav_next<CLOSEST>(S, st, stk));
         if (runaway) {
@@ -951,6 +957,19 @@ k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __rest
                yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
   trace_body<false, 1>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+}
+// trees with a leaf of 2^17 references or more (coop_leaves BIG)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
+k_trace_closest_big(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+                    yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
+                    unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
+  trace_body<true, 8, false, true>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+}
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
+k_trace_shadow_big(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+                   yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
+                   unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
+  trace_body<false, 1, false, true>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 // transparent shadows (scene_t::isShadowed(state, ray, maxDepth, filt),
 // scene.cc:904-928 -> IntersectTS): occlusion + filter colour per ray
@@ -2511,6 +2530,7 @@ struct yk_device {
   int ordinal = 0;
   int cus = 0;
   int per_cu[2] = {1, 1};  // resident trace waves per CU: [0] any-hit, [1] closest
+  int per_cu_big[2] = {1, 1};  // the same for the BIG-leaf kernels
   hipStream_t stream = nullptr;  // = pipe[0].stream (ray queries, film resolve)
   bool uploaded = false;
   const yk_scene* uploaded_scene = nullptr;  // the scene the resident arrays came from
@@ -2527,6 +2547,7 @@ struct yk_device {
   DScene S{};
   int ntris = 0, max_depth = 0, nlights = 0, sum_light_slots = 0;
   bool spec = false;  // some material has SPECULAR|FILTER components: recursion pipeline
+  bool big_leaves = false;  // the resident tree has a leaf of 2^17 references or more: *_big kernels
   bool crowded_leaves = false;  // mean references per non-empty leaf above YK_CROWDED_LEAF: 64-ray hand-out chunks
   int per_cu_ts = 1;
   // node store of the specular recursion (k_finish_spec / k_spawn / k_fold)
@@ -2767,11 +2788,12 @@ int refill_min() {
 template <bool CLOSEST>
 void enqueue_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* idx, RayCount n, yk_hit* hits,
                    uint8_t* occ, unsigned long long* work, unsigned long long* acc, hipEvent_t ev0, hipEvent_t ev1) {
-  const long long grid = (long long)d->cus * d->per_cu[CLOSEST];
+  const long long grid = (long long)d->cus * (d->big_leaves ? d->per_cu_big[CLOSEST] : d->per_cu[CLOSEST]);
   const int ovf_depth = std::max(1, stack_depth(d) - kStackLds);
   P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
   if (ev0) HIPCHK(hipEventRecord(ev0, P.stream));
-  auto kern = CLOSEST ? k_trace_closest : k_trace_shadow;
+  auto kern = CLOSEST ? (d->big_leaves ? k_trace_closest_big : k_trace_closest)
+                      : (d->big_leaves ? k_trace_shadow_big : k_trace_shadow);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays, idx, n, hits, occ, work, acc,
                      P.ovf.p, ovf_depth, refill_min());
   HIPCHK(hipGetLastError());
@@ -2832,14 +2854,17 @@ void launch_trace(yk_device* d, Pipe& P, const yk_ray* rays, long long n, yk_hit
 }
 
 inline unsigned grid_for(long long n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+// traversal stack entries hold (node + 1) in 30 bits
+constexpr size_t kMaxNodes = (1u << 30) - 2u;
+// leaves of this many references need the BIG owner keys (coop_leaves)
+constexpr uint32_t kBigLeaf = 1u << 17;
 
 // Traversal copies of the resident tree: the leaf-ordered triangles
 // (k_gather_leaf_tris) and the node packets (k_pack_nodes).
+// Callers check the node count (kMaxNodes) before they touch any resident
+// buffer, so a refused tree leaves the previous one intact.
 void install_traversal(yk_device* d, size_t nn, size_t nleaf, uint32_t max_leaf_refs) {
-  // traversal stack entries hold (node + 1) in 30 bits
-  if (nn >= (1u << 30) - 1u) throw std::invalid_argument("kd-tree has 2^30 - 1 nodes or more");
-  if (max_leaf_refs >= (1u << 17))
-    throw std::invalid_argument("kd-tree leaf with 2^17 references or more (coop_leaves owner keys)");
+  d->big_leaves = max_leaf_refs >= kBigLeaf;
   HIPCHK(hipDeviceSynchronize());  // every copy into nodes / leaf / tris has landed
   if (nleaf) {
     d->ltris.ensure(kTriWords * nleaf);
@@ -2882,6 +2907,10 @@ int yk_device_open(int32_t ordinal, yk_device** out) {
   d->per_cu[0] = std::max(1, blocks);
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_closest, 64, 0));
   d->per_cu[1] = std::max(1, blocks);
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow_big, 64, 0));
+  d->per_cu_big[0] = std::max(1, blocks);
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_closest_big, 64, 0));
+  d->per_cu_big[1] = std::max(1, blocks);
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow_ts, 64, 0));
   d->per_cu_ts = std::max(1, blocks);
   upload_qmc();
@@ -2914,8 +2943,26 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   if (!S.has_camera) return set_error(YK_ERR_STATE, "yk_device_upload: scene has no camera");
   if ((int)S.material_states.size() > kMaxMats) return set_error(YK_ERR_UNSUPPORTED, "too many materials");
   if ((int)S.light_states.size() > kMaxLights) return set_error(YK_ERR_UNSUPPORTED, "too many lights");
+  if (S.tree.nodes.size() / 2 > kMaxNodes) return set_error(YK_ERR_UNSUPPORTED, "kd-tree has 2^30 - 1 nodes or more");
+  {
+    int slots = 0;  // shadow slots per doLightEstimation sweep (DLight.nslots)
+    for (size_t i = 0; i < S.light_states.size(); ++i) {
+      if (S.light_kind[i] != YK_LIGHT_AREA) {
+        slots += 1;
+      } else if (S.light_states[i].samples < 1) {
+        return set_error(YK_ERR_ARG, "light samples must be >= 1");
+      } else {
+        slots += 2 * S.light_states[i].samples;
+      }
+    }
+    if (slots > 8192) return set_error(YK_ERR_UNSUPPORTED, "too many light samples per shading point");
+  }
   YK_GUARD_BEGIN
   HIPCHK(hipSetDevice(d->ordinal));
+  // the resident arrays are replaced below: until that has succeeded the
+  // device holds no usable scene
+  d->uploaded = false;
+  d->uploaded_scene = nullptr;
   const int nt = (int)S.tri_material.size();
   std::vector<float> tris((size_t)nt * kTriWords, 0.f);
   std::vector<float4> ng(nt);
@@ -2966,7 +3013,6 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   int sum_slots = 0;
   for (size_t i = 0; i < S.light_states.size(); ++i) {
     if (S.light_kind[i] == YK_LIGHT_AREA) {
-      if (S.light_states[i].samples < 1) return set_error(YK_ERR_ARG, "light samples must be >= 1");
       lights.push_back(make_light(S.light_states[i]));
     } else {
       lights.push_back(make_dirac_light(S.dirac_states[i]));
@@ -2974,7 +3020,6 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
     }
     sum_slots += lights.back().nslots;
   }
-  if (sum_slots > 8192) return set_error(YK_ERR_UNSUPPORTED, "too many light samples per shading point");
   d->sum_light_slots = sum_slots;
   d->lights_host = lights;
   d->pm_ready = false;

@@ -261,3 +261,23 @@ def test_object_state_scene_renders_identically(gpu_device):
     gpu_device.upload(t)
     b = gpu_device.render(p)
     assert (a.view(np.uint32) == b.view(np.uint32)).all()
+
+
+def test_refused_upload_keeps_the_resident_scene(gpu_device):
+    """An upload refused by validation (here an area light with 0 samples)
+    leaves the previously uploaded scene resident and bit-exact; the checks run
+    before any resident buffer is touched."""
+    from core_amd.scene import Scene
+    s, _, orc = scene("cornell_pt", 64, 64)
+    gpu_device.upload(s)
+    bad = Scene()
+    bad.generate("cornell_pt", 16, 16)
+    bad.add_area_light((-0.1, 1.9, -0.1), (0.1, 1.9, -0.1), (-0.1, 1.9, 0.1), samples=0)
+    bad.build()
+    with pytest.raises(A.YkError) as e:
+        gpu_device.upload(bad)
+    assert e.value.code == A.YK_ERR_ARG
+    rays = _ray_batch(s, 3)
+    prim, t, *_ = orc.intersect(rays)
+    gp, gt, *_ = gpu_device.split_hits(gpu_device.trace_closest(gpu_device.rays_to_device(rays)))
+    assert (gp == prim).all() and (gt[prim >= 0].view(np.uint32) == t[prim >= 0].view(np.uint32)).all()
