@@ -63,7 +63,13 @@ def main():
                          "documented tie-break; not the parity default)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC HBM-traffic summary (tools/pmc_traffic.py output) to attach, if present")
+    ap.add_argument("--pipes", type=int, default=0,
+                    help="batch pipelines of the timed frames (default: libyk's 4; 1 serialises the kernels)")
+    ap.add_argument("--no-roofline-frame", action="store_true",
+                    help="skip the extra serialised frame the roofline line is measured on")
     args = ap.parse_args()
+    if args.pipes:
+        os.environ["YK_PIPES"] = str(args.pipes)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -141,40 +147,29 @@ def main():
     rays = w[0] + w[1]
     value = rays / elapsed / 1e6
 
+    # Roofline frame: one more frame (not part of `value`) with the kernels
+    # serialised on one pipeline (YK_PIPES=1), so that each traversal
+    # launch's HIP-event duration is its own and not time shared with the
+    # other pipes' kernels. rocprofv3 --kernel-trace --stats of
+    # `bench.py --pipes 1` gives the same per-launch averages (profiles/).
+    rst = None
+    if not args.no_roofline_frame:
+        prev = os.environ.get("YK_PIPES")
+        os.environ["YK_PIPES"] = "1"
+        rst = A.yk_stats()
+        barrier()
+        step(rst)
+        barrier()
+        if prev is None:
+            del os.environ["YK_PIPES"]
+        else:
+            os.environ["YK_PIPES"] = prev
+
     if rank != 0:
         dist.destroy_process_group()
         return
 
-    # roofline of the dominant kernel, from HIP events on the kernel's stream
-    kc = dict(name="k_trace_closest", launches=w[6], ms=ms_c,
-              bytes=algorithmic_bytes(w[0], w[2], w[3], 16))
-    ks = dict(name="k_trace_shadow", launches=w[7], ms=ms_s,
-              bytes=algorithmic_bytes(w[1], w[4], w[5], 1))
-    for k in (kc, ks):
-        k["gbs"] = k["bytes"] / (k["ms"] * 1e-3) / 1e9 if k["ms"] > 0 else 0.0
-        k["avg_ms"] = k["ms"] / max(k["launches"], 1)
-    dom = kc if kc["ms"] >= ks["ms"] else ks
-    traffic = None
-    traffic_note = None
-    if os.path.exists(args.traffic) and args.scene == "bumpy" and pm_info is None:  # PMC summary of the PT bumpy run
-        with open(args.traffic) as f:
-            tj = json.load(f)
-        key = "closest" if dom is kc else "shadow"
-        if key in tj:
-            traffic = tj[key].get("hbm_bytes_per_launch")
-            traffic_note = tj.get("source")
-    roofline = {"bound": "hbm", "achieved": round(dom["gbs"], 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": dom["name"], "avg_launch_ms": round(dom["avg_ms"], 4),
-                "algorithmic_bytes_per_launch": round(dom["bytes"] / max(dom["launches"], 1)),
-                "other_kernel": {"name": (ks if dom is kc else kc)["name"],
-                                 "achieved": round((ks if dom is kc else kc)["gbs"], 2)}}
-    if traffic_note:
-        roofline["traffic_source"] = traffic_note
-    # two batch pipelines overlap on the GPU, so event-timed kernel durations
-    # include time shared with the other pipe; the wall-clock aggregate of all
-    # traversal bytes is reported beside the per-kernel figure
-    roofline["traversal_achieved_wall"] = round((kc["bytes"] + ks["bytes"]) / elapsed / 1e9, 2)
+    roofline = roofline_line(args, w, ms_c, ms_s, rst, elapsed, pm_info is None)
 
     cpu = None
     if not args.no_cpu:
@@ -227,9 +222,68 @@ def main():
         dist.destroy_process_group()
 
 
+def roofline_line(args, w, ms_c, ms_s, rst, elapsed, pt):
+    """Roofline of the dominant traversal kernel. Durations come from the
+    serialised roofline frame (rst) when it ran, else from the timed frames'
+    HIP events (overlapped by the other pipes: a lower bound on the rate)."""
+    if rst is not None:
+        cnt = [rst.closest_rays, rst.shadow_rays, rst.closest_nodes, rst.closest_tris, rst.shadow_nodes,
+               rst.shadow_tris, rst.closest_launches, rst.shadow_launches]
+        ms = (rst.ms_closest, rst.ms_shadow)
+        timing = "serialised frame (YK_PIPES=1): HIP events around every launch on its stream"
+    else:
+        cnt = list(w[:8])
+        ms = (ms_c, ms_s)
+        timing = "timed frames: HIP events around every launch, overlapped by the other pipes"
+    kc = dict(name="k_trace_closest", launches=cnt[6], ms=ms[0], bytes=algorithmic_bytes(cnt[0], cnt[2], cnt[3], 16))
+    ks = dict(name="k_trace_shadow", launches=cnt[7], ms=ms[1], bytes=algorithmic_bytes(cnt[1], cnt[4], cnt[5], 1))
+    for k in (kc, ks):
+        k["gbs"] = k["bytes"] / (k["ms"] * 1e-3) / 1e9 if k["ms"] > 0 else 0.0
+        k["avg_ms"] = k["ms"] / max(k["launches"], 1)
+    dom, other = (kc, ks) if kc["ms"] >= ks["ms"] else (ks, kc)
+    traffic = traffic_note = None
+    if os.path.exists(args.traffic) and args.scene == "bumpy" and pt:  # PMC summary of the PT bumpy run
+        with open(args.traffic) as f:
+            tj = json.load(f)
+        key = "closest" if dom is kc else "shadow"
+        if key in tj:
+            traffic = tj[key].get("hbm_bytes_per_launch")
+            traffic_note = tj.get("source")
+    out = {"bound": "hbm", "achieved": round(dom["gbs"], 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
+           "kernel": dom["name"], "avg_launch_ms": round(dom["avg_ms"], 4), "launches": int(dom["launches"]),
+           "algorithmic_bytes_per_launch": round(dom["bytes"] / max(dom["launches"], 1)), "timing": timing,
+           "other_kernel": {"name": other["name"], "achieved": round(other["gbs"], 2),
+                            "avg_launch_ms": round(other["avg_ms"], 4),
+                            "frac": round(other["gbs"] / HBM_PEAK_GBS, 4)}}
+    if traffic:
+        # counter view: measured HBM bytes per launch over the same duration
+        out["traffic_gbs"] = round(traffic / (dom["avg_ms"] * 1e-3) / 1e9, 2)
+        out["frac_traffic"] = round(out["traffic_gbs"] / HBM_PEAK_GBS, 4)
+        out["traffic_source"] = traffic_note
+    # all traversal bytes of the timed frames over their wall time
+    out["traversal_achieved_wall"] = round((algorithmic_bytes(w[0], w[2], w[3], 16) +
+                                            algorithmic_bytes(w[1], w[4], w[5], 1)) / elapsed / 1e9, 2)
+    return out
+
+
+def host_threads():
+    """Host cores this process may use: its CPU affinity, capped by
+    OMP_NUM_THREADS where the box sets it to the job's CPU share."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
+
+
 def cpu_baseline(scene, p, seconds):
-    """The oracle (scalar C restatement, 1 thread) on a bounded crop of the
-    same frame: rays/s scaled from a short probe to about `seconds` of work."""
+    """The oracle (the C restatement of the reference's CPU path) on all host
+    cores, on a bounded centred crop of the same frame: like the reference's
+    tiledIntegrator_t::render (integrator.cc:177-211), every thread renders
+    tiles, here the shards t % (4 threads) == k. The crop is sized from a
+    1-thread probe to about `seconds` of wall time."""
+    from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, ROOT)
     from oracle.oracle import Oracle
     orc = Oracle(scene)
@@ -239,20 +293,23 @@ def cpu_baseline(scene, p, seconds):
     q.width, q.height = 16, 16
     q.xstart, q.ystart = p.width // 2, p.height // 2
     t0 = time.perf_counter()
-    _, _, c = orc.render(q)
+    orc.render(q)  # also initialises the oracle's shared tables before the threads start
     probe = time.perf_counter() - t0
-    # grow the crop to ~`seconds` of work (square, centred)
-    px = max(256, int(16 * 16 * seconds / max(probe, 1e-3)))
+    nt = host_threads()
+    # grow the crop to ~`seconds` of wall time on nt threads (square, centred)
+    px = max(256, int(16 * 16 * seconds * nt / max(probe, 1e-3)))
     side = int(np.sqrt(px))
     q.width, q.height = min(side, p.width), min(side, p.height)
     q.xstart, q.ystart = (p.width - q.width) // 2, (p.height - q.height) // 2
+    nsh = 4 * nt
     t0 = time.perf_counter()
-    _, _, c = orc.render(q)
+    with ThreadPoolExecutor(max_workers=nt) as ex:  # ctypes releases the GIL inside orc_render_shard
+        res = list(ex.map(lambda k: orc.render_shard(q, k, nsh)[1], range(nsh)))
     dt = time.perf_counter() - t0
-    r = c["closest"] + c["shadow"]
-    return {"value": round(r / dt / 1e6, 4), "unit": "Mrays/s", "cores": 1, "kind": "port",
-            "sample": f"oracle, 1 thread: {q.width}x{q.height} crop at ({q.xstart},{q.ystart}) of the same "
-                      f"frame, {p.aa_samples} spp, {r} rays in {dt:.1f} s"}
+    r = sum(c["closest"] + c["shadow"] for c in res)
+    return {"value": round(r / dt / 1e6, 4), "unit": "Mrays/s", "cores": nt, "kind": "port",
+            "sample": f"oracle on {nt} threads ({nsh} tile shards): {q.width}x{q.height} crop at "
+                      f"({q.xstart},{q.ystart}) of the same frame, {p.aa_samples} spp, {r} rays in {dt:.1f} s"}
 
 
 if __name__ == "__main__":

@@ -176,6 +176,7 @@ SIGNATURES = {
     "yk_render_shard": (C.c_int, [P, C.POINTER(yk_render_params), i32, i32, P, C.POINTER(yk_stats)]),
     "yk_film_resolve": (C.c_int, [P, C.POINTER(yk_render_params), P, P]),
     "yk_render_film": (C.c_int, [P, C.POINTER(yk_render_params), i32, i32, fp, C.POINTER(yk_stats)]),
+    "yk_render_multi": (C.c_int, [C.POINTER(P), i32, C.POINTER(yk_render_params), fp, C.POINTER(yk_stats)]),
     "yk_render": (C.c_int, [P, C.POINTER(yk_render_params), fp, C.POINTER(yk_stats)]),
     "yk_photon_build": (C.c_int, [P, C.POINTER(yk_render_params), C.POINTER(yk_photon_info)]),
     "yk_photon_export": (C.c_int, [P, i32, fp, i32, i32p]),

@@ -22,6 +22,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/yk_api.h"
@@ -2302,6 +2303,12 @@ __global__ void __launch_bounds__(256) k_film_gather(FilmConst F, const float4* 
   px[4] = aW;
 }
 
+// acc += src, film sums of another shard (yk_render_multi's reduce)
+__global__ void k_film_add(float* __restrict__ acc, const float* __restrict__ src, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) acc[i] = acc[i] + src[i];
+}
+
 // imageFilm_t::nextPass (imagefilm.cc:213-271): flag the pixels whose
 // brightness differs from a neighbour's by >= threshold. Compiled form: the
 // centre as abscol2bri of col*(1/w); each neighbour folded as
@@ -2521,10 +2528,16 @@ struct Pipe {
   }
 };
 
-#ifndef YK_PIPES
-#define YK_PIPES 4  // measured: 2 -> 1873, 3 -> 1892, 4 -> 1923 Mrays/s (1M-tri frame)
-#endif
-constexpr int kPipes = YK_PIPES;
+// Batch pipelines (streams) in flight. Measured: 2 -> 1873, 3 -> 1892, 4 ->
+// 1923 Mrays/s (round 1); 2 / 6 -> 2794 / 2790 against 2803 with 4 (round 2).
+// YK_PIPES=1 serialises the kernels of a frame (each kernel's duration is then
+// its own, for the roofline measurement in bench.py), read on every render.
+constexpr int kPipes = 4;
+inline int pipes_env() {
+  const char* e = std::getenv("YK_PIPES");
+  const int v = e ? std::atoi(e) : 0;
+  return (v >= 1 && v <= kPipes) ? v : kPipes;
+}
 
 struct yk_device {
   int ordinal = 0;
@@ -3303,7 +3316,8 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     return (v > 0 && v <= 240 ? v : 64ll) << 30;
   }();
   const long long bytes_per_sample = 400 + 52ll * K;
-  const long long target = std::max(1ll << 20, std::min(target_env, batch_bytes / kPipes / bytes_per_sample));
+  const int pipes_cfg = pipes_env();
+  const long long target = std::max(1ll << 20, std::min(target_env, batch_bytes / pipes_cfg / bytes_per_sample));
   const long long tile_samples = (long long)F.tile * F.tile * spp;
   if (d->spec && spec_worst * tile_samples * kNodeBytes > (48ll << 30))
     return set_error(YK_ERR_UNSUPPORTED, "raydepth too large for the tile size / spp (node store > 48 GB)");
@@ -3311,7 +3325,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   const int tiles_per_batch = (int)std::max<long long>(1, target_spec / tile_samples);
   const long long maxc = (long long)tiles_per_batch * tile_samples;
   const int nbatch = (int)((owned.size() + tiles_per_batch - 1) / tiles_per_batch);
-  const int npipes = d->spec ? 1 : std::min(kPipes, std::max(1, nbatch));
+  const int npipes = d->spec ? 1 : std::min(pipes_cfg, std::max(1, nbatch));
   const bool path = p->integrator == YK_INTEGRATOR_PATH;
   // final gathering: hits 0..fg_bounces of each gather path, queue words up to fg_bounces + 1
   const int bounces = path ? R.bounces : (R.pm_fg ? p->photon.fg_bounces + 1 : 0);
@@ -3711,6 +3725,132 @@ int yk_render_film(yk_device* d, const yk_render_params* p, int32_t shard, int32
   const int rc = yk_render_shard(d, p, shard, nshards, film.p, st);
   if (rc != YK_OK) return rc;
   HIPCHK(hipMemcpy(film_host, film.p, npx * 5 * sizeof(float), hipMemcpyDeviceToHost));
+  return YK_OK;
+  YK_GUARD_END
+}
+
+// Whole frame on ndev devices (tiledIntegrator_t::render's threads,
+// integrator.cc:177-211, one host thread per device): device i renders the
+// tiles t % ndev == i into its own film; the films are reduced into device
+// 0's by peer copies over xGMI (hipMemcpyPeerAsync) and one add per shard,
+// in shard order. Adaptive passes (AA_passes > 1): after every pass the
+// reduced film gives imageFilm_t::nextPass's flags (k_aa_flags, imagefilm.cc:
+// 213-289), which every device then resamples in its own tiles.
+int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params* p, float* film_host,
+                    yk_stats* st) {
+  if (!devs || ndev < 1 || !p || !film_host) return set_error(YK_ERR_ARG, "yk_render_multi: bad arguments");
+  for (int i = 0; i < ndev; ++i) {
+    if (!devs[i]) return set_error(YK_ERR_ARG, "yk_render_multi: NULL device");
+    if (!devs[i]->uploaded) return set_error(YK_ERR_STATE, "yk_render_multi: a device has no scene uploaded");
+    for (int j = 0; j < i; ++j)
+      if (devs[j] == devs[i]) return set_error(YK_ERR_ARG, "yk_render_multi: a device handle is listed twice");
+  }
+  if (p->aa_passes < 1) return set_error(YK_ERR_ARG, "AA_passes must be >= 1");
+  if (p->width <= 0 || p->height <= 0) return set_error(YK_ERR_ARG, "empty render area");
+  YK_GUARD_BEGIN
+  const size_t npx = (size_t)p->width * p->height, nfl = npx * 5;
+  yk_device* d0 = devs[0];
+  std::vector<DBuf<float>> film(ndev);
+  for (int i = 0; i < ndev; ++i) {
+    HIPCHK(hipSetDevice(devs[i]->ordinal));
+    film[i].ensure(nfl);
+    HIPCHK(hipMemsetAsync(film[i].p, 0, nfl * sizeof(float), devs[i]->stream));
+    HIPCHK(hipStreamSynchronize(devs[i]->stream));
+    if (devs[i]->ordinal != d0->ordinal) {  // direct xGMI access where the pair allows it
+      int can = 0;
+      HIPCHK(hipDeviceCanAccessPeer(&can, d0->ordinal, devs[i]->ordinal));
+      if (can) {
+        HIPCHK(hipSetDevice(d0->ordinal));
+        const hipError_t e = hipDeviceEnablePeerAccess(devs[i]->ordinal, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHK(e);
+        (void)hipGetLastError();
+      }
+    }
+  }
+  HIPCHK(hipSetDevice(d0->ordinal));
+  DBuf<float> acc, stage;
+  acc.ensure(nfl);
+  if (ndev > 1) stage.ensure(nfl);
+  std::vector<yk_stats> sts(ndev);
+  // one pass on every device, each in its own host thread
+  auto run = [&](const PassSpec& ps) -> int {
+    std::vector<int> rc(ndev, YK_OK);
+    std::vector<std::string> msg(ndev);
+    std::vector<std::thread> th;
+    for (int i = 0; i < ndev; ++i)
+      th.emplace_back([&, i] {
+        rc[i] = render_pass(devs[i], p, i, ndev, film[i].p, &sts[i], ps);
+        if (rc[i] != YK_OK) msg[i] = yk_last_error();
+      });
+    for (auto& t : th) t.join();
+    for (int i = 0; i < ndev; ++i)
+      if (rc[i] != YK_OK) return set_error(rc[i], "device " + std::to_string(i) + ": " + msg[i]);
+    return YK_OK;
+  };
+  // acc = film[0] + film[1] + ... (shard order) on device 0
+  auto reduce = [&]() {
+    HIPCHK(hipSetDevice(d0->ordinal));
+    hipStream_t s0 = d0->stream;
+    HIPCHK(hipMemcpyAsync(acc.p, film[0].p, nfl * sizeof(float), hipMemcpyDeviceToDevice, s0));
+    for (int i = 1; i < ndev; ++i) {
+      if (devs[i]->ordinal == d0->ordinal)
+        HIPCHK(hipMemcpyAsync(stage.p, film[i].p, nfl * sizeof(float), hipMemcpyDeviceToDevice, s0));
+      else
+        HIPCHK(hipMemcpyPeerAsync(stage.p, d0->ordinal, film[i].p, devs[i]->ordinal, nfl * sizeof(float), s0));
+      hipLaunchKernelGGL(k_film_add, dim3(grid_for((long long)nfl)), dim3(256), 0, s0, acc.p, stage.p,
+                         (long long)nfl);
+      HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipStreamSynchronize(s0));
+  };
+  const int n0 = std::max(1, p->aa_samples);  // scene_t::setAntialiasing, scene.cc:736-742
+  const bool multipass = p->aa_passes > 1;
+  int rc = run(PassSpec{n0, 0, multipass, nullptr});
+  if (rc != YK_OK) return rc;
+  reduce();
+  if (multipass) {
+    const int inc = p->aa_inc_samples > 0 ? p->aa_inc_samples : n0;
+    const int w = p->width, h = p->height;
+    std::vector<uint8_t> flags(npx);
+    DBuf<uint8_t> flags_dev;
+    flags_dev.ensure(npx);
+    for (int pass = 1; pass < p->aa_passes; ++pass) {
+      const uint8_t* fl = nullptr;  // AA_threshold <= 0: doMoreSamples is always true
+      if (p->aa_threshold > 0.f) {
+        HIPCHK(hipSetDevice(d0->ordinal));
+        HIPCHK(hipMemsetAsync(flags_dev.p, 0, npx, d0->stream));
+        if (w > 1 && h > 1) {
+          hipLaunchKernelGGL(k_aa_flags, dim3(grid_for((long long)(w - 1) * (h - 1))), dim3(256), 0, d0->stream,
+                             acc.p, w, h, p->aa_threshold, flags_dev.p);
+          HIPCHK(hipGetLastError());
+        }
+        HIPCHK(hipMemcpyAsync(flags.data(), flags_dev.p, npx, hipMemcpyDeviceToHost, d0->stream));
+        HIPCHK(hipStreamSynchronize(d0->stream));
+        fl = flags.data();
+      }
+      rc = run(PassSpec{inc, n0 + (pass - 1) * inc, true, fl});
+      if (rc != YK_OK) return rc;
+      reduce();
+    }
+  }
+  HIPCHK(hipSetDevice(d0->ordinal));
+  HIPCHK(hipMemcpy(film_host, acc.p, nfl * sizeof(float), hipMemcpyDeviceToHost));
+  if (st) {
+    for (const yk_stats& x : sts) {
+      st->closest_rays += x.closest_rays;
+      st->shadow_rays += x.shadow_rays;
+      st->closest_nodes += x.closest_nodes;
+      st->closest_tris += x.closest_tris;
+      st->shadow_nodes += x.shadow_nodes;
+      st->shadow_tris += x.shadow_tris;
+      st->camera_samples += x.camera_samples;
+      st->ms_total = std::max(st->ms_total, x.ms_total);
+      st->ms_closest += x.ms_closest;
+      st->ms_shadow += x.ms_shadow;
+      st->closest_launches += x.closest_launches;
+      st->shadow_launches += x.shadow_launches;
+    }
+  }
   return YK_OK;
   YK_GUARD_END
 }

@@ -94,6 +94,18 @@ class Device:
         A.check(A.lib().yk_render_shard(self._p, C.byref(params), shard, nshards, _ptr(film), C.byref(st)))
         return st
 
+    @staticmethod
+    def render_multi(devices, params, stats=None):
+        """Whole frame on several devices (yk_render_multi: tiles t % n on
+        devices[i], film reduced on devices[0]) -> (h, w, 5) float32 film sums."""
+        for d in devices:
+            torch.cuda.synchronize(d.torch_device)
+        arr = (C.c_void_p * len(devices))(*[d._p.value for d in devices])
+        out = np.zeros((params.height, params.width, 5), np.float32)
+        st = stats if stats is not None else A.yk_stats()
+        A.check(A.lib().yk_render_multi(arr, len(devices), C.byref(params), out.ctypes.data_as(A.fp), C.byref(st)))
+        return out, st
+
     def film_resolve(self, params, film):
         rgba = torch.empty((params.height, params.width, 4), dtype=torch.float32, device=self.torch_device)
         torch.cuda.synchronize(self.torch_device)

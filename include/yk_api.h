@@ -325,6 +325,17 @@ int yk_film_resolve(yk_device* d, const yk_render_params* p, const float* d_film
  * `shard` and return the film sums (width*height*5 floats) in host memory */
 int yk_render_film(yk_device* d, const yk_render_params* p, int32_t shard, int32_t nshards, float* film_host,
                    yk_stats* st);
+/* Whole frame on ndev devices, replacing tiledIntegrator_t::render's worker
+ * threads (integrator.cc:177-211): devs[i] renders the tiles t % ndev == i on
+ * its own host thread, and the film sums are reduced on devs[0] by peer
+ * copies over xGMI, in shard order, into film_host (width*height*5 floats).
+ * With AA_passes > 1 the reduced film gives every pass's imageFilm_t::nextPass
+ * flags (imagefilm.cc:213-289), so adaptive passes work across devices (per
+ * pixel the result equals the 1-device film up to float summation order).
+ * Every device must hold the same uploaded scene; a device handle may appear
+ * only once, but two handles may be opened on one GPU. */
+int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params* p, float* film_host,
+                    yk_stats* st);
 /* convenience: whole frame on one device, RGBA float image to host memory */
 int yk_render(yk_device* d, const yk_render_params* p, float* rgba_host, yk_stats* st);
 

@@ -282,7 +282,9 @@ typedef struct {
 static oscene G;
 
 /* counters (reference: scene_t::intersect / isShadowed calls) */
-static uint64_t g_nclosest, g_nshadow, g_nodes_c, g_tris_c, g_nodes_s, g_tris_s;
+/* ray and work counters: per thread, so that bench.py's CPU baseline can run
+ * render shards on all host cores in parallel (one scene, read-only) */
+static __thread uint64_t g_nclosest, g_nshadow, g_nodes_c, g_tris_c, g_nodes_s, g_tris_s;
 
 static v3 tri_vert(int p, int k) {
   const float* t = G.tv + 9 * (size_t)p + 3 * k;
@@ -477,7 +479,7 @@ static int scene_shadowed(v3 from, v3 dir, float tmin, float tmax) {
 }
 
 /* transparent shadows: mcIntegrator_t::trShad / sDepth (set per render) */
-static int g_trshad, g_sdepth;
+static __thread int g_trshad, g_sdepth;
 
 static col3 sd_get_transparency(int mat, const surfpt* sp, v3 wo);
 static int mat_is_transparent(int mat);

@@ -1,0 +1,107 @@
+"""Multi-GPU product paths (BASELINE configs[3]: the 1M-tri frame tiled over
+several GPUs) exercised on one GPU.
+
+* yk_render_multi (the C-ABI entry a plugin calls with one handle per GPU):
+  N device handles opened on GPU 0, tiles t % N on handle i, the films
+  reduced by peer copies on handle 0. Adaptive AA passes run across the
+  devices with nextPass flags taken from the reduced film.
+* the multi-process path bench.py runs (one process per GPU) is in
+  tests/test_0_multi_process.py.
+
+Per pixel the result equals the 1-device film up to the float summation
+order of the reduce; pixels whose filter footprint stays inside one tile
+receive samples from one shard only and are bit-identical. Ray and work
+counters split exactly.
+"""
+import numpy as np
+import pytest
+
+from core_amd import _abi as A
+from core_amd.device import Device
+from core_amd.scene import probe_scene
+
+pytestmark = pytest.mark.gpu
+
+_S = {}
+
+
+def _bumpy(w, h, spp):
+    key = (w, h, spp)
+    if key not in _S:
+        s, p = probe_scene("bumpy", w, h, 1000, 501)
+        p.aa_samples = spp
+        _S[key] = (s, p)
+    return _S[key]
+
+
+def _interior(h, w, tile, margin=3):
+    ys, xs = np.arange(h) % tile, np.arange(w) % tile
+    return ((ys >= margin) & (ys < tile - margin))[:, None] & ((xs >= margin) & (xs < tile - margin))[None, :]
+
+
+def _compare_films(f1, fn, tile):
+    assert np.allclose(fn, f1, rtol=2e-6, atol=1e-6), np.abs(fn - f1).max()
+    inner = _interior(f1.shape[0], f1.shape[1], tile)
+    assert (fn[inner].view(np.uint32) == f1[inner].view(np.uint32)).all()
+
+
+def _one_device_film(gpu_device, s, p):
+    gpu_device.upload(s)
+    film = gpu_device.new_film(p)
+    st = gpu_device.render_shard(p, film)
+    return film.cpu().numpy(), st
+
+
+@pytest.mark.parametrize("ndev", [2, 3])
+def test_render_multi_equals_one_device(gpu_device, ndev):
+    s, p = _bumpy(480, 270, 8)
+    f1, st1 = _one_device_film(gpu_device, s, p)
+    devs = [gpu_device] + [Device(0) for _ in range(ndev - 1)]
+    try:
+        for d in devs:
+            d.upload(s)
+        fn, stn = Device.render_multi(devs, p)
+    finally:
+        for d in devs[1:]:
+            d.close()
+    for f in ("closest_rays", "shadow_rays", "closest_nodes", "closest_tris", "shadow_nodes", "shadow_tris",
+              "camera_samples"):
+        assert getattr(stn, f) == getattr(st1, f), f
+    _compare_films(f1, fn, p.tile_size or 32)
+
+
+def test_render_multi_adaptive_passes(gpu_device):
+    """AA_passes > 1 across devices: every pass's nextPass flags come from the
+    reduced film. Summation order at tile borders can move a border pixel's
+    brightness across the threshold, so a handful of pixels may differ."""
+    s, p = probe_scene("cornell_pt", 96, 80)
+    p.aa_samples = 2
+    p.aa_passes = 3
+    p.aa_inc_samples = 2
+    p.aa_threshold = 0.05
+    f1, st1 = _one_device_film(gpu_device, s, p)
+    d2 = Device(0)
+    try:
+        d2.upload(s)
+        fn, stn = Device.render_multi([gpu_device, d2], p)
+    finally:
+        d2.close()
+    assert f1[..., 4].max() > p.aa_samples * f1[..., 4].min()  # passes 1, 2 resampled a subset
+    close = np.isclose(fn, f1, rtol=1e-5, atol=1e-6).all(axis=2)
+    assert (~close).mean() <= 0.002, (~close).sum()
+    assert abs(int(stn.camera_samples) - int(st1.camera_samples)) <= 0.002 * st1.camera_samples
+
+
+def test_render_multi_refuses_bad_handles(gpu_device):
+    s, p = probe_scene("cornell_pt", 16, 16)
+    gpu_device.upload(s)
+    with pytest.raises(A.YkError) as e:
+        Device.render_multi([gpu_device, gpu_device], p)
+    assert e.value.code == A.YK_ERR_ARG
+    d2 = Device(0)
+    try:
+        with pytest.raises(A.YkError) as e:
+            Device.render_multi([gpu_device, d2], p)  # d2 holds no scene
+        assert e.value.code == A.YK_ERR_STATE
+    finally:
+        d2.close()
