@@ -76,6 +76,9 @@ def _rays(s, dev_nodes, seed):
     return np.concatenate([r for _, r in fams]), ranges
 
 
+# per ray family: (differing rays, non-tie differences) as fractions of the family
+FAMILY_CAPS = {"random": (0.05, 0.01), "bounded": (0.05, 0.01), "ref-edge": (0.10, 0.05),
+               "dev-split": (0.10, 0.05), "graze": (0.30, 0.05)}
 # brute-force checks per ray family: every disagreeing ray, or an even sample
 # of this many when a family has more
 BRUTE_PER_FAMILY = 400
@@ -107,10 +110,16 @@ def _compare(gpu_device, s, name, rays, ranges, ref_hits, ref_occ, hits, occ, in
             assert gp[i] == bp or (nt > 1 and gt[i] == bt), (fam, i, rays[i].tolist(), gp[i], gt[i], bp, bt)
             f_ties += nt > 1
             f_lost += nt == 1
-        # ties may be common on axis-aligned scenes; answers the reference tree
-        # loses (clipped leaves) stay rare in every family
-        assert len(bad) <= (b - a) // 20, (fam, len(bad))
-        assert f_lost <= max(8, (b - a) // 100), (fam, f_lost)
+        # Exact-t ties are common where rays graze shared edges (the graze
+        # family aims at them) and on axis-aligned scenes; answers the
+        # reference tree loses (its clipped leaves) are rare on random rays and
+        # concentrate on rays that start on its own split planes (37 of 1284 on
+        # the Cornell box). The device answer itself is brute-force checked above.
+        cap_bad, cap_lost = FAMILY_CAPS[fam]
+        print(f"  {fam}: {len(bad)} of {b - a} differ, checked {min(len(bad), BRUTE_PER_FAMILY)}: "
+              f"{f_ties} ties, {f_lost} lost by the reference tree")
+        assert len(bad) <= max(8, int(cap_bad * (b - a))), (fam, len(bad))
+        assert f_lost <= max(8, int(cap_lost * (b - a))), (fam, f_lost)
         ties += f_ties
         lost += f_lost
     bad = np.flatnonzero(diff)

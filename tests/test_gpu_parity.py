@@ -264,7 +264,8 @@ def test_object_state_scene_renders_identically(gpu_device):
 
 
 def test_refused_upload_keeps_the_resident_scene(gpu_device):
-    """An upload refused by validation (here an area light with 0 samples)
+    """An upload refused by validation (here 8200 light samples per shading
+    point, more than the 8192 shadow slots a sample may own)
     leaves the previously uploaded scene resident and bit-exact; the checks run
     before any resident buffer is touched."""
     from core_amd.scene import Scene
@@ -272,11 +273,11 @@ def test_refused_upload_keeps_the_resident_scene(gpu_device):
     gpu_device.upload(s)
     bad = Scene()
     bad.generate("cornell_pt", 16, 16)
-    bad.add_area_light((-0.1, 1.9, -0.1), (0.1, 1.9, -0.1), (-0.1, 1.9, 0.1), samples=0)
+    bad.add_area_light((-0.1, 1.9, -0.1), (0.1, 1.9, -0.1), (-0.1, 1.9, 0.1), samples=4100)
     bad.build()
     with pytest.raises(A.YkError) as e:
         gpu_device.upload(bad)
-    assert e.value.code == A.YK_ERR_ARG
+    assert e.value.code == A.YK_ERR_UNSUPPORTED
     rays = _ray_batch(s, 3)
     prim, t, *_ = orc.intersect(rays)
     gp, gt, *_ = gpu_device.split_hits(gpu_device.trace_closest(gpu_device.rays_to_device(rays)))

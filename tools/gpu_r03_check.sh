@@ -1,7 +1,8 @@
 set -e
-# Round-3 start: GPU parity suite + headline bench on HEAD.
+# Round 3: GPU parity suite (resumable with a -k expression in $1) + headline bench.
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gputest.log 2>&1
+sel=${1:-}
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread ${sel:+-k "$sel"} > gpurun_out/gputest.log 2>&1
 timeout -k 10 300 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
