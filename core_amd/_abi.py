@@ -20,6 +20,9 @@ YK_INTEGRATOR_DIRECT, YK_INTEGRATOR_PATH, YK_INTEGRATOR_PHOTON = 0, 1, 2
 YK_PHOTON_MAP_DIFFUSE, YK_PHOTON_MAP_CAUSTIC, YK_PHOTON_MAP_RADIANCE = 0, 1, 2
 YK_FILTER_BOX, YK_FILTER_MITCHELL, YK_FILTER_GAUSS, YK_FILTER_LANCZOS = 0, 1, 2, 3
 YK_CAUSTIC_NONE, YK_CAUSTIC_PATH, YK_CAUSTIC_PHOTON, YK_CAUSTIC_BOTH = 0, 1, 2, 3
+YK_BOKEH_DISK1, YK_BOKEH_DISK2, YK_BOKEH_TRI, YK_BOKEH_SQR, YK_BOKEH_PENTA, YK_BOKEH_HEXA, YK_BOKEH_RING = \
+    0, 1, 3, 4, 5, 6, 7
+YK_BOKEH_BIAS_NONE, YK_BOKEH_BIAS_CENTER, YK_BOKEH_BIAS_EDGE = 0, 1, 2
 
 f3 = C.c_float * 3
 
@@ -41,7 +44,8 @@ class yk_light(C.Structure):
 class yk_camera(C.Structure):
     _fields_ = [("from_", f3), ("to", f3), ("up", f3), ("resx", C.c_int32), ("resy", C.c_int32),
                 ("focal", C.c_float), ("aspect_ratio", C.c_float), ("near_clip", C.c_float),
-                ("far_clip", C.c_float)]
+                ("far_clip", C.c_float), ("aperture", C.c_float), ("dof_distance", C.c_float),
+                ("bokeh_type", C.c_int32), ("bokeh_bias", C.c_int32), ("bokeh_rotation", C.c_float)]
 
 
 class yk_material_state(C.Structure):
@@ -63,7 +67,9 @@ class yk_dirac_light_state(C.Structure):
 
 class yk_camera_state(C.Structure):
     _fields_ = [("position", f3), ("vright", f3), ("vup", f3), ("vto", f3), ("cam_z", f3),
-                ("near_p", f3), ("far_p", f3), ("resx", C.c_int32), ("resy", C.c_int32)]
+                ("near_p", f3), ("far_p", f3), ("resx", C.c_int32), ("resy", C.c_int32),
+                ("aperture", C.c_float), ("dof_distance", C.c_float), ("dof_rt", f3), ("dof_up", f3),
+                ("bokeh_type", C.c_int32), ("bokeh_bias", C.c_int32), ("lens_ls", C.c_float * 16)]
 
 
 class yk_photon_params(C.Structure):

@@ -136,6 +136,24 @@ yk_camera_state camera_state(const yk_camera& c) {  // camera_t ctor + setAxis
   put(o.cam_z, camZ);
   put(o.near_p, hadd(pos, hmul(c.near_clip, camZ)));
   put(o.far_p, hadd(pos, hmul(c.far_clip, camZ)));
+  // depth of field: setAxis's dof_rt / dof_up, the ctor's polygon table
+  // (perspectiveCamera.cc:29-50, 57-62)
+  o.aperture = c.aperture;
+  o.dof_distance = c.dof_distance;
+  put(o.dof_rt, hmul(c.aperture, camX));
+  put(o.dof_up, hmul(c.aperture, camY));
+  o.bokeh_type = c.bokeh_type;
+  o.bokeh_bias = c.bokeh_bias;
+  if (c.bokeh_type >= YK_BOKEH_TRI && c.bokeh_type <= YK_BOKEH_HEXA) {
+    const int ns = c.bokeh_type;
+    float w = (float)((double)c.bokeh_rotation * 0.01745329251994329576922);  // degToRad
+    const float wi = (float)(6.28318530717958647692 / (double)(float)ns);    // M_2PI / ns
+    for (int i = 0; i < (ns + 2) * 2; i += 2) {
+      o.lens_ls[i] = host_fcos(w);
+      o.lens_ls[i + 1] = host_fsin(w);
+      w += wi;
+    }
+  }
   const hv3 vright = camX, vup = hmul(aspect, camY);
   put(o.vto, hsub(hmul(c.focal, camZ), hmul(0.5f, hadd(vup, vright))));
   const float ry = 1.0f / (float)c.resy, rx = 1.0f / (float)c.resx;  // compiled form of "/= res"
@@ -224,6 +242,19 @@ void rec_normal(const float* t, float* n) {
 
 // matrix4x4_t * point3d_t, compiled form of the instance's getVertex
 // (meshtypes.h:140-143): each row as (m0*x + m1*y) + (m2*z + m3)
+float host_fsin(float x) {
+  const double pi = 3.14159265358979323846, two_pi = 6.28318530717958647692;
+  if ((double)x > two_pi || (double)x < -two_pi)
+    x -= (float)((int)(x * (float)0.15915494309189533577)) * (float)two_pi;
+  if ((double)x < -pi) x += (float)two_pi;
+  else if ((double)x > pi) x -= (float)two_pi;
+  x = ((float)1.27323954473516268615 * x) - (((float)0.40528473456935108578 * x) * std::fabs(x));
+  float r = x + (std::fabs(x) - 1.0f) * (0.225f * x);
+  if (r > 1.0f) r = 1.0f;
+  if (r < -1.0f) r = -1.0f;
+  return r;
+}
+
 static void xform_point(const float* m, const float* p, float* o) {
   for (int r = 0; r < 3; ++r) {
     const float* a = m + 4 * r;

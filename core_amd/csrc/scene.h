@@ -12,6 +12,12 @@
 
 namespace yk {
 
+// FAST_TRIG fSin / fCos (mathOptimizations.h:249-280) in the compiled form of
+// yk_math.h's fsin_ref, host IEEE arithmetic (camera polygon table, film
+// filter tables)
+float host_fsin(float x);
+inline float host_fcos(float x) { return host_fsin(x + (float)1.57079632679489661923); }
+
 struct Mesh {
   std::vector<float> points;  // xyz per vertex (point3d_t, float)
   std::vector<int> faces;     // a,b,c per triangle

@@ -76,6 +76,10 @@ struct DLight {  // areaLight_t members after its constructor (arealight.cc:30-4
 
 struct DCam {  // perspectiveCam_t after camera_t ctor + setAxis
   float pos[3], vright[3], vup[3], vto[3], camZ[3], near_p[3], far_p[3];
+  // depth of field (aperture != 0): dof_rt, dof_up, dof_distance, bokeh, LS
+  float aperture, dof_distance, dof_rt[3], dof_up[3];
+  int bokeh_type, bokeh_bias;
+  float ls[16];
 };
 
 constexpr int kMaxMats = 64;
@@ -1451,6 +1455,35 @@ struct TileList {
   const int* pix;     // adaptive pass: the batch's resampled pixels ((y << 16) | x), tile order
 };
 
+// perspectiveCam_t::biasDist (perspectiveCamera.cc:73-86)
+__device__ __forceinline__ float lens_bias(float r) {
+  if (c_cam.bokeh_bias == YK_BOKEH_BIAS_CENTER) return sqrtf(sqrtf(r) * r);
+  if (c_cam.bokeh_bias == YK_BOKEH_BIAS_EDGE) return sqrtf(1.0f - r * r);
+  return sqrtf(r);
+}
+// perspectiveCam_t::getLensUV (perspectiveCamera.cc:100-121) with sampleTSD
+// (:88-98) for the polygon shapes and ShirleyDisk (vector3d.cc:156-182)
+__device__ __forceinline__ void lens_uv(float r1, float r2, float& u, float& v) {
+  const int bt = c_cam.bokeh_type;
+  if (bt >= YK_BOKEH_TRI && bt <= YK_BOKEH_HEXA) {
+    const float fn = (float)bt;
+    int idx = (int)(r1 * fn);
+    r1 = (r1 - (float)idx / fn) * fn;
+    r1 = lens_bias(r1);
+    const float b1 = r1 * r2, b0 = r1 - b1;
+    idx <<= 1;
+    u = c_cam.ls[idx] * b0 + c_cam.ls[idx + 2] * b1;
+    v = c_cam.ls[idx + 1] * b0 + c_cam.ls[idx + 3] * b1;
+  } else if (bt == YK_BOKEH_DISK2 || bt == YK_BOKEH_RING) {
+    const float w = (float)(YK_2PI_D * (double)r2);
+    r1 = (bt == YK_BOKEH_RING) ? sqrtf(0.707106781f + 0.292893218f) : lens_bias(r1);
+    u = r1 * fcos_ref(w);
+    v = r1 * fsin_ref(w);
+  } else {
+    shirley_disk(r1, r2, u, v);
+  }
+}
+
 __global__ void __launch_bounds__(256) k_camera(TileList TL, Batch B, RenderConst R, long long nc) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= nc) return;
@@ -1502,6 +1535,32 @@ __global__ void __launch_bounds__(256) k_camera(TileList TL, Batch B, RenderCons
   const float den = vdot(d, cz);
   r.tmin = vdot(cz, vsub(ld3(c_cam.near_p), from)) / den;
   r.tmax = vdot(cz, vsub(ld3(c_cam.far_p), from)) / den;
+  if (c_cam.aperture != 0.f) {
+    // renderTile's lens samples (integrator.cc:248-291): Halton(3) / Halton(5)
+    // set to pass_offs + samplingOffs per pixel, one getNext per sample in
+    // sample order -- so sample s takes the (s+1)-th value
+    Halton hu, hv;
+    hal_start(hu, 3u, (unsigned)R.pass_off + so);
+    hal_start(hv, 5u, (unsigned)R.pass_off + so);
+    float lu = 0.f, lv = 0.f;
+    for (int k = 0; k <= s; ++k) {
+      lu = hal_next(hu);
+      lv = hal_next(hv);
+    }
+    // shootRay's aperture branch (perspectiveCamera.cc:139-147): tmin / tmax
+    // stay those of the pinhole ray
+    float u, v;
+    lens_uv(lu, lv, u, v);
+    const v3 LI = vadd(vmul(u, ld3(c_cam.dof_rt)), vmul(v, ld3(c_cam.dof_up)));
+    const v3 f2 = vadd(from, LI);
+    const v3 d2 = vnormalize(vsub(vmul(c_cam.dof_distance, d), LI));
+    r.from[0] = f2.x;
+    r.from[1] = f2.y;
+    r.from[2] = f2.z;
+    r.dir[0] = d2.x;
+    r.dir[1] = d2.y;
+    r.dir[2] = d2.z;
+  }
   B.p_rays[c] = r;
 }
 
@@ -2612,6 +2671,13 @@ DCam make_cam(const yk_camera_state& c) {
   std::memcpy(C.camZ, c.cam_z, sizeof C.camZ);
   std::memcpy(C.near_p, c.near_p, sizeof C.near_p);
   std::memcpy(C.far_p, c.far_p, sizeof C.far_p);
+  C.aperture = c.aperture;
+  C.dof_distance = c.dof_distance;
+  std::memcpy(C.dof_rt, c.dof_rt, sizeof C.dof_rt);
+  std::memcpy(C.dof_up, c.dof_up, sizeof C.dof_up);
+  C.bokeh_type = c.bokeh_type;
+  C.bokeh_bias = c.bokeh_bias;
+  std::memcpy(C.ls, c.lens_ls, sizeof C.ls);
   return C;
 }
 
@@ -3135,18 +3201,7 @@ int yk_trace_shadow_filtered(yk_device* d, const yk_ray* d_rays, int64_t n, uint
 // Filter functions of imageFilm_t (imagefilm.cc:81-123), in the survey
 // build's compiled forms: Gauss folds -6*log2(e) into one constant and drops
 // fExp2's upper clamp (the argument is never positive); Lanczos2 uses the
-// FAST_TRIG fSin on (float)(x*pi) and (float)(x*pi/2).
-static float host_fsin(float x) {  // fSin, mathOptimizations.h:249-268 (compiled form, see yk_math.h)
-  if ((double)x > YK_2PI_D || (double)x < -YK_2PI_D)
-    x -= (float)((int)(x * (float)0.15915494309189533577)) * (float)YK_2PI_D;
-  if ((double)x < -YK_PI_D) x += (float)YK_2PI_D;
-  else if ((double)x > YK_PI_D) x -= (float)YK_2PI_D;
-  x = ((float)1.27323954473516268615 * x) - (((float)0.40528473456935108578 * x) * std::fabs(x));
-  float r = x + (std::fabs(x) - 1.0f) * (0.225f * x);
-  if (r > 1.0f) r = 1.0f;
-  if (r < -1.0f) r = -1.0f;
-  return r;
-}
+// FAST_TRIG fSin (yk::host_fsin) on (float)(x*pi) and (float)(x*pi/2).
 static float filter_gauss(float dx, float dy) {
   const float r2 = dx * dx + dy * dy;
   float k;

@@ -175,6 +175,31 @@ __device__ __forceinline__ float fsin_ref(float x) {
 }
 __device__ __forceinline__ float fcos_ref(float x) { return fsin_ref(x + (float)1.57079632679489661923); }
 
+// ShirleyDisk, vector3d.cc:156-182
+__device__ __forceinline__ void shirley_disk(float r1, float r2, float& u, float& v) {
+  float phi = 0.f, r = 0.f;
+  const float a = 2 * r1 - 1, b = 2 * r2 - 1;
+  if (a > -b) {
+    if (a > b) {
+      r = a;
+      phi = (float)(YK_PI_D / 4 * (double)(b / a));
+    } else {
+      r = b;
+      phi = (float)(YK_PI_D / 4 * (double)(2 - a / b));
+    }
+  } else {
+    if (a < b) {
+      r = -a;
+      phi = (float)(YK_PI_D / 4 * (double)(4 + b / a));
+    } else {
+      r = -b;
+      phi = (b != 0.f) ? (float)(YK_PI_D / 4 * (double)(6 - a / b)) : 0.f;
+    }
+  }
+  u = r * fcos_ref(phi);
+  v = r * fsin_ref(phi);
+}
+
 // vector3d_t::normalize, vector3d.h:249-260
 __device__ __forceinline__ v3 vnormalize(v3 a) {
   float len = a.x * a.x + a.y * a.y + a.z * a.z;

@@ -112,9 +112,11 @@ class Scene:
         return tuple(rgb) if has.value else None
 
     def set_camera(self, from_, to, up, resx, resy, focal=1.0, aspect_ratio=1.0, near_clip=0.0,
-                   far_clip=-1.0):
+                   far_clip=-1.0, aperture=0.0, dof_distance=0.0, bokeh_type=0, bokeh_bias=0, bokeh_rotation=0.0):
+        """perspectiveCam_t::factory parameters (perspectiveCamera.cc:191-232);
+        bokeh_type / bokeh_bias: YK_BOKEH_* / YK_BOKEH_BIAS_*"""
         c = A.yk_camera(A.f3(*from_), A.f3(*to), A.f3(*up), resx, resy, focal, aspect_ratio, near_clip,
-                        far_clip)
+                        far_clip, aperture, dof_distance, bokeh_type, bokeh_bias, bokeh_rotation)
         A.check(A.lib().yk_scene_set_camera(self._p, C.byref(c)))
 
     def generate(self, name, resx, resy, p0=0, p1=0):

@@ -76,10 +76,19 @@ typedef struct yk_light {
   int32_t infinite;
 } yk_light;
 
+/* perspectiveCam_t bokeh shapes and bias (perspectiveCamera.h:33-34) */
+enum { YK_BOKEH_DISK1 = 0, YK_BOKEH_DISK2 = 1, YK_BOKEH_TRI = 3, YK_BOKEH_SQR = 4, YK_BOKEH_PENTA = 5,
+       YK_BOKEH_HEXA = 6, YK_BOKEH_RING = 7 };
+enum { YK_BOKEH_BIAS_NONE = 0, YK_BOKEH_BIAS_CENTER = 1, YK_BOKEH_BIAS_EDGE = 2 };
 typedef struct yk_camera { /* perspectiveCam_t::factory, perspectiveCamera.cc:191-232 */
   float from[3], to[3], up[3];
   int32_t resx, resy;
   float focal, aspect_ratio, near_clip, far_clip;
+  /* depth of field: "aperture" [0 = pinhole], "dof_distance", "bokeh_type",
+   * "bokeh_bias", "bokeh_rotation" (degrees) */
+  float aperture, dof_distance;
+  int32_t bokeh_type, bokeh_bias;
+  float bokeh_rotation;
 } yk_camera;
 
 enum { YK_INTEGRATOR_DIRECT = 0, YK_INTEGRATOR_PATH = 1, YK_INTEGRATOR_PHOTON = 2 };
@@ -270,6 +279,13 @@ typedef struct yk_camera_state { /* perspectiveCam_t after setAxis (perspectiveC
   float position[3], vright[3], vup[3], vto[3], cam_z[3];
   float near_p[3], far_p[3]; /* near_plane.p / far_plane.p (camera.h:54-57)            */
   int32_t resx, resy;
+  /* depth of field (perspectiveCam_t ctor + setAxis): aperture (0 = pinhole),
+   * dof_distance, dof_rt = aperture * camX, dof_up = aperture * camY, bokeh
+   * type / bias and the polygon corner table LS (cos, sin pairs, up to 16) */
+  float aperture, dof_distance;
+  float dof_rt[3], dof_up[3];
+  int32_t bokeh_type, bokeh_bias;
+  float lens_ls[16];
 } yk_camera_state;
 
 int yk_scene_add_material_state(yk_scene* s, const yk_material_state* m, int32_t* id_out);

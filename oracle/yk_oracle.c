@@ -276,6 +276,8 @@ typedef struct {
   col3 bg;
   /* derived camera data, camera.h:41-60 + perspectiveCamera.cc:28-71 */
   v3 cam_pos, vright, vup, vto, camZ;
+  v3 dof_rt, dof_up; /* depth of field (perspectiveCam_t::setAxis) */
+  float lens_ls[16];  /* polygon bokeh corners (perspectiveCam_t ctor) */
   v3 near_p, far_p;
 } oscene;
 
@@ -604,9 +606,67 @@ static void camera_setup(void) {
   G.vup = V(vup.x * ry, vup.y * ry, vup.z * ry);
   G.vright = V(vright.x * rx, vright.y * rx, vright.z * rx);
   G.vto = vto;
+  /* depth of field: dof_rt = aperture * camX, dof_up = aperture * camY
+   * (setAxis, perspectiveCamera.cc:62-63); polygon corners LS from the
+   * bokeh rotation (ctor, perspectiveCamera.cc:38-49) */
+  G.dof_rt = vmul(c->aperture, camX);
+  G.dof_up = vmul(c->aperture, camY);
+  memset(G.lens_ls, 0, sizeof G.lens_ls);
+  if (c->bokeh_type >= YK_BOKEH_TRI && c->bokeh_type <= YK_BOKEH_HEXA) {
+    int ns = c->bokeh_type;
+    float w = (float)((double)c->bokeh_rotation * 0.01745329251994329576922);
+    float wi = (float)(6.28318530717958647692 / (double)(float)ns);
+    for (int i = 0; i < (ns + 2) * 2; i += 2) {
+      G.lens_ls[i] = fCos(w);
+      G.lens_ls[i + 1] = fSin(w);
+      w += wi;
+    }
+  }
 }
 
-/* perspectiveCam_t::shootRay, perspectiveCamera.cc:127-149 (no DOF) */
+/* perspectiveCam_t::biasDist, perspectiveCamera.cc:73-86 */
+static float lens_bias(float r) {
+  if (G.cam.bokeh_bias == YK_BOKEH_BIAS_CENTER) return sqrtf(sqrtf(r) * r);
+  if (G.cam.bokeh_bias == YK_BOKEH_BIAS_EDGE) return sqrtf(1.0f - r * r);
+  return sqrtf(r);
+}
+
+static void shirley_disk(float r1, float r2, float* u, float* v);
+
+/* perspectiveCam_t::getLensUV, perspectiveCamera.cc:100-121 (sampleTSD :88-98) */
+static void lens_uv(float r1, float r2, float* u, float* v) {
+  int bt = G.cam.bokeh_type;
+  if (bt >= YK_BOKEH_TRI && bt <= YK_BOKEH_HEXA) {
+    float fn = (float)bt;
+    int idx = (int)(r1 * fn);
+    r1 = (r1 - (float)idx / fn) * fn;
+    r1 = lens_bias(r1);
+    float b1 = r1 * r2, b0 = r1 - b1;
+    idx <<= 1;
+    *u = G.lens_ls[idx] * b0 + G.lens_ls[idx + 2] * b1;
+    *v = G.lens_ls[idx + 1] * b0 + G.lens_ls[idx + 3] * b1;
+  } else if (bt == YK_BOKEH_DISK2 || bt == YK_BOKEH_RING) {
+    float w = (float)(6.28318530717958647692 * (double)r2);
+    r1 = (bt == YK_BOKEH_RING) ? sqrtf(0.707106781f + 0.292893218f) : lens_bias(r1);
+    *u = r1 * fCos(w);
+    *v = r1 * fSin(w);
+  } else {
+    shirley_disk(r1, r2, u, v);
+  }
+}
+
+/* shootRay's aperture branch, perspectiveCamera.cc:139-147: the lens point
+ * (lu, lv) moves the origin and re-aims at the focal plane; tmin / tmax stay */
+static void camera_lens(float lu, float lv, v3* from, v3* dir) {
+  if (G.cam.aperture == 0.f) return;
+  float u, v;
+  lens_uv(lu, lv, &u, &v);
+  v3 LI = vadd(vmul(u, G.dof_rt), vmul(v, G.dof_up));
+  *from = vadd(*from, LI);
+  *dir = vnormalize(vsub(vmul(G.cam.dof_distance, *dir), LI));
+}
+
+/* perspectiveCam_t::shootRay, perspectiveCamera.cc:127-138 (DOF: camera_lens) */
 static void camera_ray(float px, float py, v3* from, v3* dir, float* tmin, float* tmax) {
   *from = G.cam_pos;
   v3 d = vadd(vadd(vmul(px, G.vright), vmul(py, G.vup)), G.vto);
@@ -2388,6 +2448,12 @@ static int render_tiles(const yk_render_params* P, int shard, int nshards, float
             if (adaptive && !flags[(size_t)(i - F.cy0) * F.w + (j - F.cx0)]) continue; /* doMoreSamples */
             rstate st;
             st.samplingOffs = fnv_32a_buf((unsigned)i * fnv_32a_buf((unsigned)j));
+            /* lens samples, integrator.cc:248-291 */
+            halton halU, halV;
+            hal_init(&halU, 3);
+            hal_init(&halV, 5);
+            hal_setstart(&halU, (unsigned)pass_offs + st.samplingOffs);
+            hal_setstart(&halV, (unsigned)pass_offs + st.samplingOffs);
             st.includeLights = 0;
             st.raylevel = 0;
             for (int s = 0; s < n; ++s) {
@@ -2403,6 +2469,10 @@ static int render_tiles(const yk_render_params* P, int shard, int nshards, float
               v3 from, dir;
               float tmin, tmax;
               camera_ray((float)j + dx, (float)i + dy, &from, &dir, &tmin, &tmax);
+              if (G.cam.aperture != 0.f) {
+                float lu = hal_next(&halU), lv = hal_next(&halV);
+                camera_lens(lu, lv, &from, &dir);
+              }
               rgba c = integrate(&st, P, from, dir, tmin, tmax);
               c.r = 1.f * c.r; c.g = 1.f * c.g; c.b = 1.f * c.b; c.a = 1.f * c.a; /* wt * col */
               film_add(&F, c, j, i, dx, dy);

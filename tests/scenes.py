@@ -185,3 +185,15 @@ def transparent_panes(resx, resy, integrator="cornell_pt", panes=3):
         s.add_mesh(pts, np.asarray(faces, np.int32), mats[k % 2])
     s.build()
     return s, p
+
+
+def dof_cornell(resx, resy, integrator="cornell_pt", bokeh_type=0, bokeh_bias=0, rotation=17.0, aperture=0.08):
+    """Cornell box seen through a thin lens (perspectiveCam_t with aperture,
+    perspectiveCamera.cc:127-149 + renderTile's Halton(3)/Halton(5) lens
+    samples, integrator.cc:248-291), focused on the far wall."""
+    s = Scene()
+    p = s.generate(integrator, resx, resy)
+    s.set_camera((0, 1, -3.6), (0, 1, 0), (0, 2, -3.6), resx, resy, focal=1.3, aperture=aperture,
+                 dof_distance=4.2, bokeh_type=bokeh_type, bokeh_bias=bokeh_bias, bokeh_rotation=rotation)
+    s.build()
+    return s, p

@@ -13,7 +13,7 @@ from core_amd import _abi as A
 from core_amd.scene import probe_scene
 from oracle.oracle import Oracle
 from tests.raygen import edge_rays, random_rays
-from tests.scenes import dirac_lights, smooth_instanced, specular
+from tests.scenes import dirac_lights, dof_cornell, smooth_instanced, specular
 
 pytestmark = pytest.mark.gpu
 
@@ -28,6 +28,8 @@ def scene(name, resx, resy, nu=0, nv=0):
             s, p, _ = smooth_instanced(resx, resy, gen)
         elif name.startswith("dirac"):  # point + directional lights, constant background (§8 f1)
             s, p = dirac_lights(resx, resy, gen)
+        elif name.startswith("dof"):  # thin-lens camera: nu = bokeh type, nv = bokeh bias
+            s, p = dof_cornell(resx, resy, gen, bokeh_type=nu, bokeh_bias=nv)
         elif name.startswith("spec"):  # mirror / glass / translucent shinydiffuse + recursiveRaytrace (§8 f1)
             s, p = specular(resx, resy, gen, raydepth=nu or 3, caustic=bool(nv))
         else:
@@ -141,6 +143,17 @@ RENDER_CASES = [
     ("dl_spec_rd3", ("spec_dl", 64, 64, 3, 0), (0, 0, 64, 64), {}),
     ("pt_spec_rd5_caustic", ("spec", 64, 64, 5, 1), (0, 0, 64, 64), {"path_samples": 2}),
     ("pt_spec_rd1_b5", ("spec", 48, 48, 1, 0), (0, 0, 48, 48), {"bounces": 5}),
+    # depth of field (perspectiveCam_t aperture branch + renderTile lens QMC): every bokeh shape,
+    # the three biases, adaptive passes (lens samples continue from pass_offs); parity unpinned vs reference
+    ("pt_dof_disk1", ("dof", 64, 64, A.YK_BOKEH_DISK1, 0), (0, 0, 64, 64), {"aa_samples": 4}),
+    ("pt_dof_disk2_center", ("dof", 64, 64, A.YK_BOKEH_DISK2, A.YK_BOKEH_BIAS_CENTER), (0, 0, 64, 64),
+     {"aa_samples": 3}),
+    ("dl_dof_tri_edge", ("dof_dl", 64, 64, A.YK_BOKEH_TRI, A.YK_BOKEH_BIAS_EDGE), (0, 0, 64, 64), {"aa_samples": 5}),
+    ("pt_dof_hexa", ("dof", 64, 64, A.YK_BOKEH_HEXA, 0), (8, 4, 48, 52), {"aa_samples": 4}),
+    ("pt_dof_ring_aa2", ("dof", 48, 48, A.YK_BOKEH_RING, 0), (0, 0, 48, 48),
+     {"aa_samples": 2, "aa_passes": 2, "aa_inc_samples": 2, "aa_threshold": 0.02}),
+    ("pt_dof_square_pentagon", ("dof", 48, 48, A.YK_BOKEH_PENTA, A.YK_BOKEH_BIAS_CENTER), (0, 0, 48, 48),
+     {"aa_samples": 2}),
 ]
 
 

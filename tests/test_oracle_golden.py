@@ -90,3 +90,26 @@ def test_bumpy1m_frame(bumpy1m):
     d = np.abs(to8(rgba).astype(int) - frame("bumpy1m_480x270_4spp_t1").astype(int))
     assert (d == 0).mean() > 0.999
     assert (d.max(-1) > 1).sum() <= 16
+
+
+def test_dof_camera_changes_only_the_camera_rays():
+    """A thin-lens camera (aperture != 0) moves the camera rays' origins and
+    directions; with aperture 0 the lens code is skipped (the pinhole frame)."""
+    from core_amd import _abi as A
+    from oracle.oracle import Oracle
+    from tests.scenes import dof_cornell
+    s0, p = dof_cornell(32, 32, aperture=0.0)
+    s1, _ = dof_cornell(32, 32, bokeh_type=A.YK_BOKEH_HEXA, aperture=0.08)
+    p.aa_samples = 2
+    _, f0, c0 = Oracle(s0).render(p)
+    _, f1, c1 = Oracle(s1).render(p)
+    from core_amd.scene import probe_scene
+    s2, p2 = probe_scene("cornell_pt", 32, 32)
+    p2.aa_samples = 2
+    _, f2, _ = Oracle(s2).render(p2)
+    assert (f0.view(np.uint32) == f2.view(np.uint32)).all()  # aperture 0 == the generated pinhole camera
+    assert np.abs(f1 - f0).max() > 1e-3
+    st = s1.camera_state()
+    assert abs(st.aperture - 0.08) < 1e-7 and st.bokeh_type == A.YK_BOKEH_HEXA
+    ls = np.array(st.lens_ls[:16])
+    assert np.allclose(ls[0::2] ** 2 + ls[1::2] ** 2, 1.0, atol=2e-3)  # fCos/fSin polynomial pairs
