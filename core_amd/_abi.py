@@ -12,6 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("YK_LIB") or os.path.join(_HERE, "libyk.so")  # YK_LIB: tuning builds
 
 YK_OK = 0
+YK_ERR_ABORTED = 7
 YK_ERR_ARG, YK_ERR_STATE, YK_ERR_HIP, YK_ERR_UNSUPPORTED, YK_ERR_ALLOC, YK_ERR_INTERNAL = 1, 2, 3, 4, 5, 6
 YK_MAT_SHINYDIFFUSE, YK_MAT_LIGHT = 0, 1
 YK_LIGHT_AREA, YK_LIGHT_POINT, YK_LIGHT_DIRECTIONAL = 0, 1, 2
@@ -100,7 +101,8 @@ class yk_render_params(C.Structure):
                 ("aa_samples", C.c_int32), ("aa_passes", C.c_int32), ("filter", C.c_int32),
                 ("aa_pixelwidth", C.c_float), ("tile_size", C.c_int32),
                 ("transp_background", C.c_int32), ("aa_inc_samples", C.c_int32), ("aa_threshold", C.c_float),
-                ("photon", yk_photon_params), ("transp_shadows", C.c_int32), ("shadow_depth", C.c_int32)]
+                ("photon", yk_photon_params), ("transp_shadows", C.c_int32), ("shadow_depth", C.c_int32),
+                ("filter_width", C.c_float)]
 
     def copy(self):
         p = yk_render_params()
@@ -138,6 +140,9 @@ P = C.c_void_p
 i32, i64, u32p = C.c_int32, C.c_int64, C.POINTER(C.c_uint32)
 fp, i32p = C.POINTER(C.c_float), C.POINTER(C.c_int32)
 
+# int32_t (*yk_abort_fn)(void* user)
+ABORT_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p)
+
 # name -> (restype, argtypes); every symbol include/yk_api.h declares
 SIGNATURES = {
     "yk_last_error": (C.c_char_p, []),
@@ -171,6 +176,9 @@ SIGNATURES = {
     "yk_scene_get_camera_state": (C.c_int, [P, C.POINTER(yk_camera_state)]),
     "yk_scene_generate": (C.c_int, [P, C.c_char_p, i32, i32, i32, i32, C.POINTER(yk_render_params)]),
     "yk_render_params_default": (None, [C.POINTER(yk_render_params)]),
+    "yk_film_filter_from_table": (C.c_int, [fp, C.c_float, C.POINTER(yk_render_params)]),
+    "yk_device_count": (C.c_int, [C.POINTER(i32)]),
+    "yk_device_set_abort": (C.c_int, [P, ABORT_FN, P]),
     "yk_device_open": (C.c_int, [i32, C.POINTER(P)]),
     "yk_device_close": (None, [P]),
     "yk_device_upload": (C.c_int, [P, P]),

@@ -2619,6 +2619,8 @@ struct yk_device {
   DScene S{};
   int ntris = 0, max_depth = 0, nlights = 0, sum_light_slots = 0;
   bool spec = false;  // some material has SPECULAR|FILTER components: recursion pipeline
+  yk_abort_fn abort_fn = nullptr;  // yk_device_set_abort: polled between batches
+  void* abort_user = nullptr;
   bool big_leaves = false;  // the resident tree has a leaf of 2^17 references or more: *_big kernels
   bool crowded_leaves = false;  // mean references per non-empty leaf above YK_CROWDED_LEAF: 64-ray hand-out chunks
   int per_cu_ts = 1;
@@ -3007,6 +3009,23 @@ void yk_device_close(yk_device* d) {
 
 void* yk_device_stream(yk_device* d) { return d ? (void*)d->stream : nullptr; }
 
+int yk_device_count(int32_t* n) {
+  if (!n) return set_error(YK_ERR_ARG, "yk_device_count: NULL argument");
+  YK_GUARD_BEGIN
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+  *n = c;
+  return YK_OK;
+  YK_GUARD_END
+}
+
+int yk_device_set_abort(yk_device* d, yk_abort_fn fn, void* user) {
+  if (!d) return set_error(YK_ERR_ARG, "yk_device_set_abort: NULL device");
+  d->abort_fn = fn;
+  d->abort_user = user;
+  return YK_OK;
+}
+
 int yk_device_sync(yk_device* d) {
   if (!d) return set_error(YK_ERR_ARG, "yk_device_sync: NULL device");
   YK_GUARD_BEGIN
@@ -3243,6 +3262,7 @@ static FilmConst make_film(const yk_render_params* p) {
   else if (p->filter == YK_FILTER_GAUSS) fw *= 2.f;
   if (fw < 0.501f) fw = 0.501f;
   if (fw > 4.f) fw = 4.f;
+  if (p->filter_width > 0.f) fw = p->filter_width;  // the live film's filterw (yk_film_filter_from_table)
   F.filterw = fw;
   F.tableScale = 0.9999 * 16 / F.filterw;
   auto r2i = [](double v) { return (int)(v + (0.5 - 1.4e-11)); };
@@ -3269,6 +3289,23 @@ static FilmConst make_film(const yk_render_params* p) {
   F.spp = p->aa_samples > 0 ? p->aa_samples : 1;
   F.d1 = (float)(1.0 / (double)(float)F.spp);
   return F;
+}
+
+int yk_film_filter_from_table(const float* table, float filterw, yk_render_params* p) {
+  if (!table || !p) return set_error(YK_ERR_ARG, "yk_film_filter_from_table: NULL argument");
+  if (!(filterw >= 0.501f && filterw <= 4.f))
+    return set_error(YK_ERR_UNSUPPORTED, "film filterw outside [0.501, 4] (imagefilm.cc:150)");
+  for (int f : {YK_FILTER_BOX, YK_FILTER_MITCHELL, YK_FILTER_GAUSS, YK_FILTER_LANCZOS}) {
+    yk_render_params q = *p;
+    q.filter = f;
+    const FilmConst F = make_film(&q);
+    if (std::memcmp(F.table, table, sizeof F.table) == 0) {
+      p->filter = f;
+      p->filter_width = filterw;
+      return YK_OK;
+    }
+  }
+  return set_error(YK_ERR_UNSUPPORTED, "film filter table is none of box / Mitchell / Gauss / Lanczos2");
 }
 
 }  // extern "C"
@@ -3308,6 +3345,8 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   if (p->integrator == YK_INTEGRATOR_PATH && (p->bounces < 1 || 4 * p->bounces + 4 >= 50))
     return set_error(YK_ERR_UNSUPPORTED, "bounces must be in [1, 11]");
   if (p->width <= 0 || p->height <= 0) return set_error(YK_ERR_ARG, "empty render area");
+  if (p->filter_width != 0.f && !(p->filter_width >= 0.501f && p->filter_width <= 4.f))
+    return set_error(YK_ERR_ARG, "filter_width must be 0 or in [0.501, 4]");
   YK_GUARD_BEGIN
   HIPCHK(hipSetDevice(d->ordinal));
   auto t0 = std::chrono::steady_clock::now();
@@ -3323,6 +3362,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   if (ntiles >= (1 << 19)) return set_error(YK_ERR_UNSUPPORTED, "too many tiles");
   std::vector<int> owned;
   for (int t = shard; t < ntiles; t += nshards) owned.push_back(t);
+  bool aborted = false;
   RenderConst R{};
   R.spp = spp;
   R.nsub = p->integrator == YK_INTEGRATOR_PATH ? std::max(1, p->path_samples) : 1;
@@ -3501,6 +3541,15 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     const int pi = bi % npipes;
     Pipe& P = d->pipe[pi];
     const Batch& B = Bp[pi];
+    if (d->abort_fn) {
+      // abort polling between batches: this pipe's previous batch has
+      // finished (the other pipes keep the GPU busy meanwhile)
+      if (bi >= npipes) HIPCHK(hipStreamSynchronize(P.stream));
+      if (d->abort_fn(d->abort_user)) {
+        aborted = true;
+        break;
+      }
+    }
     const long long nc = nc_of[bi];
     unsigned long long* bw = d->spec ? d->spec_words.p : P.words.p + 8 + words_per_batch * (bi / npipes);
     auto qw = [&](int isub, int depth) { return bw + isub * (bounces + 1) + depth; };
@@ -3710,6 +3759,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   }
   S->camera_samples += (uint64_t)samples_total;
   S->ms_total += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (aborted) return set_error(YK_ERR_ABORTED, "render aborted by the abort callback");
   return YK_OK;
   YK_GUARD_END
 }
@@ -3729,7 +3779,7 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
     return set_error(YK_ERR_UNSUPPORTED, "AA_passes > 1 needs the whole film (nshards = 1): nextPass reads it");
   const int inc = p->aa_inc_samples > 0 ? p->aa_inc_samples : n0;
   int rc = render_pass(d, p, 0, 1, d_film, st, PassSpec{n0, 0, true, nullptr});
-  if (rc != YK_OK) return rc;
+  if (rc != YK_OK) return rc;  // YK_ERR_ABORTED included: no further passes
   YK_GUARD_BEGIN
   const int w = p->width, h = p->height;
   std::vector<uint8_t> flags((size_t)w * h);
@@ -3838,9 +3888,13 @@ int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params
         if (rc[i] != YK_OK) msg[i] = yk_last_error();
       });
     for (auto& t : th) t.join();
-    for (int i = 0; i < ndev; ++i)
-      if (rc[i] != YK_OK) return set_error(rc[i], "device " + std::to_string(i) + ": " + msg[i]);
-    return YK_OK;
+    int out = YK_OK;
+    for (int i = 0; i < ndev; ++i) {
+      if (rc[i] == YK_OK) continue;
+      if (rc[i] != YK_ERR_ABORTED) return set_error(rc[i], "device " + std::to_string(i) + ": " + msg[i]);
+      out = YK_ERR_ABORTED;
+    }
+    return out;
   };
   // acc = film[0] + film[1] + ... (shard order) on device 0
   auto reduce = [&]() {
@@ -3861,9 +3915,9 @@ int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params
   const int n0 = std::max(1, p->aa_samples);  // scene_t::setAntialiasing, scene.cc:736-742
   const bool multipass = p->aa_passes > 1;
   int rc = run(PassSpec{n0, 0, multipass, nullptr});
-  if (rc != YK_OK) return rc;
+  if (rc != YK_OK && rc != YK_ERR_ABORTED) return rc;
   reduce();
-  if (multipass) {
+  if (multipass && rc == YK_OK) {
     const int inc = p->aa_inc_samples > 0 ? p->aa_inc_samples : n0;
     const int w = p->width, h = p->height;
     std::vector<uint8_t> flags(npx);
@@ -3884,8 +3938,9 @@ int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params
         fl = flags.data();
       }
       rc = run(PassSpec{inc, n0 + (pass - 1) * inc, true, fl});
-      if (rc != YK_OK) return rc;
+      if (rc != YK_OK && rc != YK_ERR_ABORTED) return rc;
       reduce();
+      if (rc == YK_ERR_ABORTED) break;
     }
   }
   HIPCHK(hipSetDevice(d0->ordinal));
@@ -3906,6 +3961,7 @@ int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params
       st->shadow_launches += x.shadow_launches;
     }
   }
+  if (rc == YK_ERR_ABORTED) return set_error(rc, "render aborted by the abort callback (film holds the finished batches)");
   return YK_OK;
   YK_GUARD_END
 }

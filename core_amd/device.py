@@ -94,6 +94,11 @@ class Device:
         A.check(A.lib().yk_render_shard(self._p, C.byref(params), shard, nshards, _ptr(film), C.byref(st)))
         return st
 
+    def set_abort(self, fn):
+        """yk_device_set_abort: fn() -> bool is polled between batches; None removes it."""
+        self._abort_cb = None if fn is None else A.ABORT_FN(lambda _user: 1 if fn() else 0)
+        A.check(A.lib().yk_device_set_abort(self._p, self._abort_cb, None))
+
     @staticmethod
     def render_multi(devices, params, stats=None):
         """Whole frame on several devices (yk_render_multi: tiles t % n on

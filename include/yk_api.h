@@ -37,6 +37,7 @@ extern "C" {
 #define YK_ERR_UNSUPPORTED 4
 #define YK_ERR_ALLOC 5
 #define YK_ERR_INTERNAL 6
+#define YK_ERR_ABORTED 7 /* the abort callback asked to stop: the film holds the finished batches */
 
 /* ---- scene description (POD mirrors of the reference paraMap_t params) ---- */
 
@@ -141,6 +142,9 @@ typedef struct yk_render_params {
                               scene_t::isShadowed(.., maxDepth, filt) / IntersectTS    */
   int32_t shadow_depth;    /* "shadowDepth" [5]: transparent surfaces a shadow ray may
                               cross (mcIntegrator_t::sDepth)                           */
+  float filter_width;      /* imageFilm_t::filterw as the film holds it (> 0), taking
+                              precedence over aa_pixelwidth; 0: derived from
+                              aa_pixelwidth as imagefilm.cc:143-150 does [0]            */
 } yk_render_params;
 
 /* one ray, 32 bytes: ray_t (ray.h:26-49) without time */
@@ -235,6 +239,12 @@ int yk_scene_get_camera(const yk_scene* s, yk_camera* out);
 int yk_scene_generate(yk_scene* s, const char* name, int32_t p0, int32_t p1, int32_t resx,
                       int32_t resy, yk_render_params* params_out);
 void yk_render_params_default(yk_render_params* p);
+/* A live imageFilm_t -> render parameters: identifies the film's filter by
+ * comparing its 16x16 filterTable (imagefilm.cc:119-165) with the box /
+ * Mitchell / Gauss / Lanczos2 tables libyk builds, bit for bit, and takes its
+ * filterw as is (p->filter, p->filter_width). YK_ERR_UNSUPPORTED when the
+ * table is none of them or filterw lies outside [0.501, 4]. */
+int yk_film_filter_from_table(const float* filter_table, float filterw, yk_render_params* p);
 
 /* ---- reference object state ----
  * What the reference's constructors computed, for a plugin that reads it out
@@ -305,6 +315,8 @@ int yk_scene_get_area_light_state(const yk_scene* s, int32_t i, yk_area_light_st
 int yk_scene_get_camera_state(const yk_scene* s, yk_camera_state* out);
 
 /* ---- device ---- */
+/* number of GPUs libyk can open (ordinals 0 .. n-1) */
+int yk_device_count(int32_t* n);
 int yk_device_open(int32_t ordinal, yk_device** out);
 void yk_device_close(yk_device* d);
 /* Uploads scene s (geometry, kd-tree, materials, lights, camera) and builds
@@ -313,6 +325,12 @@ void yk_device_close(yk_device* d);
  * cooperative leaf test's limit) or 2^30 - 1 nodes or more (stack entries). */
 int yk_device_upload(yk_device* d, const yk_scene* s);
 int yk_device_sync(yk_device* d);
+/* Abort polling (scene_t::getSignals() & Y_SIG_ABORT, integrator.cc:255):
+ * renders on d call fn(user) between batches (tens of ms apart) and stop when
+ * it returns non-zero -- the batches already running finish, the film holds
+ * them, and the render returns YK_ERR_ABORTED. fn NULL removes the callback. */
+typedef int32_t (*yk_abort_fn)(void* user);
+int yk_device_set_abort(yk_device* d, yk_abort_fn fn, void* user);
 /* hipStream_t the kernels run on, as an opaque pointer (for external timing) */
 void* yk_device_stream(yk_device* d);
 

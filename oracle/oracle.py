@@ -49,6 +49,8 @@ def lib():
         L.orc_shadow_ts.argtypes = [vp, C.c_int64, C.c_int32, vp, vp, vp]
         L.orc_point_gather.argtypes = [vp, C.c_int32, vp, C.c_int32, vp, vp, vp]
         L.orc_point_nearest.argtypes = [vp, vp, C.c_int32, vp, vp, C.c_float]
+        L.orc_film_table.restype = C.c_float
+        L.orc_film_table.argtypes = [vp, vp]
         _lib = L
     return _lib
 
@@ -194,3 +196,12 @@ def point_nearest(pos, dirs, q, nrm, dist):
     q = np.ascontiguousarray(q, np.float32)
     nrm = np.ascontiguousarray(nrm, np.float32)
     return lib().orc_point_nearest(pos.ctypes.data, dirs.ctypes.data, len(pos), q.ctypes.data, nrm.ctypes.data, dist)
+
+
+def film_table(params):
+    """imageFilm_t's 16x16 filter table and filterw for these params (the
+    oracle's restatement of imagefilm.cc:119-165)."""
+    t = np.zeros(256, np.float32)
+    fw = lib().orc_film_table(C.addressof(params), t.ctypes.data)
+    return t, fw
+

@@ -2187,6 +2187,7 @@ static void film_init(film_t* F, const yk_render_params* P) {
   else if (P->filter == YK_FILTER_GAUSS) { ff = f_gauss; F->filterw *= 2.f; }
   float fw = F->filterw < 0.501f ? 0.501f : F->filterw;
   if (fw > 0.5f * MAX_FILTER_SIZE) fw = 0.5f * MAX_FILTER_SIZE;
+  if (P->filter_width > 0.f) fw = P->filter_width; /* the live film's filterw (plugin) */
   F->filterw = fw;
   float scale = 1.f / (float)FILTER_TABLE_SIZE;
   for (int y = 0; y < FILTER_TABLE_SIZE; ++y)
@@ -2501,6 +2502,18 @@ static int render_tiles(const yk_render_params* P, int shard, int nshards, float
   }
   free(F.acc);
   return 0;
+}
+
+/* imageFilm_t's filter table and filterw for params P (imagefilm.cc:119-165):
+ * the checker for yk_film_filter_from_table */
+float orc_film_table(const yk_render_params* P, float* table256) {
+  film_t F;
+  yk_render_params q = *P;
+  q.width = q.height = 1;
+  film_init(&F, &q);
+  memcpy(table256, F.table, 256 * sizeof(float));
+  free(F.acc);
+  return F.filterw;
 }
 
 /* QMC probes for the unit tests */

@@ -112,6 +112,9 @@ RENDER_CASES = [
     ("dl_cornell", ("cornell_dl", 128, 128, 0, 0), (16, 20, 80, 72), {}),
     ("pt_cornell", ("cornell_pt", 64, 64, 0, 0), (0, 0, 64, 64), {}),
     ("pt_cornell_mitchell", ("cornell_pt", 64, 64, 0, 0), (5, 3, 50, 45), {"filter": A.YK_FILTER_MITCHELL}),
+    # the live film's filterw handed over as is (yk_film_filter_from_table, the plugin's path)
+    ("pt_cornell_mitchell_fw", ("cornell_pt", 64, 64, 0, 0), (5, 3, 50, 45),
+     {"filter": A.YK_FILTER_MITCHELL, "filter_width": 1.7}),
     # Gauss / Lanczos2 filter tables (imagefilm.cc:97-119, compiled forms; parity unpinned vs reference outputs)
     ("pt_cornell_gauss", ("cornell_pt", 64, 64, 0, 0), (3, 2, 56, 50),
      {"filter": A.YK_FILTER_GAUSS, "aa_pixelwidth": 1.5}),
@@ -295,3 +298,30 @@ def test_refused_upload_keeps_the_resident_scene(gpu_device):
     prim, t, *_ = orc.intersect(rays)
     gp, gt, *_ = gpu_device.split_hits(gpu_device.trace_closest(gpu_device.rays_to_device(rays)))
     assert (gp == prim).all() and (gt[prim >= 0].view(np.uint32) == t[prim >= 0].view(np.uint32)).all()
+
+
+def test_abort_callback_stops_between_batches(gpu_device):
+    """yk_device_set_abort (Y_SIG_ABORT polling, integrator.cc:255): the
+    callback runs between batches; once it answers yes no further batch
+    starts, the film keeps the finished ones and the render reports
+    YK_ERR_ABORTED. Removing the callback restores full renders."""
+    s, p = probe_scene("bumpy", 1920, 1080, 120, 61)
+    p.aa_samples = 64  # 133M camera samples: several 32M-sample batches
+    gpu_device.upload(s)
+    calls = []
+
+    def abort_after_two_batches():
+        calls.append(1)
+        return len(calls) > 2
+
+    gpu_device.set_abort(abort_after_two_batches)
+    film = gpu_device.new_film(p)
+    with pytest.raises(A.YkError) as e:
+        gpu_device.render_shard(p, film)
+    assert e.value.code == A.YK_ERR_ABORTED
+    w = film.cpu().numpy()[..., 4]
+    assert len(calls) == 3
+    assert (w > 0).any() and (w == 0).any()  # the first two batches' tiles only
+    gpu_device.set_abort(None)
+    st = gpu_device.render_shard(p, gpu_device.new_film(p))
+    assert st.camera_samples == 1920 * 1080 * 64
