@@ -12,9 +12,15 @@
 //   preprocess(): hand prims (scene_t::update order, scene.cc:760-781),
 //                 material / area-light / camera *object state* to libyk,
 //                 build the kd-tree, upload to the device
-//   render():     yk_render_shard over all tiles, then write the film sums
-//                 into imageFilm_t's pixel buffer; the reference's own flush()
-//                 normalises them exactly as k_film_resolve does
+//   render():     yk_render_multi over all GPUs of the node (tiles t % N on
+//                 GPU i, one host thread per GPU, film reduced over xGMI),
+//                 then write the film sums into imageFilm_t's pixel buffer;
+//                 the reference's own flush() normalises them exactly as
+//                 k_film_resolve does
+// What the GPU path cannot reproduce is refused with an error, never rendered
+// differently: textured / Oren-Nayar materials, other lights / backgrounds /
+// cameras / volume integrators, film filters libyk does not build, premultiplied
+// alpha (compounded per pixel, imagefilm.cc:502), depth passes.
 #include <core_api/environment.h>
 #include <core_api/imagefilm.h>
 #include <core_api/scene.h>
@@ -25,6 +31,7 @@
 #include <yafraycore/meshtypes.h>
 #include <yafraycore/triangle.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -106,12 +113,20 @@ YK_MEMBER(CamVup, camera_t, vector3d_t, vup)
 YK_MEMBER(CamVright, camera_t, vector3d_t, vright)
 YK_MEMBER(CamNear, camera_t, plane_t, near_plane)
 YK_MEMBER(CamFar, camera_t, plane_t, far_plane)
+YK_MEMBER(CamAperture, perspectiveCam_t, PFLOAT, aperture)
+YK_MEMBER(CamDofDistance, perspectiveCam_t, PFLOAT, dof_distance)
+YK_MEMBER(CamDofRt, perspectiveCam_t, vector3d_t, dof_rt)
+YK_MEMBER(CamDofUp, perspectiveCam_t, vector3d_t, dof_up)
+YK_MEMBER(CamBokeh, perspectiveCam_t, perspectiveCam_t::bokehType, bkhtype)
+YK_MEMBER(CamBokehBias, perspectiveCam_t, perspectiveCam_t::bkhBiasType, bkhbias)
+YK_MEMBER(CamLS, perspectiveCam_t, std::vector<PFLOAT>, LS)
 YK_MEMBER(FilmImage, imageFilm_t, rgba2DImage_t*, image)
 YK_MEMBER(FilmCx0, imageFilm_t, int, cx0)
 YK_MEMBER(FilmCy0, imageFilm_t, int, cy0)
 YK_MEMBER(FilmFilterW, imageFilm_t, float, filterw)
 YK_MEMBER(FilmTable, imageFilm_t, float*, filterTable)
 YK_MEMBER(FilmTileSize, imageFilm_t, int, tileSize)
+YK_MEMBER(FilmPremult, imageFilm_t, bool, premultAlpha)
 #define GET(obj, Tag) ((obj).*member_of<Tag>::ptr)
 
 // pointLight_t, directionalLight_t and constBackground_t are defined inside
@@ -273,22 +288,54 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     put3(cs.far_p, fp.x, fp.y, fp.z);
     cs.resx = cam->resX();
     cs.resy = cam->resY();
+    // depth of field: the lens state the constructor and setAxis computed
+    // (perspectiveCamera.cc:29-71); libyk samples it as renderTile does
+    const perspectiveCam_t& pc = *cam;
+    cs.aperture = GET(pc, CamAperture);
+    cs.dof_distance = GET(pc, CamDofDistance);
+    const vector3d_t &drt = GET(pc, CamDofRt), &dup = GET(pc, CamDofUp);
+    put3(cs.dof_rt, drt.x, drt.y, drt.z);
+    put3(cs.dof_up, dup.x, dup.y, dup.z);
+    cs.bokeh_type = (int32_t)GET(pc, CamBokeh);
+    cs.bokeh_bias = (int32_t)GET(pc, CamBokehBias);
+    const std::vector<PFLOAT>& ls = GET(pc, CamLS);
+    if (ls.size() > 16) return unsupported("bokeh polygon table larger than 16 entries");
+    for (size_t i = 0; i < ls.size(); ++i) cs.lens_ls[i] = ls[i];
     if (yk_scene_set_camera_state(ys, &cs) != YK_OK) return fail();
+    // the empty volume integrator leaves integrate()'s colour as is
+    // (pathtracer.cc:323-328 with transmittance 1, integrate 0)
+    if (scene->volIntegrator && std::string(typeid(*scene->volIntegrator).name()) != "N7yafaray21EmptyVolumeIntegratorE")
+      return unsupported("volume integrators other than \"none\" are not on the GPU path");
     if (yk_scene_build(ys) != YK_OK) return fail();
-    if (yk_device_open(0, &dev) != YK_OK || yk_device_upload(dev, ys) != YK_OK) return fail();
-    if (gpu_tree) {  // opt-in: replace the reference tree by the device-built one
-      yk_tree_info ti{};
-      if (yk_device_build_tree(dev, ys, 0, &ti) != YK_OK) return fail();
-      Y_INFO << integratorName << ": device kd-tree, " << ti.nodes << " nodes (" << ti.ms_build << " ms)" << yendl;
+    // every GPU of the node holds the scene (replicated
+    // scene, tiles sharded); "gpus" > 0 limits the count
+    int32_t ndev = 0;
+    if (yk_device_count(&ndev) != YK_OK || ndev < 1) return unsupported("no GPU for the GPU path");
+    if (max_gpus > 0 && ndev > max_gpus) ndev = max_gpus;
+    for (int32_t g = 0; g < ndev; ++g) {
+      yk_device* d = nullptr;
+      if (yk_device_open(g, &d) != YK_OK) return fail();
+      devs.push_back(d);
+      if (yk_device_upload(d, ys) != YK_OK) return fail();
+      if (yk_device_set_abort(d, &gpuTiledIntegrator_t::abort_requested, scene) != YK_OK) return fail();
+      if (gpu_tree) {  // opt-in: replace the reference tree by the device-built one
+        yk_tree_info ti{};
+        if (yk_device_build_tree(d, ys, 0, &ti) != YK_OK) return fail();
+        if (g == 0)
+          Y_INFO << integratorName << ": device kd-tree, " << ti.nodes << " nodes (" << ti.ms_build << " ms)" << yendl;
+      }
     }
     const bool pt_photons = params.integrator == YK_INTEGRATOR_PATH &&
                             (params.caustic_type == YK_CAUSTIC_PHOTON || params.caustic_type == YK_CAUSTIC_BOTH);
+    // photon maps: every GPU builds the same maps from the same inputs (the
+    // build is deterministic), so each holds a replica
     if (pt_photons) {
       // pathIntegrator_t::preprocess -> mcIntegrator_t::createCausticMap
       // (pathtracer.cc:90-93, mcintegrator.cc:197-377) on the device; the
       // caustic pass draws no ourRandom() numbers
       yk_photon_info info{};
-      if (yk_photon_build(dev, &params, &info) != YK_OK) return fail();
+      for (yk_device* d : devs)
+        if (yk_photon_build(d, &params, &info) != YK_OK) return fail();
       Y_INFO << integratorName << ": " << info.caustic_photons << " caustic photons (" << info.ms_total << " ms)"
              << yendl;
     }
@@ -299,11 +346,13 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
       // reference had drawn them
       params.photon.seed = myseed;
       yk_photon_info info{};
-      if (yk_photon_build(dev, &params, &info) != YK_OK) return fail();
+      for (yk_device* d : devs)
+        if (yk_photon_build(d, &params, &info) != YK_OK) return fail();
       myseed = info.seed_out;
       Y_INFO << integratorName << ": " << info.diffuse_photons << " diffuse photons, " << info.radiance_photons
              << " radiance photons (" << info.ms_total << " ms)" << yendl;
     }
+    Y_INFO << integratorName << ": rendering on " << devs.size() << " GPU(s)" << yendl;
     return true;
   }
 
@@ -312,8 +361,8 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     int aa_inc;
     CFLOAT thr;
     scene->getAAParameters(params.aa_samples, params.aa_passes, aa_inc, thr);
-    // AA_passes > 1: the device runs nextPass's adaptive passes itself
-    // (single shard: this process renders the whole film)
+    // AA_passes > 1: libyk runs nextPass's adaptive passes itself, with the
+    // flags of the film reduced over all GPUs
     params.aa_inc_samples = aa_inc;
     params.aa_threshold = (float)thr;
     rgba2DImage_t* img = GET(*film, FilmImage);
@@ -323,15 +372,15 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     params.xstart = GET(*film, FilmCx0);
     params.ystart = GET(*film, FilmCy0);
     params.tile_size = GET(*film, FilmTileSize);
-    // filter: the film built its table from (type, AA_pixelwidth)
-    // (imagefilm.cc:119-165); box tables are all 1, Mitchell's are not, and
-    // filterw = clamp(0.5 * pixelwidth * k, 0.501, 4) gives the width back
-    const float fw = GET(*film, FilmFilterW);
-    const bool box = GET(*film, FilmTable)[0] == 1.f && GET(*film, FilmTable)[255] == 1.f;
-    params.filter = box ? YK_FILTER_BOX : YK_FILTER_MITCHELL;
-    params.aa_pixelwidth = box ? 2.f * fw : 2.f * fw / 2.6f;
+    // filter: libyk names it from the table the film built (imagefilm.cc:
+    // 119-165) and takes filterw as the film holds it; a table it does not
+    // build is refused
+    if (yk_film_filter_from_table(GET(*film, FilmTable), GET(*film, FilmFilterW), &params) != YK_OK) return fail();
+    if (GET(*film, FilmPremult)) return unsupported("premultiplied alpha films are not on the GPU path");
+    if (scene->doDepth()) return unsupported("depth passes are not on the GPU path");
     std::vector<float> sums((size_t)w * h * 5);
-    if (yk_render_film(dev, &params, 0, 1, sums.data(), nullptr) != YK_OK) return fail();
+    const int rc = yk_render_multi(devs.data(), (int32_t)devs.size(), &params, sums.data(), nullptr);
+    if (rc != YK_OK && rc != YK_ERR_ABORTED) return fail();  // aborted: keep what was rendered, as renderTile does
     for (int j = 0; j < h; ++j)
       for (int i = 0; i < w; ++i) {
         const float* s = &sums[5 * ((size_t)j * w + i)];
@@ -346,6 +395,12 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
 
   // unused: render() never calls renderTile()
   colorA_t integrate(renderState_t&, diffRay_t&) const override { return colorA_t(0.f); }
+
+  // Y_SIG_ABORT polling (renderTile, integrator.cc:255), called by libyk
+  // between batches on every GPU's host thread
+  static int32_t abort_requested(void* user) {
+    return (static_cast<const scene_t*>(user)->getSignals() & Y_SIG_ABORT) ? 1 : 0;
+  }
 
   static integrator_t* factory_path(paraMap_t& pm, renderEnvironment_t&) {
     yk_render_params p;
@@ -383,7 +438,7 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
       }
     }
     auto* it = new gpuTiledIntegrator_t(p, "PathTracer");
-    pm.getParam("gpu_kdtree", it->gpu_tree);
+    it->read_plugin_params(pm);
     return it;
   }
   static integrator_t* factory_direct(paraMap_t& pm, renderEnvironment_t&) {
@@ -396,7 +451,7 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     pm.getParam("bg_transp", bg);
     p.transp_background = bg;
     auto* it = new gpuTiledIntegrator_t(p, "DirectLight");
-    pm.getParam("gpu_kdtree", it->gpu_tree);
+    it->read_plugin_params(pm);
     return it;
   }
   // "transpShad" / "shadowDepth" -> mcIntegrator_t::trShad / sDepth; the
@@ -455,11 +510,17 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     q.fg_min_pathlen = gather_dist;
     q.show_map = show_map;
     auto* it = new gpuTiledIntegrator_t(p, "PhotonMap");
-    pm.getParam("gpu_kdtree", it->gpu_tree);
+    it->read_plugin_params(pm);
     return it;
   }
 
  private:
+  // GPU-path options: "gpu_kdtree" (device-built tree, documented tie-break)
+  // and "gpus" (> 0: at most this many GPUs)
+  void read_plugin_params(paraMap_t& pm) {
+    pm.getParam("gpu_kdtree", gpu_tree);
+    pm.getParam("gpus", max_gpus);
+  }
   bool material_id(const material_t* m, std::map<const material_t*, int32_t>& ids, int32_t& id) {
     auto it = ids.find(m);
     if (it != ids.end()) return (id = it->second), true;
@@ -518,16 +579,17 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     return false;
   }
   void release() {
-    if (dev) yk_device_close(dev);
+    for (yk_device* d : devs) yk_device_close(d);
     if (ys) yk_scene_destroy(ys);
-    dev = nullptr;
+    devs.clear();
     ys = nullptr;
   }
 
   yk_render_params params;
   bool gpu_tree = false;  // "gpu_kdtree": device-built tree (yk_device_build_tree), documented tie-break
+  int max_gpus = 0;       // "gpus": 0 = every GPU of the node
   yk_scene* ys = nullptr;
-  yk_device* dev = nullptr;
+  std::vector<yk_device*> devs;  // one per GPU, the scene replicated on each
 };
 
 extern "C" {
