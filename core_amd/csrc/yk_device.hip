@@ -773,6 +773,8 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   // are the other kernel kind's accumulators): wave iterations, active lanes per iteration, wave-level
   // descent / leaf-loop trips (max over lanes), refills
   unsigned long long s_it = 0, s_act = 0, s_dmax = 0, s_lmax = 0, s_refill = 0;
+  // cycles per phase (clock64 deltas, wave-uniform): refill, descent, leaf test, pop
+  unsigned long long c_ref = 0, c_desc = 0, c_leaf = 0, c_pop = 0, c_t0 = clock64();
 #endif
   for (;;) {
     const unsigned long long want = __ballot(rid < 0 && !exhausted);
@@ -836,6 +838,13 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       pool_next = (unsigned)__builtin_amdgcn_readfirstlane((int)pool_next);
       pool_end = (unsigned)__builtin_amdgcn_readfirstlane((int)pool_end);
     }
+#ifdef YK_TRAV_STATS
+    {
+      const unsigned long long t = clock64();
+      c_ref += t - c_t0;
+      c_t0 = t;
+    }
+#endif
     if (__ballot(rid >= 0) == 0ull) {
       if (__ballot(!exhausted) == 0ull) break;
       continue;
@@ -855,8 +864,24 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       uint32_t w0 = 0, nref = 0;
       bool paused = false;
       if (act) live = trav_descend<CLOSEST>(S, st, stk, nnodes, w0, nref, paused);
+#ifdef YK_TRAV_STATS
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      {
+        const unsigned long long t = clock64();
+        c_desc += t - c_t0;
+        c_t0 = t;
+      }
+#endif
       bool occ = false;
       coop_leaves<CLOSEST, BIG>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, otab, ntris, occ);
+#ifdef YK_TRAV_STATS
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      {
+        const unsigned long long t = clock64();
+        c_leaf += t - c_t0;
+        c_t0 = t;
+      }
+#endif
       if (act) {
         bool done = !live || occ || (!paused && trav_next<CLOSEST>(S, st, stk));
         if (runaway) {
@@ -876,6 +901,14 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
           rid = -1;
         }
       }
+#ifdef YK_TRAV_STATS
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      {
+        const unsigned long long t = clock64();
+        c_pop += t - c_t0;
+        c_t0 = t;
+      }
+#endif
     } else if (rid >= 0) {
       bool occ = false;
       bool done = trav_step<CLOSEST, TS>(S, st, stk, nnodes, ntris, occ);
@@ -922,6 +955,10 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
     atomicAdd(&ctr[6], s_dmax);
     atomicAdd(&ctr[7], s_lmax);
     atomicAdd(&ctr[8], s_refill);
+    atomicAdd(&ctr[9], c_ref);
+    atomicAdd(&ctr[10], c_desc);
+    atomicAdd(&ctr[11], c_leaf);
+    atomicAdd(&ctr[12], c_pop);
   }
 #endif
   // wave-reduced work counters (nodes visited, triangle tests)
@@ -2904,7 +2941,7 @@ void launch_trace(yk_device* d, Pipe& P, const yk_ray* rays, long long n, yk_hit
   unsigned long long* acc = P.counters.p + 128;
   HIPCHK(hipMemsetAsync(work, 0, 144 * sizeof(unsigned long long), P.stream));
   enqueue_trace<CLOSEST>(d, P, rays, nullptr, RayCount{nullptr, 0, n}, hits, occ, work, acc, P.ev0, P.ev1);
-  unsigned long long h[9];
+  unsigned long long h[13];
   HIPCHK(hipMemcpyAsync(h, acc, sizeof h, hipMemcpyDeviceToHost, P.stream));
   HIPCHK(hipStreamSynchronize(P.stream));
   if (h[2]) throw std::runtime_error("kd-tree traversal watchdog fired on " + std::to_string(h[2]) + " rays");
@@ -2917,6 +2954,12 @@ void launch_trace(yk_device* d, Pipe& P, const yk_ray* rays, long long n, yk_hit
                CLOSEST ? "closest" : "shadow", n, h[4], (double)h[5] / (double)h[4], (double)h[6] / (double)h[4],
                (double)h[0] / (double)h[5], (double)h[7] / (double)h[4], (double)h[1] / (double)h[5], h[8],
                (double)n / (double)h[8]);
+  {
+    const double tot = (double)(h[9] + h[10] + h[11] + h[12]);
+    std::fprintf(stderr, "[trav-stats] %s cycles: refill %.1f%% descent %.1f%% leaf %.1f%% pop %.1f%%; per wave iteration %.0f\n",
+                 CLOSEST ? "closest" : "shadow", 100.0 * h[9] / tot, 100.0 * h[10] / tot, 100.0 * h[11] / tot,
+                 100.0 * h[12] / tot, tot / (double)h[4]);
+  }
 #endif
   if (!st) return;
   if (CLOSEST) {

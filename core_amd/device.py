@@ -96,7 +96,7 @@ class Device:
 
     def set_abort(self, fn):
         """yk_device_set_abort: fn() -> bool is polled between batches; None removes it."""
-        self._abort_cb = None if fn is None else A.ABORT_FN(lambda _user: 1 if fn() else 0)
+        self._abort_cb = A.ABORT_FN() if fn is None else A.ABORT_FN(lambda _user: 1 if fn() else 0)
         A.check(A.lib().yk_device_set_abort(self._p, self._abort_cb, None))
 
     @staticmethod
