@@ -24,6 +24,8 @@ YK_CAUSTIC_NONE, YK_CAUSTIC_PATH, YK_CAUSTIC_PHOTON, YK_CAUSTIC_BOTH = 0, 1, 2, 
 YK_BOKEH_DISK1, YK_BOKEH_DISK2, YK_BOKEH_TRI, YK_BOKEH_SQR, YK_BOKEH_PENTA, YK_BOKEH_HEXA, YK_BOKEH_RING = \
     0, 1, 3, 4, 5, 6, 7
 YK_BOKEH_BIAS_NONE, YK_BOKEH_BIAS_CENTER, YK_BOKEH_BIAS_EDGE = 0, 1, 2
+YK_MODE_TRIANGLE, YK_MODE_UNIVERSAL = 0, 1
+YK_MESH_TRIM, YK_MESH_VTRIM = 0, 1
 
 f3 = C.c_float * 3
 
@@ -124,7 +126,7 @@ class yk_scene_info(C.Structure):
                 ("max_depth", C.c_int32), ("inodes", C.c_int32), ("leaves", C.c_int32),
                 ("empty_leaves", C.c_int32), ("leaf_refs", C.c_int32),
                 ("depth_limit_leaves", C.c_int32), ("bad_split_leaves", C.c_int32),
-                ("bound", C.c_float * 6), ("build_seconds", C.c_double)]
+                ("bound", C.c_float * 6), ("build_seconds", C.c_double), ("mode", C.c_int32)]
 
 
 class yk_stats(C.Structure):
@@ -153,6 +155,8 @@ SIGNATURES = {
     "yk_scene_add_mesh": (C.c_int, [P, fp, i32, i32p, i32, i32, i32p]),
     "yk_scene_set_mesh_normals": (C.c_int, [P, i32, fp, i32, i32p, i32]),
     "yk_scene_set_mesh_base": (C.c_int, [P, i32]),
+    "yk_scene_set_mode": (C.c_int, [P, i32]),
+    "yk_scene_set_mesh_type": (C.c_int, [P, i32, i32]),
     "yk_scene_add_curve": (C.c_int, [P, fp, i32, i32, C.c_float, C.c_float, C.c_float, i32p]),
     "yk_scene_add_instance": (C.c_int, [P, i32, fp, i32p]),
     "yk_scene_export_shading": (C.c_int, [P, C.c_void_p, fp]),

@@ -282,8 +282,12 @@ static void normalize3(float* v) {
 
 void Scene::finalize() {
   // scene_t::update, scene.cc:755-782: visible non-base TRIM meshes and
-  // instances in object id order, triangles in insertion order.
+  // instances in object id order, triangles in insertion order. Universal
+  // mode (scene.cc:791-819): the VTRIM meshes in object id order, visible or
+  // not; vTriangle_t::getSurface smooths with is_smooth and takes normal
+  // index 0 as "none" (na > 0, triangle.cc:410-415).
   auto t0 = std::chrono::steady_clock::now();
+  const bool uni = mode == YK_MODE_UNIVERSAL;
   tri_verts.clear();
   tri_material.clear();
   tri_normal.clear();
@@ -291,7 +295,7 @@ void Scene::finalize() {
   tri_vnormal.clear();
   any_smooth = false;
   for (const Mesh& inst : meshes) {
-    if (!inst.visible || inst.is_base) continue;
+    if (uni ? inst.type != YK_MESH_VTRIM : (!inst.visible || inst.is_base || inst.type != YK_MESH_TRIM)) continue;
     const bool is_inst = inst.instance_of >= 0;
     const Mesh& m = is_inst ? meshes[inst.instance_of] : inst;
     const size_t nf = m.faces.size() / 3;
@@ -301,6 +305,7 @@ void Scene::finalize() {
     // is_smooth || normals_exported and treats normal index 0 as missing
     // (triangle.cc:19-26 vs 185-192)
     const bool smooth = is_inst ? (m.is_smooth || m.normals_exported) : m.is_smooth;
+    const bool idx0_none = is_inst || uni;  // normal index 0 treated as missing
     for (size_t f = 0; f < nf; ++f) {
       float tv[9], base_tv[9];
       for (int k = 0; k < 3; ++k) {
@@ -327,7 +332,7 @@ void Scene::finalize() {
       if (smooth) {
         for (int k = 0; k < 3; ++k) {
           const int ni = m.face_normals.empty() ? -1 : m.face_normals[3 * f + k];
-          const bool has = is_inst ? (ni > 0) : (ni >= 0);
+          const bool has = idx0_none ? (ni > 0) : (ni >= 0);
           if (has && ni >= nn) throw std::invalid_argument("face references a missing vertex normal");
           if (has) {
             if (is_inst) xform_vector(inst.m, &m.normals[3 * ni], vn + 3 * k);

@@ -24,6 +24,7 @@ struct Mesh {
   int material = -1;
   bool visible = true;
   bool is_base = false;       // instancing base: not traced itself
+  int type = YK_MESH_TRIM;    // startTriMesh type: TRIM (triangle_t) or VTRIM (vTriangle_t)
   // vertex normals (triangleObject_t::normals) and per-face indices (na,nb,nc)
   std::vector<float> normals;
   std::vector<int> face_normals;  // 3 per face, -1 = none (empty: all -1)
@@ -35,6 +36,7 @@ struct Mesh {
 
 struct Scene {
   std::vector<Mesh> meshes;          // object-id order
+  int mode = YK_MODE_TRIANGLE;       // scene_t::mode: which meshes the tree holds
   // parameter-level descriptions (when the caller gave them) ...
   std::vector<yk_material> materials;
   std::vector<bool> material_has_params;

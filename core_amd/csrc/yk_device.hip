@@ -101,6 +101,7 @@ struct DScene {
   int nlights;
   unsigned nnodes;  // node count, for the pop-time bounds guard
   unsigned chunk_max;  // largest ray hand-out chunk (64 for crowded-leaf scenes, whose rays are costly)
+  int uni;             // universal mode (vTriangle_t getSurface: b0 = 0; IntersectS t > tmin)
 };
 
 __device__ __forceinline__ v3 ld3(const float* p) { return V3(p[0], p[1], p[2]); }
@@ -216,8 +217,10 @@ __device__ __forceinline__ void exit_pb(Trav& st) {
 }
 
 // scene_t::intersect (scene.cc:852-879) / isShadowed (scene.cc:881-902)
-// setup + tree bound test; false = miss.
-template <bool CLOSEST, bool TS = false>
+// setup + tree bound test; false = miss. UNI: universal mode, whose
+// IntersectS accepts t > tmin of the shifted ray (ray_kdtree.cc:936), kept
+// as t >= the next float after tmin.
+template <bool CLOSEST, bool TS = false, bool UNI = false>
 __device__ __forceinline__ bool trav_begin(const DScene& S, Trav& st, const yk_ray& r) {
   st.d = V3(r.dir[0], r.dir[1], r.dir[2]);
   if (CLOSEST) {
@@ -226,8 +229,9 @@ __device__ __forceinline__ bool trav_begin(const DScene& S, Trav& st, const yk_r
     st.dist = (r.tmax < 0.f) ? INFINITY : r.tmax;
   } else {
     st.o = V3(r.from[0] + r.tmin * st.d.x, r.from[1] + r.tmin * st.d.y, r.from[2] + r.tmin * st.d.z);
-    // IntersectS accepts t >= 0; IntersectTS keeps the ray's tmin (kdtree.cc:1061)
-    st.tmin = TS ? r.tmin : 0.f;
+    // IntersectS accepts t >= 0 (universal: t > tmin); IntersectTS keeps the
+    // ray's tmin in both modes (kdtree.cc:1061, ray_kdtree.cc identical)
+    st.tmin = TS ? r.tmin : (UNI ? nextafterf(r.tmin, INFINITY) : 0.f);
     st.dist = (r.tmax < 0.f) ? INFINITY : r.tmax - 2.0f * r.tmin;
   }
   if (TS) {
@@ -608,7 +612,7 @@ __device__ __forceinline__ unsigned dpp_max_scan(unsigned x) {
 // 24-bit owner keys: the keys then hold the start relative to the round and
 // the owner's start is read from its lane (one cross-lane read more per
 // round; measured 0.7 % slower, so only such trees run it).
-template <bool CLOSEST, bool BIG = false>
+template <bool CLOSEST, bool BIG = false, bool UNI = false>
 __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t nref, uint32_t w0, int lane,
                                             unsigned long long* keys, float4* cand, unsigned* otab,
                                             unsigned& ntris, bool& occluded) {
@@ -650,7 +654,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
     const v3 ro = V3(__shfl(st.o.x, own), __shfl(st.o.y, own), __shfl(st.o.z, own));
     const v3 rd = V3(__shfl(st.d.x, own), __shfl(st.d.y, own), __shfl(st.d.z, own));
     const float rz = __shfl(zlim, own);
-    const float rtmin = CLOSEST ? __shfl(st.tmin, own) : 0.f;
+    const float rtmin = (CLOSEST || UNI) ? __shfl(st.tmin, own) : 0.f;
     bool valid = false;
     unsigned long long key = 0;
     float th = 0.f, u = 0.f, v = 0.f;
@@ -724,7 +728,7 @@ struct RayCount {
   }
 };
 
-template <bool CLOSEST, int NSEG, bool TS = false, bool BIG = false>
+template <bool CLOSEST, int NSEG, bool TS = false, bool BIG = false, bool UNI = false>
 __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx,
                                            RayCount rc, yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
                                            unsigned long long* __restrict__ work, unsigned long long* __restrict__ ctr,
@@ -814,7 +818,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
           const int r = idx ? (int)idx[q] : (int)q;
           const yk_ray ray = rays[r];
           if (TS) st.ts_max = ts_depth;
-          if (trav_begin<CLOSEST, TS>(S, st, ray)) {
+          if (trav_begin<CLOSEST, TS, UNI>(S, st, ray)) {
             rid = r;
           } else if (CLOSEST) {
             hits[r] = yk_hit{-1, 0.f, 0.f, 0.f};
@@ -873,7 +877,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       }
 #endif
       bool occ = false;
-      coop_leaves<CLOSEST, BIG>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, otab, ntris, occ);
+      coop_leaves<CLOSEST, BIG, UNI>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, otab, ntris, occ);
 #ifdef YK_TRAV_STATS
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       {
@@ -979,8 +983,14 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 // closest-hit at 5 waves/SIMD (96 VGPRs; 6 / 4 waves measured 2644 / 2593
 // against 2810 Mrays/s) with per-XCD ray segments (+12 % from L2 locality);
 // any-hit at 5 (92 VGPRs, no spill: at 6 it spilled 13-17 VGPRs and moved
-// between 2806 and 2636 with unrelated code changes) with one shared segment
-// (per-XCD segments measured 2700 against 2719). Crowded-leaf scenes (hair)
+// between 2806 and 2636 with unrelated code changes; round 3: 6 waves with 17
+// spills 2668, 4 waves 2781 against 2835) with one shared segment (per-XCD
+// segments: 2700 against 2719 in round 2, 2806 against 2800 in round 3).
+// Non-temporal ray / result accesses measured 2775 against 2824; resident
+// grids below the occupancy limit (room for the other pipes' shading) lost
+// 2-4 %. PMC (round 3, tools/gpu_pmc_tb.sh): the any-hit kernel's texture
+// data path is busy 85 % of its cycles, 58 % of them stalled on L1 misses
+// (L1 hit 68 %, L2 hit 65 %, 360-cycle L2 latency). Crowded-leaf scenes (hair)
 // run the same kernels with 64-ray hand-out chunks (DScene.chunk_max).
 #ifndef YK_CLOSEST_WAVES
 #define YK_CLOSEST_WAVES 5
@@ -1013,6 +1023,20 @@ k_trace_shadow_big(DScene S, const yk_ray* __restrict__ rays, const unsigned* __
                    unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
   trace_body<false, 1, false, true>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
+// universal-mode scenes (kdTree_t<primitive_t>::IntersectS: t > tmin)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
+k_trace_shadow_uni(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+                   yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
+                   unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
+  trace_body<false, 1, false, false, true>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth,
+                                                        refill_min);
+}
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
+k_trace_shadow_big_uni(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+                       yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
+                       unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
+  trace_body<false, 1, false, true, true>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+}
 // transparent shadows (scene_t::isShadowed(state, ray, maxDepth, filt),
 // scene.cc:904-928 -> IntersectTS): occlusion + filter colour per ray
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5)))
@@ -1040,7 +1064,9 @@ __device__ __forceinline__ SurfPt make_surface(const DScene& S, v3 from, v3 dir,
     // u = b0 = 1-(b1+b2) (compiled form of intersect's 1-u-v); va..vc resolved
     // on the host (missing normals -> Ng, instance transform applied)
     const float* vn = S.vn + 9 * (size_t)h.prim;
-    const float b0 = 1.0f - (h.b1 + h.b2);
+    // vTriangle_t (universal mode): intersect never sets data.b0, which keeps
+    // its 0 from intersectData_t's constructor (triangle.cc:365-385, 409)
+    const float b0 = S.uni ? 0.0f : 1.0f - (h.b1 + h.b2);
     sp.N = vnormalize(vadd(vadd(vmul(b0, ld3(vn)), vmul(h.b1, ld3(vn + 3))), vmul(h.b2, ld3(vn + 6))));
   }
   create_cs(sp.N, sp.NU, sp.NV);
@@ -2906,12 +2932,14 @@ int refill_min() {
 template <bool CLOSEST>
 void enqueue_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* idx, RayCount n, yk_hit* hits,
                    uint8_t* occ, unsigned long long* work, unsigned long long* acc, hipEvent_t ev0, hipEvent_t ev1) {
-  const long long grid = (long long)d->cus * (d->big_leaves ? d->per_cu_big[CLOSEST] : d->per_cu[CLOSEST]);
+  const long long per_cu = d->big_leaves ? d->per_cu_big[CLOSEST] : d->per_cu[CLOSEST];
+  const long long grid = (long long)d->cus * per_cu;
   const int ovf_depth = std::max(1, stack_depth(d) - kStackLds);
   P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
   if (ev0) HIPCHK(hipEventRecord(ev0, P.stream));
   auto kern = CLOSEST ? (d->big_leaves ? k_trace_closest_big : k_trace_closest)
-                      : (d->big_leaves ? k_trace_shadow_big : k_trace_shadow);
+                      : (d->S.uni ? (d->big_leaves ? k_trace_shadow_big_uni : k_trace_shadow_uni)
+                                  : (d->big_leaves ? k_trace_shadow_big : k_trace_shadow));
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays, idx, n, hits, occ, work, acc,
                      P.ovf.p, ovf_depth, refill_min());
   HIPCHK(hipGetLastError());
@@ -3178,6 +3206,7 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   std::memcpy(d->S.bound, S.tree.bound, sizeof d->S.bound);
   d->S.nlights = (int)S.light_states.size();
   d->S.nnodes = (unsigned)nn;
+  d->S.uni = S.mode == YK_MODE_UNIVERSAL ? 1 : 0;
   {
     uint32_t max_refs = 0;
     for (size_t i = 0; i < nn; ++i)

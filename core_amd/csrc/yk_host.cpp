@@ -115,6 +115,26 @@ int yk_scene_set_mesh_normals(yk_scene* s, int32_t obj_id, const float* normals,
   YK_GUARD_END
 }
 
+int yk_scene_set_mode(yk_scene* s, int32_t mode) {
+  if (!s || (mode != YK_MODE_TRIANGLE && mode != YK_MODE_UNIVERSAL))
+    return set_error(YK_ERR_ARG, "yk_scene_set_mode: bad arguments");
+  s->s.mode = mode;
+  s->s.built = false;
+  return YK_OK;
+}
+
+int yk_scene_set_mesh_type(yk_scene* s, int32_t obj_id, int32_t type) {
+  if (!s || obj_id < 1 || obj_id > (int32_t)s->s.meshes.size())
+    return set_error(YK_ERR_ARG, "yk_scene_set_mesh_type: bad object id");
+  if (type != YK_MESH_TRIM && type != YK_MESH_VTRIM)
+    return set_error(YK_ERR_UNSUPPORTED, "yk_scene_set_mesh_type: only TRIM and VTRIM meshes (MTRIM bezier is not on the path)");
+  yk::Mesh& m = s->s.meshes[obj_id - 1];
+  if (m.instance_of >= 0) return set_error(YK_ERR_ARG, "yk_scene_set_mesh_type: object is an instance");
+  m.type = type;
+  s->s.built = false;
+  return YK_OK;
+}
+
 int yk_scene_set_mesh_base(yk_scene* s, int32_t obj_id) {
   if (!s || obj_id < 1 || obj_id > (int32_t)s->s.meshes.size())
     return set_error(YK_ERR_ARG, "yk_scene_set_mesh_base: bad object id");
@@ -247,6 +267,10 @@ int yk_scene_get_camera_state(const yk_scene* s, yk_camera_state* out) {
 
 int yk_scene_build(yk_scene* s) {
   if (!s) return set_error(YK_ERR_ARG, "yk_scene_build: NULL scene");
+  if (s->s.mode == YK_MODE_UNIVERSAL)
+    for (const yk::Mesh& m : s->s.meshes)
+      if (m.instance_of >= 0)  // scene_t::addInstance refuses outside triangle mode (scene.cc:985)
+        return set_error(YK_ERR_UNSUPPORTED, "yk_scene_build: universal mode has no instances");
   YK_GUARD_BEGIN
   s->s.finalize();
   return YK_OK;
@@ -274,6 +298,7 @@ int yk_scene_info_get(const yk_scene* s, yk_scene_info* o) {
     std::memcpy(o->bound, S.tree.bound, sizeof o->bound);
     o->build_seconds = S.build_seconds;
   }
+  o->mode = S.mode;
   return YK_OK;
 }
 

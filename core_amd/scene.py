@@ -68,6 +68,14 @@ class Scene:
                                            strand_end, strand_shape, C.byref(oid)))
         return oid.value
 
+    def set_mode(self, mode):
+        """scene_t::setMode: A.YK_MODE_TRIANGLE or A.YK_MODE_UNIVERSAL"""
+        A.check(A.lib().yk_scene_set_mode(self._p, mode))
+
+    def set_mesh_type(self, obj_id, type_):
+        """startTriMesh's mesh type: A.YK_MESH_TRIM or A.YK_MESH_VTRIM"""
+        A.check(A.lib().yk_scene_set_mesh_type(self._p, obj_id, type_))
+
     def set_mesh_base(self, obj_id):
         """Mark a mesh as an instancing base (not traced itself)."""
         A.check(A.lib().yk_scene_set_mesh_base(self._p, obj_id))

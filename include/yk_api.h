@@ -170,6 +170,7 @@ typedef struct yk_scene_info {
   int32_t inodes, leaves, empty_leaves, leaf_refs, depth_limit_leaves, bad_split_leaves;
   float bound[6];
   double build_seconds;
+  int32_t mode; /* YK_MODE_* of the built scene */
 } yk_scene_info;
 
 typedef struct yk_stats {
@@ -213,6 +214,19 @@ int yk_scene_set_mesh_normals(yk_scene* s, int32_t obj_id, const float* normals,
  * (strand_start/end/shape) and vertex arithmetic. */
 int yk_scene_add_curve(yk_scene* s, const float* points, int32_t npoints, int32_t material, float strand_start,
                        float strand_end, float strand_shape, int32_t* obj_id_out);
+/* Scene mode (scene_t::setMode, xmlparser.cc:282-283; scene_t's default is
+ * universal). YK_MODE_TRIANGLE: the tree holds the TRIM meshes and instances
+ * (triKdTree_t); YK_MODE_UNIVERSAL: it holds the VTRIM meshes
+ * (kdTree_t<primitive_t> over vTriangle_t, scene.cc:791-819), every one
+ * whatever its visibility, whose any-hit test accepts t > tmin of the shifted
+ * shadow ray (ray_kdtree.cc:936) and whose smooth shading weighs the first
+ * vertex normal by intersectData_t::b0 = 0 (vTriangle_t::intersect never sets
+ * it, triangle.cc:365-410) with normal index 0 meaning "none". */
+enum { YK_MODE_TRIANGLE = 0, YK_MODE_UNIVERSAL = 1 };
+int yk_scene_set_mode(yk_scene* s, int32_t mode);
+/* the mesh type startTriMesh was given (object3d.h: TRIM 0, VTRIM 1) */
+enum { YK_MESH_TRIM = 0, YK_MESH_VTRIM = 1 };
+int yk_scene_set_mesh_type(yk_scene* s, int32_t obj_id, int32_t type);
 /* mark a mesh as an instancing base: not traced itself (objData_t BASEMESH,
  * scene_t::update skips isBaseObject(), scene.cc:764) */
 int yk_scene_set_mesh_base(yk_scene* s, int32_t obj_id);

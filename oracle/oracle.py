@@ -49,6 +49,7 @@ def lib():
         L.orc_shadow_ts.argtypes = [vp, C.c_int64, C.c_int32, vp, vp, vp]
         L.orc_point_gather.argtypes = [vp, C.c_int32, vp, C.c_int32, vp, vp, vp]
         L.orc_point_nearest.argtypes = [vp, vp, C.c_int32, vp, vp, C.c_float]
+        L.orc_set_mode.argtypes = [C.c_int]
         L.orc_film_table.restype = C.c_float
         L.orc_film_table.argtypes = [vp, vp]
         _lib = L
@@ -74,6 +75,7 @@ class Oracle:
         self._cam = scene.camera()
         self._nmats, self._nlights = len(mats), len(lights)
         self.instanced = bool(getattr(scene, "instanced", False))
+        self._mode = scene.info().mode
         bg = scene.background()
         self._bg = None if bg is None else (C.c_float * 3)(*bg)
         self._activate()
@@ -90,6 +92,7 @@ class Oracle:
         # instanced / smooth scenes: the geometric normals and vertex normals
         # of the host flattening (checked separately by tests/test_instances.py)
         lib().orc_set_background(None if self._bg is None else C.addressof(self._bg))
+        lib().orc_set_mode(self._mode)
         if e["tri_smooth"].any() or self.instanced:
             lib().orc_set_shading(e["tri_normal"].ctypes.data, e["tri_smooth"].ctypes.data,
                                   e["tri_vnormal"].ctypes.data)

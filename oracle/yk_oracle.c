@@ -279,6 +279,7 @@ typedef struct {
   v3 dof_rt, dof_up; /* depth of field (perspectiveCam_t::setAxis) */
   float lens_ls[16];  /* polygon bokeh corners (perspectiveCam_t ctor) */
   v3 near_p, far_p;
+  int universal; /* scene mode universal: kdTree_t<primitive_t> over vTriangle_t */
 } oscene;
 
 static oscene G;
@@ -346,7 +347,8 @@ typedef struct { int node; float t; v3 pb; int prev; } kdstack;
 
 /* descend-and-leaf loop shared by Intersect / IntersectS (kdtree.cc:675-947).
  * closest=1: accept t<Z && t>=tmin, stop when hit && Z<=exit.t
- * closest=0: return at the first t<dist && t>=0 */
+ * closest=0: return at the first t<dist && t>=0 (universal mode: t > tmin,
+ * ray_kdtree.cc:936) */
 static int kd_traverse(v3 from, v3 dir, float tmin, float dist, int closest, int* hprim, float* Z,
                        float* hb1, float* hb2, uint64_t* nnodes, uint64_t* ntris) {
   float a, b, t, t_hit, b1, b2;
@@ -410,7 +412,7 @@ static int kd_traverse(v3 from, v3 dir, float tmin, float dist, int closest, int
             cb2 = b2;
             hit = 1;
           }
-        } else if (t_hit < dist && t_hit >= 0.f) {
+        } else if (t_hit < dist && (G.universal ? t_hit > tmin : t_hit >= 0.f)) {
           *hprim = p;
           return 1;
         }
@@ -460,7 +462,7 @@ static int scene_intersect(v3 from, v3 dir, float tmin, float* tmax, surfpt* sp)
     /* triangle.cc:19-28 (instances 185-194): u*va + v*vb + w*vc, normalized;
      * u = data.b0, which intersect computes as 1-(u+v) (compiled form) */
     const float* n = G.vn + 9 * (size_t)prim;
-    float b0 = 1.0f - (b1 + b2);
+    float b0 = G.universal ? 0.0f : 1.0f - (b1 + b2); /* vTriangle_t: intersectData_t::b0 stays 0 */
     v3 va = V(n[0], n[1], n[2]), vb = V(n[3], n[4], n[5]), vc = V(n[6], n[7], n[8]);
     sp->N = vnormalize(vadd(vadd(vmul(b0, va), vmul(b1, vb)), vmul(b2, vc)));
   }
@@ -477,7 +479,7 @@ static int scene_shadowed(v3 from, v3 dir, float tmin, float tmax) {
   v3 f = vadd(from, vmul(tmin, dir));
   float dis = (tmax < 0) ? INFINITY : tmax - 2.0f * tmin;
   int prim;
-  return kd_traverse(f, dir, 0.f, dis, 0, &prim, NULL, NULL, NULL, &g_nodes_s, &g_tris_s);
+  return kd_traverse(f, dir, tmin, dis, 0, &prim, NULL, NULL, NULL, &g_nodes_s, &g_tris_s);
 }
 
 /* transparent shadows: mcIntegrator_t::trShad / sDepth (set per render) */
@@ -563,7 +565,7 @@ static int scene_shadowed_ts(v3 from0, v3 dir, float tmin, float tmax, int maxDe
       sp.N = sp.Ng;
       if (G.smooth && G.smooth[p]) {
         const float* nv = G.vn + 9 * (size_t)p;
-        float b0 = 1.0f - (b1 + b2);
+        float b0 = G.universal ? 0.0f : 1.0f - (b1 + b2); /* vTriangle_t: intersectData_t::b0 stays 0 */
         sp.N = vnormalize(vadd(vadd(vmul(b0, V(nv[0], nv[1], nv[2])), vmul(b1, V(nv[3], nv[4], nv[5]))),
                                vmul(b2, V(nv[6], nv[7], nv[8]))));
       }
@@ -2501,6 +2503,12 @@ static int render_tiles(const yk_render_params* P, int shard, int nshards, float
     counts[4] = g_nodes_s; counts[5] = g_tris_s;
   }
   free(F.acc);
+  return 0;
+}
+
+/* scene mode of the loaded scene (YK_MODE_*); call after orc_load */
+int orc_set_mode(int mode) {
+  G.universal = mode == YK_MODE_UNIVERSAL;
   return 0;
 }
 

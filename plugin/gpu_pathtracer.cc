@@ -65,6 +65,19 @@ grant<Tag, P> grant<Tag, P>::instance;
   };                                                    \
   template struct grant<name, &cls::member>;
 YK_MEMBER(SceneMeshes, scene_t, std::map<objID_t YK_COMMA objData_t>, meshes)
+YK_MEMBER(SceneObjects, scene_t, std::map<objID_t YK_COMMA object3d_t*>, objects)
+YK_MEMBER(SceneMode, scene_t, int, mode)
+YK_MEMBER(MObjTris, meshObject_t, std::vector<vTriangle_t>, triangles)
+YK_MEMBER(MObjBsTris, meshObject_t, std::vector<bsTriangle_t>, s_triangles)
+YK_MEMBER(MObjPoints, meshObject_t, std::vector<point3d_t>, points)
+YK_MEMBER(MObjNormals, meshObject_t, std::vector<normal_t>, normals)
+YK_MEMBER(MObjSmooth, meshObject_t, bool, is_smooth)
+YK_MEMBER(VTriPa, vTriangle_t, int, pa)
+YK_MEMBER(VTriPb, vTriangle_t, int, pb)
+YK_MEMBER(VTriPc, vTriangle_t, int, pc)
+YK_MEMBER(VTriNa, vTriangle_t, int, na)
+YK_MEMBER(VTriNb, vTriangle_t, int, nb)
+YK_MEMBER(VTriNc, vTriangle_t, int, nc)
 YK_MEMBER(TriPa, triangle_t, int, pa)
 YK_MEMBER(TriPb, triangle_t, int, pb)
 YK_MEMBER(TriPc, triangle_t, int, pc)
@@ -175,9 +188,53 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     // yk object ids of each reference mesh (one per material run), so that
     // instances (scene_t::addInstance, scene.cc:983-1008) can name their base
     std::map<const triangleObject_t*, std::vector<int32_t>> yk_ids;
+    // universal mode (scene_t::mode 1): the tree holds the VTRIM meshes'
+    // vTriangle_t prims, every one whatever its visibility (scene.cc:791-819)
+    const bool universal = GET(*scene, SceneMode) != 0;
+    if (universal) {
+      if (yk_scene_set_mode(ys, YK_MODE_UNIVERSAL) != YK_OK) return fail();
+      if (!GET(*scene, SceneObjects).empty()) return unsupported("non-mesh primitives are not on the GPU path");
+      for (auto& kv : meshes) {
+        objData_t& dat = kv.second;
+        if (dat.type == TRIM) continue;  // not in the universal tree
+        if (dat.type != VTRIM || !GET(*dat.mobj, MObjBsTris).empty())
+          return unsupported("bezier (MTRIM) meshes are not on the GPU path");
+        const std::vector<vTriangle_t>& tris = GET(*dat.mobj, MObjTris);
+        // points keep their orco interleaved (pa + 1): faces index them as stored
+        const std::vector<point3d_t>& pts = GET(*dat.mobj, MObjPoints);
+        std::vector<float> xyz(3 * pts.size());
+        for (size_t i = 0; i < pts.size(); ++i) put3(&xyz[3 * i], pts[i].x, pts[i].y, pts[i].z);
+        const std::vector<normal_t>& nrm = GET(*dat.mobj, MObjNormals);
+        std::vector<float> nxyz(3 * nrm.size());
+        for (size_t i = 0; i < nrm.size(); ++i) put3(&nxyz[3 * i], nrm[i].x, nrm[i].y, nrm[i].z);
+        for (size_t a = 0; a < tris.size();) {  // one yk mesh per run of prims with the same material
+          const material_t* m = tris[a].getMaterial();
+          size_t b = a;
+          std::vector<int32_t> faces, fnrm;
+          while (b < tris.size() && tris[b].getMaterial() == m) {
+            faces.push_back(GET(tris[b], VTriPa));
+            faces.push_back(GET(tris[b], VTriPb));
+            faces.push_back(GET(tris[b], VTriPc));
+            for (int k : {GET(tris[b], VTriNa), GET(tris[b], VTriNb), GET(tris[b], VTriNc)})
+              fnrm.push_back(k >= 0 && k < (int)nrm.size() ? k : -1);
+            ++b;
+          }
+          int32_t mid, oid;
+          if (!material_id(m, mat_ids, mid)) return false;
+          if (yk_scene_add_mesh(ys, xyz.data(), (int32_t)pts.size(), faces.data(), (int32_t)(faces.size() / 3), mid,
+                                &oid) != YK_OK ||
+              yk_scene_set_mesh_type(ys, oid, YK_MESH_VTRIM) != YK_OK)
+            return fail();
+          if (GET(*dat.mobj, MObjSmooth) &&
+              yk_scene_set_mesh_normals(ys, oid, nxyz.data(), (int32_t)nrm.size(), fnrm.data(), YK_MESH_SMOOTH) != YK_OK)
+            return fail();
+          a = b;
+        }
+      }
+    }
     for (auto& kv : meshes) {
       objData_t& dat = kv.second;
-      if (!dat.obj->isVisible() || dat.type != TRIM) continue;
+      if (universal || !dat.obj->isVisible() || dat.type != TRIM) continue;
       if (triangleObjectInstance_t* inst = dynamic_cast<triangleObjectInstance_t*>(dat.obj)) {
         // prims of an instance = the base's prims in order: instance each run
         const matrix4x4_t& M = GET(*inst, InstToWorld);

@@ -57,12 +57,11 @@ def main():
     b2 = bounce_rays(P1, N1, gen)  # second-bounce rays: incoherent origins
     s2 = shadow_rays(P1, gen)      # shadow rays from the first bounce's hits
     out = {"spp": args.spp}
-    for name, rays, closest in (("shadow_bounce", s2, False), ("bounce2", b2, True)):
+    sh1 = shadow_rays(P, gen)
+    for name, rays, closest in (("shadow_bounce", s2, False), ("bounce2", b2, True), ("shadow_camera", sh1, False)):
         o = morton_order(rays[:, 0:3], lo, hi)
         out[name] = {"rays": len(rays), "queue_order": rate(dev, rays, closest),
                      "morton_sorted": rate(dev, rays[o].contiguous(), closest)}
-    sh1 = shadow_rays(P, gen)
-    out["shadow_camera"] = {"rays": len(sh1), "queue_order": rate(dev, sh1, False)}
     print(json.dumps(out), flush=True)
     dev.close()
 
