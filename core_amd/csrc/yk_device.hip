@@ -1370,7 +1370,7 @@ __device__ __forceinline__ bool dirac_illum(const DLight& L, v3 P, v3& ldir, flo
 // shading at 1024 threads 2038 -> 2075 Mrays/s (k_shade_primary at 512:
 // 2744 against 2811); the photon / final-gather kernels best at 512
 // (1261 -> 1274; 1024: 1240).
-#define YK_SHADE_BLOCK 1024
+#define YK_SHADE_BLOCK 1024  // round 3: 256 / 512 measured C2 7785-7977 / 7679-7827 against 7932-8090
 #define YK_APPEND_BLOCK 512
 // Reserves m_s shadow-queue and m_b bounce-queue entries with ONE returning
 // atomic per wave: the counter word holds (bounce count << 32) | shadow
