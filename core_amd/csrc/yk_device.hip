@@ -1586,7 +1586,7 @@ __global__ void __launch_bounds__(256) k_camera(TileList TL, Batch B, RenderCons
   const float px = (float)j + dx, py = (float)i + dy;
   const v3 vr = ld3(c_cam.vright), vu = ld3(c_cam.vup), vt = ld3(c_cam.vto), cz = ld3(c_cam.camZ);
   v3 d = vadd(vadd(vmul(px, vr), vmul(py, vu)), vt);
-  d = vnormalize(d);
+  d = vnormalize_cam(d);
   const v3 from = ld3(c_cam.pos);
   yk_ray r;
   r.from[0] = from.x;
@@ -1616,7 +1616,7 @@ __global__ void __launch_bounds__(256) k_camera(TileList TL, Batch B, RenderCons
     lens_uv(lu, lv, u, v);
     const v3 LI = vadd(vmul(u, ld3(c_cam.dof_rt)), vmul(v, ld3(c_cam.dof_up)));
     const v3 f2 = vadd(from, LI);
-    const v3 d2 = vnormalize(vsub(vmul(c_cam.dof_distance, d), LI));
+    const v3 d2 = vnormalize_cam(vsub(vmul(c_cam.dof_distance, d), LI));
     r.from[0] = f2.x;
     r.from[1] = f2.y;
     r.from[2] = f2.z;

@@ -201,6 +201,20 @@ __device__ __forceinline__ void shirley_disk(float r1, float r2, float& u, float
 }
 
 // vector3d_t::normalize, vector3d.h:249-260
+// The camera ray's normalize() in the survey build's shootRay sums the
+// squared length as (y*y + z*z) + x*x (pinned by the reference's float crop:
+// every value bit-identical with this form, 11 % off by 1-2 ulp with the
+// source order). The other normalize() sites keep the source order.
+__device__ __forceinline__ v3 vnormalize_cam(v3 a) {
+  float len = (a.y * a.y + a.z * a.z) + a.x * a.x;
+  if (len != 0.f) {
+    len = 1.0f / sqrtf(len);
+    a.x *= len;
+    a.y *= len;
+    a.z *= len;
+  }
+  return a;
+}
 __device__ __forceinline__ v3 vnormalize(v3 a) {
   float len = a.x * a.x + a.y * a.y + a.z * a.z;
   if (len != 0.f) {

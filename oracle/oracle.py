@@ -52,6 +52,7 @@ def lib():
         L.orc_set_mode.argtypes = [C.c_int]
         L.orc_film_table.restype = C.c_float
         L.orc_film_table.argtypes = [vp, vp]
+        L.orc_debug_pixel.argtypes = [C.c_int32, C.c_int32, vp, C.c_int32]
         _lib = L
     return _lib
 
@@ -97,6 +98,18 @@ class Oracle:
             lib().orc_set_shading(e["tri_normal"].ctypes.data, e["tri_smooth"].ctypes.data,
                                   e["tri_vnormal"].ctypes.data)
         _active = self
+
+    def render_logged(self, params, x, y, cap=100000):
+        """render() plus the ray log of pixel (x, y): rows of (kind 0 closest /
+        1 shadow, sample, from xyz, dir xyz, tmin, tmax, prim or -1, t)."""
+        buf = np.zeros((cap, 12), np.float32)
+        lib().orc_debug_pixel(x, y, buf.ctypes.data, cap)
+        try:
+            out = self.render(params)
+            n = lib().orc_debug_count()
+        finally:
+            lib().orc_debug_pixel(-1, -1, None, 0)
+        return out, buf[:n].copy()
 
     def render(self, params):
         self._activate()

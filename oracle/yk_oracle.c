@@ -448,13 +448,39 @@ static void createCS(v3 N, v3* u, v3* v) {
   }
 }
 
+/* debug ray log (tests / tools only): every ray query of one pixel, 12
+ * floats each: kind (0 closest, 1 shadow), sample, from, dir, tmin, tmax,
+ * result (prim or occluded), t */
+static int g_dbg_x = -1, g_dbg_y = -1;
+static __thread int g_dbg_on, g_dbg_s;
+static float* g_dbg_buf;
+static int g_dbg_cap, g_dbg_n;
+static void dbg_log(int kind, v3 from, v3 dir, float tmin, float tmax, float res, float t) {
+  if (!g_dbg_on || g_dbg_n >= g_dbg_cap) return;
+  float* r = g_dbg_buf + 12 * (size_t)g_dbg_n++;
+  r[0] = (float)kind; r[1] = (float)g_dbg_s;
+  r[2] = from.x; r[3] = from.y; r[4] = from.z; r[5] = dir.x; r[6] = dir.y; r[7] = dir.z;
+  r[8] = tmin; r[9] = tmax; r[10] = res; r[11] = t;
+}
+static const v3 kZero3 = {0, 0, 0};
+#define DBG_CMP(tag, val) dbg_log(3, kZero3, kZero3, 0.f, 0.f, (float)(tag), (val))
+int orc_debug_pixel(int32_t x, int32_t y, float* buf, int32_t cap) {
+  g_dbg_x = x; g_dbg_y = y; g_dbg_buf = buf; g_dbg_cap = buf ? cap : 0; g_dbg_n = 0;
+  return 0;
+}
+int orc_debug_count(void) { return g_dbg_n; }
+
 /* scene_t::intersect (scene.cc:852-879) + triangle_t::getSurface
  * (triangle.cc:12-108, flat-shaded subset). Returns hit, sets ray tmax. */
 static int scene_intersect(v3 from, v3 dir, float tmin, float* tmax, surfpt* sp) {
   g_nclosest++;
   float dis = (*tmax < 0) ? INFINITY : *tmax, Z, b1 = 0, b2 = 0;
   int prim = -1;
-  if (!kd_traverse(from, dir, tmin, dis, 1, &prim, &Z, &b1, &b2, &g_nodes_c, &g_tris_c)) return 0;
+  if (!kd_traverse(from, dir, tmin, dis, 1, &prim, &Z, &b1, &b2, &g_nodes_c, &g_tris_c)) {
+    dbg_log(0, from, dir, tmin, *tmax, -1.f, 0.f);
+    return 0;
+  }
+  dbg_log(0, from, dir, tmin, *tmax, (float)prim, Z);
   sp->P = vadd(from, vmul(Z, dir));
   sp->Ng = G.ng[prim];
   sp->N = sp->Ng;
@@ -478,8 +504,10 @@ static int scene_shadowed(v3 from, v3 dir, float tmin, float tmax) {
   g_nshadow++;
   v3 f = vadd(from, vmul(tmin, dir));
   float dis = (tmax < 0) ? INFINITY : tmax - 2.0f * tmin;
-  int prim;
-  return kd_traverse(f, dir, tmin, dis, 0, &prim, NULL, NULL, NULL, &g_nodes_s, &g_tris_s);
+  int prim = -1;
+  int occ = kd_traverse(f, dir, tmin, dis, 0, &prim, NULL, NULL, NULL, &g_nodes_s, &g_tris_s);
+  dbg_log(1, from, dir, tmin, tmax, occ ? (float)prim : -1.f, 0.f);
+  return occ;
 }
 
 /* transparent shadows: mcIntegrator_t::trShad / sDepth (set per render) */
@@ -657,6 +685,7 @@ static void lens_uv(float r1, float r2, float* u, float* v) {
   }
 }
 
+static v3 vnormalize_cam(v3 a);
 /* shootRay's aperture branch, perspectiveCamera.cc:139-147: the lens point
  * (lu, lv) moves the origin and re-aims at the focal plane; tmin / tmax stay */
 static void camera_lens(float lu, float lv, v3* from, v3* dir) {
@@ -665,14 +694,26 @@ static void camera_lens(float lu, float lv, v3* from, v3* dir) {
   lens_uv(lu, lv, &u, &v);
   v3 LI = vadd(vmul(u, G.dof_rt), vmul(v, G.dof_up));
   *from = vadd(*from, LI);
-  *dir = vnormalize(vsub(vmul(G.cam.dof_distance, *dir), LI));
+  *dir = vnormalize_cam(vsub(vmul(G.cam.dof_distance, *dir), LI)); /* same inlined normalize (unpinned) */
 }
 
 /* perspectiveCam_t::shootRay, perspectiveCamera.cc:127-138 (DOF: camera_lens) */
+/* the camera ray's normalize() as the survey build compiled it in shootRay:
+ * the squared length summed as (y*y + z*z) + x*x (pinned: with the source
+ * order 11 % of the Cornell float crop's values differed by 1-2 ulp and two
+ * pixels by 1e-4; with this form all 12,288 are bit-identical) */
+static v3 vnormalize_cam(v3 a) {
+  float len = (a.y * a.y + a.z * a.z) + a.x * a.x;
+  if (len != 0) {
+    len = 1.0f / sqrtf(len);
+    a.x *= len; a.y *= len; a.z *= len;
+  }
+  return a;
+}
 static void camera_ray(float px, float py, v3* from, v3* dir, float* tmin, float* tmax) {
   *from = G.cam_pos;
   v3 d = vadd(vadd(vmul(px, G.vright), vmul(py, G.vup)), G.vto);
-  d = vnormalize(d);
+  d = vnormalize_cam(d);
   *dir = d;
   /* ray_plane_intersection, geometry.h:33-36 */
   *tmin = vdot(G.camZ, vsub(G.near_p, *from)) / vdot(d, G.camZ);
@@ -795,6 +836,7 @@ static col3 sd_eval(const sdmat* M, const surfpt* sp, v3 wo, v3 wl, unsigned bsd
   float Kr = sd_fresnel(M, wo, N);
   float mT = (1.f - Kr * M->comp[0]) * (1.f - M->comp[1]);
   if (cos_Ng_wo * cos_Ng_wl < 0.f && M->is_translucent) return cscale(mT * M->comp[2], M->diff);
+  DBG_CMP(3, vdot(wl, N));
   if (vdot(wl, N) < 0.0f) return C(0, 0, 0);
   float mD = ((1.f - M->comp[2]) * M->comp[3]) * mT;
   return cscale(mD, M->diff);
@@ -884,6 +926,7 @@ static col3 sd_sample(const sdmat* M, const surfpt* sp, v3 wo, v3* wi, float s1i
       break;
     default:
       w = sample_cos_hemisphere(N, sp->NU, sp->NV, s1, s2in);
+      DBG_CMP(4, cos_Ng_wo * vdot(sp->Ng, w));
       if (cos_Ng_wo * vdot(sp->Ng, w) > 0) sc = cscale(a[3], M->diff);
       *pdf = fabsf(vdot(N, w)) * width[pick];
       break;
@@ -1078,6 +1121,7 @@ static int al_illum_sample(const struct arealight* A, v3 P, float s1, float s2, 
   float id = 1.f / dist;
   ldir = V(ldir.x * id, ldir.y * id, ldir.z * id);
   float cos_angle = vdot(ldir, A->fnormal);
+  DBG_CMP(1, cos_angle);
   if (cos_angle <= 0) return 0;
   *tmax = dist;
   *ldir_out = ldir;
@@ -1089,11 +1133,16 @@ static int al_illum_sample(const struct arealight* A, v3 P, float s1, float s2, 
 /* areaLight_t::intersect, arealight.cc:138-154 */
 static int al_intersect(const struct arealight* A, v3 from, v3 dir, float* t, col3* col, float* ipdf) {
   float cos_angle = vdot(dir, A->fnormal);
+  DBG_CMP(5, cos_angle);
   if (cos_angle <= 0) return 0;
   if (!tri_isect_pts(A->corner, A->c2, A->c3, from, dir, t)) {
-    if (!tri_isect_pts(A->corner, A->c3, A->c4, from, dir, t)) return 0;
+    if (!tri_isect_pts(A->corner, A->c3, A->c4, from, dir, t)) {
+      dbg_log(2, from, dir, 0.f, -1.f, 0.f, 0.f);
+      return 0;
+    }
   }
   if (!(*t > 1.0e-10f)) return 0;
+  dbg_log(2, from, dir, 0.f, -1.f, 1.f, *t);
   *col = A->color;
   *ipdf = (float)((double)((1.f / (*t * *t)) * A->area * cos_angle) * M_1_PI_D);
   return 1;
@@ -1181,6 +1230,7 @@ static col3 do_light_estimation(rstate* st, int li, const surfpt* sp, v3 wo, uns
       col3 scol;
       int shadowed = g_trshad ? scene_shadowed_ts(sp->P, ldir, SHADOW_BIAS, ltmax, g_sdepth, &scol)
                               : scene_shadowed(sp->P, ldir, SHADOW_BIAS, ltmax);
+      DBG_CMP(6, lpdf / 1e-6f - 1.f);
       if (!shadowed && lpdf > 1e-6f) {
         if (g_trshad) lcol = cmul(lcol, scol); /* ls.col *= scol */
         col3 surf = sd_eval(M, sp, wo, ldir, BSDF_ALL);
@@ -1188,10 +1238,12 @@ static col3 do_light_estimation(rstate* st, int li, const surfpt* sp, v3 wo, uns
         /* compiled form: ((surf*lcol) * (|N.l| * (1/pdf))) [* w] */
         float k = fabsf(vdot(sp->N, ldir)) * (1.0f / lpdf);
         col3 sl = cmul(surf, lcol);
+        DBG_CMP(7, mPdf / 1e-6f - 1.f);
         if (mPdf > 1e-6f) {
           float l2 = lpdf * lpdf, m2 = mPdf * mPdf;
           float w = l2 / (l2 + m2);
           ccol = cadd(ccol, C((sl.r * k) * w, (sl.g * k) * w, (sl.b * k) * w));
+          dbg_log(5, V((sl.r * k) * w, (sl.g * k) * w, (sl.b * k) * w), V(w, lpdf, mPdf), 0.f, 0.f, (float)i, 0.f);
         } else {
           ccol = cadd(ccol, C(sl.r * k, sl.g * k, sl.b * k));
         }
@@ -1213,10 +1265,12 @@ static col3 do_light_estimation(rstate* st, int li, const surfpt* sp, v3 wo, uns
                           NULL);
     float bt, lightPdf;
     col3 lcol;
+    DBG_CMP(8, spdf / 1e-6f - 1.f);
     if (spdf > 1e-6f && al_intersect(A, sp->P, bdir, &bt, &lcol, &lightPdf)) {
       col3 scol;
       int shadowed = g_trshad ? scene_shadowed_ts(sp->P, bdir, MIN_RAYDIST, bt, g_sdepth, &scol)
                               : scene_shadowed(sp->P, bdir, MIN_RAYDIST, bt);
+      DBG_CMP(9, lightPdf / 1e-6f - 1.f);
       if (!shadowed && lightPdf > 1e-6f) {
         if (g_trshad) lcol = cmul(lcol, scol);
         float lPdf = 1.f / lightPdf;
@@ -1228,6 +1282,7 @@ static col3 do_light_estimation(rstate* st, int li, const surfpt* sp, v3 wo, uns
         ccol2 = cadd(ccol2, C(((surf.r * lcol.r) * w) * W, ((surf.g * lcol.g) * w) * W, ((surf.b * lcol.b) * w) * W));
 #else
         ccol2 = cadd(ccol2, C(((surf.r * W) * lcol.r) * w, ((surf.g * W) * lcol.g) * w, (surf.b * W) * (w * lcol.b)));
+        dbg_log(6, V(((surf.r * W) * lcol.r) * w, ((surf.g * W) * lcol.g) * w, (surf.b * W) * (w * lcol.b)), V(w, lPdf, spdf), 0.f, 0.f, (float)i, 0.f);
 #endif
       }
     }
@@ -1338,6 +1393,7 @@ static rgba pt_integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir,
         lcol = estimate_one_direct(st, &hit, pwo, (int)offs);
         if (matBSDFs & BSDF_EMIT) lcol = cadd(lcol, mat_emit(pm, &hit, pwo, st->includeLights));
         pathCol = cadd(pathCol, cmul(lcol, throughput));
+        { col3 tt = cmul(lcol, throughput); dbg_log(4, V(tt.r, tt.g, tt.b), V(throughput.r, throughput.g, throughput.b), 0.f, 0.f, 0.f, 0.f); }
         int caustic = 0;
         for (int depth = 1; depth < P->bounces; ++depth) {
           int d4 = 4 * depth;
@@ -1365,6 +1421,7 @@ static rgba pt_integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir,
           /* "matBSDFs & (BSDF_EMIT && caustic)" == matBSDFs & BSDF_SPECULAR when caustic */
           if (caustic && (matBSDFs & BSDF_SPECULAR)) lcol = cadd(lcol, mat_emit(pm, &hit, pwo, st->includeLights));
           pathCol = cadd(pathCol, cmul(lcol, throughput));
+          { col3 tt = cmul(lcol, throughput); dbg_log(4, V(tt.r, tt.g, tt.b), V(throughput.r, throughput.g, throughput.b), 0.f, 0.f, (float)depth, 0.f); }
         }
       }
       float ns = (float)nSamples;
@@ -2450,6 +2507,7 @@ static int render_tiles(const yk_render_params* P, int shard, int nshards, float
           for (int j = X; j < X + W; ++j) {
             if (adaptive && !flags[(size_t)(i - F.cy0) * F.w + (j - F.cx0)]) continue; /* doMoreSamples */
             rstate st;
+            g_dbg_on = (i == g_dbg_y && j == g_dbg_x);
             st.samplingOffs = fnv_32a_buf((unsigned)i * fnv_32a_buf((unsigned)j));
             /* lens samples, integrator.cc:248-291 */
             halton halU, halV;
@@ -2461,6 +2519,7 @@ static int render_tiles(const yk_render_params* P, int shard, int nshards, float
             st.raylevel = 0;
             for (int s = 0; s < n; ++s) {
               st.pixelSample = pass_offs + s;
+              g_dbg_s = st.pixelSample;
               float dx = 0.5f, dy = 0.5f;
               if (P->aa_passes > 1) { /* scrambled vdC / Sobol for multipass AA */
                 dx = RI_vdC((unsigned)st.pixelSample, st.samplingOffs);
@@ -2484,6 +2543,7 @@ static int render_tiles(const yk_render_params* P, int shard, int nshards, float
       }
   }
   free(flags);
+  g_dbg_on = 0;
   size_t npx = (size_t)F.w * F.h;
   for (size_t p = 0; p < npx; ++p) {
     float* a = F.acc + 5 * p;

@@ -211,19 +211,18 @@ def _golden_counts():
     return json.load(open(os.path.join(GOLDEN, "counts.json")))
 
 
-@pytest.mark.parametrize("key,scene_args,max_off", [
-    ("cornell_dl_512_4spp_t1", ("cornell_dl", 512, 512, 0, 0), 3),
-    ("cornell_pt_256_16spp_t1", ("cornell_pt", 256, 256, 0, 0), 0),
+@pytest.mark.parametrize("key,scene_args", [
+    ("cornell_dl_512_4spp_t1", ("cornell_dl", 512, 512, 0, 0)),
+    ("cornell_pt_256_16spp_t1", ("cornell_pt", 256, 256, 0, 0)),
 ])
-def test_full_frame_vs_reference_and_oracle(gpu_device, key, scene_args, max_off):
+def test_full_frame_vs_reference_and_oracle(gpu_device, key, scene_args):
     s, p, orc = scene(*scene_args)
     gpu_device.upload(s)
     st = A.yk_stats()
     rgba = gpu_device.render(p, st)
     ref = _golden_counts()[key]
     assert (st.closest_rays, st.shadow_rays) == (ref["closest"], ref["shadow"])
-    d = np.abs(_to8(rgba).astype(int) - _golden(key).astype(int))
-    assert d.max() <= 1 and (d > 0).sum() <= max_off
+    assert (_to8(rgba) == _golden(key)).all()
     rgba_o, _, _ = orc.render(p)
     assert (rgba.view(np.uint32) == rgba_o.view(np.uint32)).all()
 
@@ -237,19 +236,17 @@ def test_bumpy1m_frame_vs_reference_and_oracle(gpu_device):
     assert (st.closest_rays, st.shadow_rays) == (cnt["closest"], cnt["shadow"])
     assert (rgba.view(np.uint32) == rgba_o.view(np.uint32)).all()
     ref = _golden_counts()["bumpy1m_480x270_4spp_t1"]
-    assert abs(st.closest_rays - ref["closest"]) <= 8 and abs(st.shadow_rays - ref["shadow"]) <= 16
-    d = np.abs(_to8(rgba).astype(int) - _golden("bumpy1m_480x270_4spp_t1").astype(int))
-    assert (d == 0).mean() > 0.999
+    assert (st.closest_rays, st.shadow_rays) == (ref["closest"], ref["shadow"])
+    assert (_to8(rgba) == _golden("bumpy1m_480x270_4spp_t1")).all()
 
 
 def test_c2_config_counts_and_frame(gpu_device):
-    """BASELINE configs[1]: Cornell PT 1024^2, 64 spp, 954M rays. Ray counts
-    within the oracle's pinned residual against the reference's fast-math
-    build (measured: 3 closest and 35 shadow rays fewer, <4e-8 of the total;
-    the same compiled-form residual as the 1M-tri frame, DESIGN.md 'Oracle
-    pinning'); the 8-bit frame matches the reference's 8-thread output
-    (whose film differs from the single-thread order by <=1e-7 relative at
-    tile borders) except for rare rounding steps."""
+    """BASELINE configs[1]: Cornell PT 1024^2, 64 spp, 954M rays. The
+    reference's exact ray counts (250,394,892 closest, 703,523,953 shadow), and
+    its 8-bit frame, which it rendered on 8 threads: tiles finishing in another
+    order change the float summation order of the pixels whose filter
+    footprint crosses a tile border (<=1e-7 relative), so a rare
+    value there may sit one 8-bit step away."""
     s, p, _ = scene("cornell_pt", 1024, 1024)
     p = A.yk_render_params.from_buffer_copy(p)
     p.aa_samples = 64
@@ -257,13 +254,11 @@ def test_c2_config_counts_and_frame(gpu_device):
     st = A.yk_stats()
     rgba = gpu_device.render(p, st)
     ref = _golden_counts()["cornell_pt_1024_64spp_t8"]
-    assert abs(st.closest_rays - ref["closest"]) <= 8
-    assert abs(st.shadow_rays - ref["shadow"]) <= 64
+    assert (st.closest_rays, st.shadow_rays) == (ref["closest"], ref["shadow"])
     d = np.abs(_to8(rgba).astype(int) - _golden("cornell_pt_1024_64spp_t8").astype(int))
-    # the ~40 paths of the count residual move a handful of pixels by more
-    # than one 8-bit step; everything else is within one step
-    msg = f"8-bit diff: max {d.max()}, >0: {(d > 0).sum()}, >1: {(d > 1).sum()} of {d.size}"
-    assert (d > 0).mean() < 2e-4 and (d > 1).sum() <= 32 and d.max() <= 8, msg
+    msg = f"8-bit diff: max {d.max()}, >0: {(d > 0).sum()} of {d.size}"
+    print(msg)
+    assert d.max() <= 1 and (d > 0).sum() <= 64, msg
 
 
 def test_object_state_scene_renders_identically(gpu_device):
