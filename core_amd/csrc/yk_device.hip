@@ -1638,11 +1638,24 @@ __device__ __forceinline__ void put_ray(yk_ray& r, v3 f, v3 d, float tmin, float
   r.tmax = tmax;
 }
 
+// A slot's contribution is read only when its SL_ADDS flag is set
+// (resolve_light), so slots without it store the flag alone: on C2 the
+// shading kernels are write-bound (k_shade_bounce writes ~280 B per path
+// vertex) and most MIS-half slots carry no contribution.
+typedef float f3v __attribute__((ext_vector_type(3)));
 __device__ __forceinline__ void put_slot(const Batch& B, long long slot, uint8_t fl, c3 v) {
   B.sl_flags[slot] = fl;
-  B.sl_contrib[3 * slot] = v.r;
-  B.sl_contrib[3 * slot + 1] = v.g;
-  B.sl_contrib[3 * slot + 2] = v.b;
+  if (fl & SL_ADDS) {
+    f3v x;
+    x.x = v.r;
+    x.y = v.g;
+    x.z = v.b;
+    *reinterpret_cast<f3v*>(B.sl_contrib + 3 * slot) = x;
+  }
+}
+__device__ __forceinline__ c3 get_contrib(const Batch& B, long long slot) {
+  const f3v x = *reinterpret_cast<const f3v*>(B.sl_contrib + 3 * slot);
+  return C3(x.x, x.y, x.z);
 }
 __device__ __forceinline__ void put_aux(const Batch& B, long long slot, float a, float b, float c, float d) {
   *reinterpret_cast<float4*>(B.sl_aux + 4 * slot) = make_float4(a, b, c, d);
@@ -1893,7 +1906,7 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) k_shade_primary(DScene S, Batc
 // Contribution of an unoccluded slot under transparent shadows: the light
 // colour times the shadow ray's filter, then the reference's products.
 __device__ __forceinline__ c3 slot_value_ts(const Batch& B, long long slot, int kind, c3 lcol) {
-  const c3 a = C3(B.sl_contrib[3 * slot], B.sl_contrib[3 * slot + 1], B.sl_contrib[3 * slot + 2]);
+  const c3 a = get_contrib(B, slot);
   const float4 x = *reinterpret_cast<const float4*>(B.sl_aux + 4 * slot);
   const c3 sc = C3(B.s_filt[3 * slot], B.s_filt[3 * slot + 1], B.s_filt[3 * slot + 2]);
   if (kind == 0) {  // Dirac: R,G (lcol*surf)*f, B surf*(lcol*f)
@@ -1916,7 +1929,7 @@ __device__ __forceinline__ c3 resolve_light(const Batch& B, long long c, int k0,
     c3 col = C3(0.f, 0.f, 0.f);
     if ((B.sl_flags[slot] & SL_ADDS) && !B.s_occl[slot])
       col = cadd(col, B.ts ? slot_value_ts(B, slot, 0, col)
-                           : C3(B.sl_contrib[3 * slot], B.sl_contrib[3 * slot + 1], B.sl_contrib[3 * slot + 2]));
+                           : get_contrib(B, slot));
     return col;
   }
   const int n = c_lights[li].samples;
@@ -1926,7 +1939,7 @@ __device__ __forceinline__ c3 resolve_light(const Batch& B, long long c, int k0,
     const long long slot = slot_of(B, c, k0 + i);
     if ((B.sl_flags[slot] & SL_ADDS) && !B.s_occl[slot]) {
       const c3 v = B.ts ? slot_value_ts(B, slot, i < n ? 1 : 2, C3(c_lights[li].color[0], c_lights[li].color[1], c_lights[li].color[2]))
-                        : C3(B.sl_contrib[3 * slot], B.sl_contrib[3 * slot + 1], B.sl_contrib[3 * slot + 2]);
+                        : get_contrib(B, slot);
       if (i < n) ccol = cadd(ccol, v);
       else ccol2 = cadd(ccol2, v);
     }

@@ -1,13 +1,15 @@
 """Per-kernel sums of every counter in rocprofv3 --pmc counter_collection.csv
 files under DIR/p*/ (tools/gpu_pmc_tb.sh), with kernel durations from
-DIR/kt and a few derived ratios.  python tools/pmc_dump.py DIR"""
+DIR/kt and a few derived ratios.  python tools/pmc_dump.py DIR [kernel-regex, default "trace"]"""
 import csv
 import glob
 import os
+import re
 import sys
 from collections import defaultdict
 
 d = sys.argv[1]
+pat = re.compile(sys.argv[2] if len(sys.argv) > 2 else "trace")
 tot = defaultdict(lambda: defaultdict(float))
 for f in glob.glob(os.path.join(d, "p*", "*counter_collection.csv")):
     for r in csv.DictReader(open(f)):
@@ -18,7 +20,7 @@ for f in glob.glob(os.path.join(d, "kt", "*kernel_stats.csv")):
     for r in csv.DictReader(open(f)):
         dur[r["Name"].split("(")[0]] += float(r["TotalDurationNs"])
 for k in sorted(tot):
-    if "trace" not in k:
+    if not pat.search(k):
         continue
     c = tot[k]
     g = c.get
@@ -38,6 +40,8 @@ for k in sorted(tot):
     if g("TCP_TCC_READ_REQ_sum") and g("TCP_TOTAL_CACHE_ACCESSES_sum"):
         print(f"   L1->L2 frac {g('TCP_TCC_READ_REQ_sum') / g('TCP_TOTAL_CACHE_ACCESSES_sum'):.3f}  "
               f"L2 read latency {g('TCP_TCC_READ_REQ_LATENCY_sum') / g('TCP_TCC_READ_REQ_sum'):.0f} cyc")
+    if g("FETCH_SIZE") is not None or g("WRITE_SIZE") is not None:
+        print(f"   FETCH {g('FETCH_SIZE', 0) / 1048576:.3f} GB  WRITE {g('WRITE_SIZE', 0) / 1048576:.3f} GB (KiB counters)")
     if g("TCC_HIT_sum") is not None and g("TCC_MISS_sum"):
         print(f"   L2 hit {g('TCC_HIT_sum') / (g('TCC_HIT_sum') + g('TCC_MISS_sum')):.3f}")
     if g("SQ_INSTS_VMEM_RD") and g("SQ_INST_LEVEL_VMEM"):
