@@ -115,6 +115,16 @@ __device__ __forceinline__ void ld_tri(const float* rec, float4& A, float4& E1, 
   E1 = *reinterpret_cast<const float4*>(rec + 4);
   E2 = *reinterpret_cast<const float4*>(rec + 8);
 }
+// the same without the prim id and the pad words: three 12-B loads (the
+// any-hit test needs only a, e1, e2)
+typedef float f3l __attribute__((ext_vector_type(3)));
+__device__ __forceinline__ void ld_tri12(const float* rec, float4& A, float4& E1, float4& E2) {
+  const f3l a = *reinterpret_cast<const f3l*>(rec), e1 = *reinterpret_cast<const f3l*>(rec + 4),
+            e2 = *reinterpret_cast<const f3l*>(rec + 8);
+  A = make_float4(a.x, a.y, a.z, 0.f);
+  E1 = make_float4(e1.x, e1.y, e1.z, 0.f);
+  E2 = make_float4(e2.x, e2.y, e2.z, 0.f);
+}
 
 struct SurfPt {
   v3 P, N, Ng, NU, NV;
@@ -663,6 +673,10 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
       // one load: the leaf's own record (prim id in A.w)
       const float* tp = (on == 1u) ? S.tris + (size_t)ow0 * kTriWords : S.ltris + (size_t)(ow0 + k) * kTriWords;
       float4 A, E1, E2;
+#ifdef YK_TRI12
+      if (!CLOSEST) ld_tri12(tp, A, E1, E2);
+      else
+#endif
       ld_tri(tp, A, E1, E2);
       p = __float_as_uint(A.w);
       asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
@@ -1360,21 +1374,40 @@ __device__ __forceinline__ bool dirac_illum(const DLight& L, v3 P, v3& ldir, flo
 
 // ------------------------------------------------------------ queues
 
-// Queue appends: one returning atomic per 256-thread block instead of per
-// wave. Every wave of a launch appends to the same counter word, and the
-// returning atomics serialise on it; measured 1068 -> 1263 Mrays/s (photon
-// mapping, 32 gather launches of 33M threads per batch) and 2008 -> 2038
-// (path tracing).
+// Queue appends (wave_append2): every wave of a launch appends to the same
+// counter word, and the returning atomics serialise on it; one atomic per
+// block measured 1068 -> 1263 Mrays/s in round 1 (photon mapping, 32 gather
+// launches of 33M threads per batch) and 2008 -> 2038 (path tracing), and
+// round 3 found the path-tracing kernels faster per wave again once the
+// block-size changes below had cut their launch count.
 // Block sizes of the kernels that append to ray queues (fewer, larger blocks
 // = fewer returning atomics on the queue word). Measured: path-tracing
 // shading at 1024 threads 2038 -> 2075 Mrays/s (k_shade_primary at 512:
 // 2744 against 2811); the photon / final-gather kernels best at 512
 // (1261 -> 1274; 1024: 1240).
-#define YK_SHADE_BLOCK 1024  // round 3: 256 / 512 measured C2 7785-7977 / 7679-7827 against 7932-8090
+#ifndef YK_SHADE_BLOCK
+#define YK_SHADE_BLOCK 1024  // round 3: 256 / 512 measured C2 7785-7977 / 7679-7827 against 7932-8090;
+                             // 512 / 256 for k_shade_bounce alone: headline and C2 unchanged
+#endif
+#ifndef YK_APPEND_BLOCK
 #define YK_APPEND_BLOCK 512
-// Reserves m_s shadow-queue and m_b bounce-queue entries with ONE returning
-// atomic per wave: the counter word holds (bounce count << 32) | shadow
-// count. Whole-wave call; returns each lane's first index in both queues.
+#endif
+// Reserves m_s shadow-queue and m_b bounce-queue entries: the counter word
+// holds (bounce count << 32) | shadow count. Whole-wave call; returns each
+// lane's first index in both queues. PER_WAVE: one returning atomic per
+// wave, each wave goes on at once; else one per block, the wave totals
+// meeting in LDS between two barriers (every wave of the block then waits
+// for the atomic's round trip). Path-tracing shading per wave (round 3,
+// 1024-thread blocks: headline 2838 -> 2917 Mrays/s, C2 8384 -> 8356);
+// the photon / final-gather kernels' launches are 33M threads each, and
+// per-block atomics measured 1068 -> 1263 Mrays/s there in round 1.
+#ifndef YK_PT_APPEND_WAVE
+#define YK_PT_APPEND_WAVE true
+#endif
+#ifndef YK_PM_APPEND_WAVE
+#define YK_PM_APPEND_WAVE false
+#endif
+template <bool PER_WAVE>
 __device__ __forceinline__ void wave_append2(unsigned long long* counter, unsigned m_s, unsigned m_b,
                                              unsigned& base_s, unsigned& base_b) {
   const int lane = threadIdx.x & 63;
@@ -1386,6 +1419,14 @@ __device__ __forceinline__ void wave_append2(unsigned long long* counter, unsign
     if (lane >= off) incl += ((unsigned long long)hi << 32) | lo;
   }
   const unsigned long long total = shfl_u64(incl, 63);
+  if (PER_WAVE) {
+    unsigned long long wb = 0;
+    if (lane == 63 && total) wb = atomicAdd(counter, total);
+    wb = shfl_u64(wb, 63) + incl - m;
+    base_s = (unsigned)wb;
+    base_b = (unsigned)(wb >> 32);
+    return;
+  }
   // one returning atomic per block: wave totals meet in LDS (all callers
   // reach this point with whole blocks)
   __shared__ unsigned long long s_tot[16];
@@ -1552,8 +1593,9 @@ __global__ void __launch_bounds__(256) k_camera(TileList TL, Batch B, RenderCons
   if (c >= nc) return;
   int s, j, i;
   if (TL.pix) {  // adaptive pass: only the flagged pixels, in tile / row order
-    const int packed = TL.pix[c / R.spp];
-    s = (int)(c % R.spp);
+    // 32-bit index arithmetic: a batch holds far fewer than 2^31 samples
+    const int packed = TL.pix[(unsigned)c / (unsigned)R.spp];
+    s = (int)((unsigned)c % (unsigned)R.spp);
     j = packed & 0xFFFF;
     i = packed >> 16;
   } else {
@@ -1565,8 +1607,8 @@ __global__ void __launch_bounds__(256) k_camera(TileList TL, Batch B, RenderCons
     }
     const int4 T = TL.tiles[lo];
     const long long local = c - TL.base[lo];
-    s = (int)(local % R.spp);
-    const int pl = (int)(local / R.spp);
+    s = (int)((unsigned)local % (unsigned)R.spp);
+    const int pl = (int)((unsigned)local / (unsigned)R.spp);
     j = T.x + pl % T.z;
     i = T.y + pl / T.z;
   }
@@ -1794,7 +1836,7 @@ __device__ __forceinline__ void flush_shadow(const Batch& B, long long c, int ke
 // primary BSDF (pathtracer.cc:169-187). Returns the segment's ray.
 __device__ __forceinline__ yk_ray path_first_segment(const Batch& B, const RenderConst& R, long long c,
                                                      const SurfPt& sp, const DMat& M, v3 dir, int isub) {
-  const unsigned s = R.ps ? B.psample[c] : (unsigned)(c % R.spp);
+  const unsigned s = R.ps ? B.psample[c] : (unsigned)c % (unsigned)R.spp;
   const unsigned offs = (unsigned)(R.nsub * (int)s) + B.soffs[c] + (unsigned)isub;
   const float s1 = ri_vdc(offs, 0u);
   const float s2 = (float)scr_halton(2, offs);
@@ -1856,7 +1898,7 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) k_shade_primary(DScene S, Batc
       }
       if (M.flags & BSDF_DIFFUSE) ph |= PH_DIFFUSE;
       if ((M.flags & BSDF_DIFFUSE) && !R.pm_showmap) {
-        const unsigned s = R.ps ? B.psample[c] : (unsigned)(c % R.spp);
+        const unsigned s = R.ps ? B.psample[c] : (unsigned)c % (unsigned)R.spp;
         int k0 = 0;
         for (int l = 0; l < R.nlights; ++l) {
           nr += gen_light(B, c, k0, l, sp, wo, s, B.soffs[c], (unsigned)l, traced);
@@ -1893,7 +1935,7 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) k_shade_primary(DScene S, Batc
     if (!emit) B.wlast[c] = 0.f;
   }
   unsigned sbase, q;
-  wave_append2(qword, valid ? (unsigned)nr : 0u, emit ? 1u : 0u, sbase, q);
+  wave_append2<YK_PT_APPEND_WAVE>(qword, valid ? (unsigned)nr : 0u, emit ? 1u : 0u, sbase, q);
   if (valid) flush_shadow(B, c, kend, nr, sbase, traced);
   if (emit) {
     B.q_rays[1][q] = seg;
@@ -1986,7 +2028,7 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) k_path_start(DScene S, Batch B
     }
   }
   unsigned sbase, q;
-  wave_append2(qword, 0u, emit ? 1u : 0u, sbase, q);
+  wave_append2<YK_PT_APPEND_WAVE>(qword, 0u, emit ? 1u : 0u, sbase, q);
   if (emit) {
     B.q_rays[1][q] = r;
     B.q_owner[1][q] = (int)c;
@@ -2038,7 +2080,7 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) k_shade_bounce(DScene S, Batch
       const SurfPt sp = make_surface(S, from, dir, h);
       const DMat& M = c_mats[sp.mat];
       const v3 pwo = vneg(dir);
-      const unsigned s = R.ps ? B.psample[c] : (unsigned)(c % R.spp);
+      const unsigned s = R.ps ? B.psample[c] : (unsigned)c % (unsigned)R.spp;
       const unsigned offs = (unsigned)(R.nsub * (int)s) + B.soffs[c] + (unsigned)isub;
       int ps = PS_RESOLVE;
       // estimateOneDirectLight(state, hit, pwo, offs): always at the first
@@ -2090,7 +2132,7 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) k_shade_bounce(DScene S, Batch
     }
   }
   unsigned sbase, qn;
-  wave_append2(qword, valid ? (unsigned)nr : 0u, emit_next ? 1u : 0u, sbase, qn);
+  wave_append2<YK_PT_APPEND_WAVE>(qword, valid ? (unsigned)nr : 0u, emit_next ? 1u : 0u, sbase, qn);
   if (valid) flush_shadow(B, c, kend, nr, sbase, traced);
   if (emit_next) {
     B.q_rays[qin ^ 1][qn] = nxt;
@@ -3504,6 +3546,10 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   const long long target_spec = d->spec ? std::min(target, (12ll << 30) / (kNodeBytes * spec_worst)) : target;
   const int tiles_per_batch = (int)std::max<long long>(1, target_spec / tile_samples);
   const long long maxc = (long long)tiles_per_batch * tile_samples;
+  // camera-sample indices are 32-bit on the device, shadow-slot indices
+  // (k * maxc + c) 32-bit in the shadow queue
+  if (maxc >= (1ll << 31) || maxc * (long long)std::max(K, 1) >= (1ll << 32))
+    return set_error(YK_ERR_UNSUPPORTED, "one tile holds too many samples (tile^2 * spp * shadow slots >= 2^32)");
   const int nbatch = (int)((owned.size() + tiles_per_batch - 1) / tiles_per_batch);
   const int npipes = d->spec ? 1 : std::min(pipes_cfg, std::max(1, nbatch));
   const bool path = p->integrator == YK_INTEGRATOR_PATH;
