@@ -673,11 +673,10 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
       // one load: the leaf's own record (prim id in A.w)
       const float* tp = (on == 1u) ? S.tris + (size_t)ow0 * kTriWords : S.ltris + (size_t)(ow0 + k) * kTriWords;
       float4 A, E1, E2;
-#ifdef YK_TRI12
-      if (!CLOSEST) ld_tri12(tp, A, E1, E2);
-      else
-#endif
-      ld_tri(tp, A, E1, E2);
+      // any-hit: 36 of the record's 48 B (round 3: headline 2907 -> 2920, C2
+      // 8191 -> 8274; the prim id is the closest-hit kernel's only)
+      if (CLOSEST) ld_tri(tp, A, E1, E2);
+      else ld_tri12(tp, A, E1, E2);
       p = __float_as_uint(A.w);
       asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
                    "+v"(E2.y), "+v"(E2.z));

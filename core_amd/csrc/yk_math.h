@@ -103,7 +103,6 @@ __device__ __forceinline__ void hal_start(Halton& h, unsigned base, unsigned i) 
   h.inv = 1.0 / (double)base;
   h.fast = 0.9999999999 - h.inv;
   const double inv = h.inv;
-#ifndef YK_HAL_LOOP
   if (base == 2u) {
     // base 2: every term bit_k * 2^-(k+1) and every partial sum (at most 32
     // significant bits) is exact in double, so the loop's result is
@@ -111,7 +110,6 @@ __device__ __forceinline__ void hal_start(Halton& h, unsigned base, unsigned i) 
     h.value = (double)__builtin_bitreverse32(i) * 0x1p-32;
     return;
   }
-#endif
   double factor = inv;
   h.value = 0.0;
   while (i > 0) {
