@@ -62,6 +62,7 @@ struct DMat {
 
 struct DLight {  // areaLight_t members after its constructor (arealight.cc:30-49)
   float corner[3], toX[3], toY[3], fnormal[3], c2[3], c3[3], c4[3], color[3];
+  float e2[3], e3[3], e4[3];  // c2 - corner, c3 - corner, c4 - corner: intersect()'s triangle edges
   float area;
   int samples;
   int type;    // YK_LIGHT_*; point / directional are Dirac lights (mcintegrator.cc:85-100)
@@ -1302,11 +1303,6 @@ __device__ __forceinline__ c3 mat_emit(const DMat& M, const SurfPt& sp, v3 wo, b
   return C3(M.emit_col[0], M.emit_col[1], M.emit_col[2]);
 }
 
-// triIntersect, arealight.cc:98-115
-__device__ __forceinline__ bool tri_isect_pts(v3 a, v3 b, v3 c, v3 from, v3 dir, float& t) {
-  float u, v;
-  return mt_intersect(a, vsub(b, a), vsub(c, a), from, dir, t, u, v);
-}
 
 // areaLight_t::illumSample, arealight.cc:68-96 (compiled sample point form)
 __device__ __forceinline__ bool light_illum(const DLight& L, v3 P, float s1, float s2, v3& ldir, float& tmax,
@@ -1331,8 +1327,10 @@ __device__ __forceinline__ bool light_illum(const DLight& L, v3 P, float s1, flo
 __device__ __forceinline__ bool light_hit(const DLight& L, v3 from, v3 dir, float& t, float& ipdf) {
   const float cos_angle = vdot(dir, ld3(L.fnormal));
   if (cos_angle <= 0.f) return false;
-  if (!tri_isect_pts(ld3(L.corner), ld3(L.c2), ld3(L.c3), from, dir, t)) {
-    if (!tri_isect_pts(ld3(L.corner), ld3(L.c3), ld3(L.c4), from, dir, t)) return false;
+  // triIntersect(corner, c2, c3) then (corner, c3, c4), edges precomputed
+  float u, v;
+  if (!mt_intersect(ld3(L.corner), ld3(L.e2), ld3(L.e3), from, dir, t, u, v)) {
+    if (!mt_intersect(ld3(L.corner), ld3(L.e3), ld3(L.e4), from, dir, t, u, v)) return false;
   }
   if (!(t > 1.0e-10f)) return false;
   ipdf = (float)((double)((1.f / (t * t)) * L.area * cos_angle) * YK_1_PI_D);
@@ -2825,6 +2823,11 @@ DLight make_light(const yk_area_light_state& L) {
     D.c3[k] = c[k] + (x[k] + y[k]);
     D.c4[k] = c[k] + y[k];
     D.color[k] = L.color[k];
+  }
+  for (int k = 0; k < 3; ++k) {  // the device's b - a of triIntersect (arealight.cc:98-115)
+    D.e2[k] = D.c2[k] - D.corner[k];
+    D.e3[k] = D.c3[k] - D.corner[k];
+    D.e4[k] = D.c4[k] - D.corner[k];
   }
   D.area = vl;
   D.samples = L.samples;

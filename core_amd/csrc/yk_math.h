@@ -169,11 +169,15 @@ __device__ __host__ __forceinline__ unsigned fnv32a(unsigned value) {
 
 // FAST_TRIG fSin (mathOptimizations.h:249-268), compiled form of the copy
 // inlined in shinyDiffuseMat_t::sample: CONST_P*(x|x|-x)+x -> x+(|x|-1)*(CONST_P*x)
+// The range tests compare the float in double against 2pi / pi; neither is a
+// float, so (double)x > D is x > (largest float below D) and (double)x < -D
+// is x < -(largest float below D): float compares, checked equal to the
+// double ones for all 2^32 bit patterns.
 __device__ __forceinline__ float fsin_ref(float x) {
-  if ((double)x > YK_2PI_D || (double)x < -YK_2PI_D)
-    x -= (float)((int)(x * (float)0.15915494309189533577)) * (float)YK_2PI_D;
-  if ((double)x < -YK_PI_D) x += (float)YK_2PI_D;
-  else if ((double)x > YK_PI_D) x -= (float)YK_2PI_D;
+  const float k2pi_dn = __uint_as_float(0x40c90fdau), kpi_dn = __uint_as_float(0x40490fdau);
+  if (x > k2pi_dn || x < -k2pi_dn) x -= (float)((int)(x * (float)0.15915494309189533577)) * (float)YK_2PI_D;
+  if (x < -kpi_dn) x += (float)YK_2PI_D;
+  else if (x > kpi_dn) x -= (float)YK_2PI_D;
   x = ((float)1.27323954473516268615 * x) - (((float)0.40528473456935108578 * x) * fabsf(x));
   float r = x + (fabsf(x) - 1.0f) * (0.225f * x);
   if (r > 1.0f) r = 1.0f;
