@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -623,7 +624,10 @@ __device__ __forceinline__ unsigned dpp_max_scan(unsigned x) {
 // 24-bit owner keys: the keys then hold the start relative to the round and
 // the owner's start is read from its lane (one cross-lane read more per
 // round; measured 0.7 % slower, so only such trees run it).
-template <bool CLOSEST, bool BIG = false, bool UNI = false>
+// LEAN (closest hit, crowded-leaf trees): every pair loads 36 of the 48 B
+// (ld_tri12); the winning reference's prim id is read once per leaf after
+// the rounds (hair: 528 tests per closest ray through the texture-data path).
+template <bool CLOSEST, bool BIG = false, bool UNI = false, bool LEAN = false>
 __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t nref, uint32_t w0, int lane,
                                             unsigned long long* keys, float4* cand, unsigned* otab,
                                             unsigned& ntris, bool& occluded) {
@@ -676,7 +680,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
       float4 A, E1, E2;
       // any-hit: 36 of the record's 48 B (round 3: headline 2907 -> 2920, C2
       // 8191 -> 8274; the prim id is the closest-hit kernel's only)
-      if (CLOSEST) ld_tri(tp, A, E1, E2);
+      if (CLOSEST && !LEAN) ld_tri(tp, A, E1, E2);
       else ld_tri12(tp, A, E1, E2);
       p = __float_as_uint(A.w);
       asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
@@ -708,7 +712,9 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
         st.Z = c.x;
         st.b1 = c.y;
         st.b2 = c.z;
-        st.prim = (int)__float_as_uint(c.w);
+        // LEAN: the winner's prim id from its record (single-prim leaves: w0)
+        st.prim = LEAN ? (nref == 1u ? (int)w0 : (int)__float_as_uint(S.ltris[(size_t)(w0 + (uint32_t)kk) * kTriWords + 3]))
+                       : (int)__float_as_uint(c.w);
       }
     } else if (kk != ~0ull) {
       occluded = true;
@@ -742,7 +748,7 @@ struct RayCount {
   }
 };
 
-template <bool CLOSEST, int NSEG, bool TS = false, bool BIG = false, bool UNI = false>
+template <bool CLOSEST, int NSEG, bool TS = false, bool BIG = false, bool UNI = false, bool LEAN = false>
 __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx,
                                            RayCount rc, yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
                                            unsigned long long* __restrict__ work, unsigned long long* __restrict__ ctr,
@@ -891,7 +897,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       }
 #endif
       bool occ = false;
-      coop_leaves<CLOSEST, BIG, UNI>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, otab, ntris, occ);
+      coop_leaves<CLOSEST, BIG, UNI, LEAN>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, otab, ntris, occ);
 #ifdef YK_TRAV_STATS
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       {
@@ -1022,7 +1028,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHAD
 k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false, 1>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+#ifndef YK_SHADOW_NSEG
+#define YK_SHADOW_NSEG 1
+#endif
+  trace_body<false, YK_SHADOW_NSEG>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+}
+// crowded-leaf trees (hair): 36-B leaf tests (coop_leaves LEAN)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
+k_trace_closest_lean(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+                     yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
+                     unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
+  trace_body<true, 8, false, false, false, true>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 // trees with a leaf of 2^17 references or more (coop_leaves BIG)
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
@@ -1384,7 +1400,9 @@ __device__ __forceinline__ bool dirac_illum(const DLight& L, v3 P, v3& ldir, flo
 // (1261 -> 1274; 1024: 1240).
 #ifndef YK_SHADE_BLOCK
 #define YK_SHADE_BLOCK 1024  // round 3: 256 / 512 measured C2 7785-7977 / 7679-7827 against 7932-8090;
-                             // 512 / 256 for k_shade_bounce alone: headline and C2 unchanged
+                             // 512 / 256 for k_shade_bounce alone: headline and C2 unchanged; 256 with
+                             // k_shade_bounce at 5 / 6 waves per SIMD (6 / 23 VGPRs spilled): headline
+                             // 2892 / 2777, C2 8326 / 7865 against 2959 / 8429
 #endif
 #ifndef YK_APPEND_BLOCK
 #define YK_APPEND_BLOCK 512
@@ -1666,6 +1684,20 @@ __global__ void __launch_bounds__(256) k_camera(TileList TL, Batch B, RenderCons
   B.p_rays[c] = r;
 }
 
+// Ray records streamed to the next kernel (shadow slots, bounce queues):
+// YK_NT_RAYS stores them non-temporally (experiment: keep the scene's lines
+// in the caches rather than the batch's streamed rays).
+__device__ __forceinline__ void st_ray(yk_ray* p, const yk_ray& r) {
+#ifdef YK_NT_RAYS
+  typedef float f4n __attribute__((ext_vector_type(4)));
+  f4n* q = reinterpret_cast<f4n*>(p);
+  const f4n a = {r.from[0], r.from[1], r.from[2], r.dir[0]}, b = {r.dir[1], r.dir[2], r.tmin, r.tmax};
+  __builtin_nontemporal_store(a, q);
+  __builtin_nontemporal_store(b, q + 1);
+#else
+  *p = r;
+#endif
+}
 __device__ __forceinline__ void put_ray(yk_ray& r, v3 f, v3 d, float tmin, float tmax) {
   r.from[0] = f.x;
   r.from[1] = f.y;
@@ -1719,7 +1751,11 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
       put_slot(B, slot, 0, black);
       return 0;
     }
-    put_ray(B.s_rays[slot], sp.P, ldir, YK_SHADOW_BIAS, ltmax);
+    {
+      yk_ray sr;
+      put_ray(sr, sp.P, ldir, YK_SHADOW_BIAS, ltmax);
+      st_ray(&B.s_rays[slot], sr);
+    }
     if (k0 < 64) traced |= 1ull << k0;
     const c3 surf = mat_eval(M, sp, wo, ldir);
     const float f = fabsf(vdot(sp.N, ldir));
@@ -1751,7 +1787,11 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
       put_slot(B, slot, 0, black);
       continue;
     }
-    put_ray(B.s_rays[slot], sp.P, ldir, YK_SHADOW_BIAS, ltmax);
+    {
+      yk_ray sr;
+      put_ray(sr, sp.P, ldir, YK_SHADOW_BIAS, ltmax);
+      st_ray(&B.s_rays[slot], sr);
+    }
     ++nr;
     if (k0 + i < 64) traced |= 1ull << (k0 + i);
     if (!(lpdf > 1e-6f)) {
@@ -1794,7 +1834,11 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
       put_slot(B, slot, 0, black);
       continue;
     }
-    put_ray(B.s_rays[slot], sp.P, bdir, YK_MIN_RAYDIST, bt);
+    {
+      yk_ray sr;
+      put_ray(sr, sp.P, bdir, YK_MIN_RAYDIST, bt);
+      st_ray(&B.s_rays[slot], sr);
+    }
     ++nr;
     if (k0 + n + i < 64) traced |= 1ull << (k0 + n + i);
     if (!(lightPdf > 1e-6f)) {
@@ -1935,7 +1979,7 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) k_shade_primary(DScene S, Batc
   wave_append2<YK_PT_APPEND_WAVE>(qword, valid ? (unsigned)nr : 0u, emit ? 1u : 0u, sbase, q);
   if (valid) flush_shadow(B, c, kend, nr, sbase, traced);
   if (emit) {
-    B.q_rays[1][q] = seg;
+    st_ray(&B.q_rays[1][q], seg);
     B.q_owner[1][q] = (int)c;
   }
 }
@@ -2027,7 +2071,7 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) k_path_start(DScene S, Batch B
   unsigned sbase, q;
   wave_append2<YK_PT_APPEND_WAVE>(qword, 0u, emit ? 1u : 0u, sbase, q);
   if (emit) {
-    B.q_rays[1][q] = r;
+    st_ray(&B.q_rays[1][q], r);
     B.q_owner[1][q] = (int)c;
   }
 }
@@ -2132,7 +2176,7 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) k_shade_bounce(DScene S, Batch
   wave_append2<YK_PT_APPEND_WAVE>(qword, valid ? (unsigned)nr : 0u, emit_next ? 1u : 0u, sbase, qn);
   if (valid) flush_shadow(B, c, kend, nr, sbase, traced);
   if (emit_next) {
-    B.q_rays[qin ^ 1][qn] = nxt;
+    st_ray(&B.q_rays[qin ^ 1][qn], nxt);
     B.q_owner[qin ^ 1][qn] = (int)c;
   }
 }
@@ -2718,6 +2762,7 @@ struct yk_device {
   int cus = 0;
   int per_cu[2] = {1, 1};  // resident trace waves per CU: [0] any-hit, [1] closest
   int per_cu_big[2] = {1, 1};  // the same for the BIG-leaf kernels
+  int per_cu_lean = 1;         // k_trace_closest_lean (crowded-leaf trees)
   hipStream_t stream = nullptr;  // = pipe[0].stream (ray queries, film resolve)
   bool uploaded = false;
   const yk_scene* uploaded_scene = nullptr;  // the scene the resident arrays came from
@@ -2989,12 +3034,17 @@ int refill_min() {
 template <bool CLOSEST>
 void enqueue_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* idx, RayCount n, yk_hit* hits,
                    uint8_t* occ, unsigned long long* work, unsigned long long* acc, hipEvent_t ev0, hipEvent_t ev1) {
-  const long long per_cu = d->big_leaves ? d->per_cu_big[CLOSEST] : d->per_cu[CLOSEST];
+#ifdef YK_LEAN
+  const bool lean = CLOSEST && d->crowded_leaves && !d->big_leaves;
+#else
+  const bool lean = false;  // k_trace_closest_lean pending measurement on the GPU
+#endif
+  const long long per_cu = d->big_leaves ? d->per_cu_big[CLOSEST] : (lean ? d->per_cu_lean : d->per_cu[CLOSEST]);
   const long long grid = (long long)d->cus * per_cu;
   const int ovf_depth = std::max(1, stack_depth(d) - kStackLds);
   P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
   if (ev0) HIPCHK(hipEventRecord(ev0, P.stream));
-  auto kern = CLOSEST ? (d->big_leaves ? k_trace_closest_big : k_trace_closest)
+  auto kern = CLOSEST ? (d->big_leaves ? k_trace_closest_big : (lean ? k_trace_closest_lean : k_trace_closest))
                       : (d->S.uni ? (d->big_leaves ? k_trace_shadow_big_uni : k_trace_shadow_uni)
                                   : (d->big_leaves ? k_trace_shadow_big : k_trace_shadow));
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays, idx, n, hits, occ, work, acc,
@@ -3120,6 +3170,8 @@ int yk_device_open(int32_t ordinal, yk_device** out) {
   d->per_cu_big[0] = std::max(1, blocks);
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_closest_big, 64, 0));
   d->per_cu_big[1] = std::max(1, blocks);
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_closest_lean, 64, 0));
+  d->per_cu_lean = std::max(1, blocks);
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow_ts, 64, 0));
   d->per_cu_ts = std::max(1, blocks);
   upload_qmc();
@@ -3546,7 +3598,13 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   if (d->spec && spec_worst * tile_samples * kNodeBytes > (48ll << 30))
     return set_error(YK_ERR_UNSUPPORTED, "raydepth too large for the tile size / spp (node store > 48 GB)");
   const long long target_spec = d->spec ? std::min(target, (12ll << 30) / (kNodeBytes * spec_worst)) : target;
-  const int tiles_per_batch = (int)std::max<long long>(1, target_spec / tile_samples);
+  // path tracing / direct light: at least one batch per pipeline when the
+  // frame has the tiles for it -- a frame of 2 full batches (C2: 1024 tiles
+  // of 64K samples) leaves two pipelines idle (C2 8388 -> 8700 Mrays/s,
+  // headline and hair unchanged); photon mapping keeps full batches (its
+  // 16-spp bench frame in 4 batches instead of 1: 1572 -> 1537)
+  const long long tiles_fill = (d->spec || pm) ? LLONG_MAX : ((long long)owned.size() + pipes_cfg - 1) / pipes_cfg;
+  const int tiles_per_batch = (int)std::max<long long>(1, std::min(target_spec / tile_samples, tiles_fill));
   const long long maxc = (long long)tiles_per_batch * tile_samples;
   // camera-sample indices are 32-bit on the device, shadow-slot indices
   // (k * maxc + c) 32-bit in the shadow queue
