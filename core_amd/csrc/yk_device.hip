@@ -624,10 +624,7 @@ __device__ __forceinline__ unsigned dpp_max_scan(unsigned x) {
 // 24-bit owner keys: the keys then hold the start relative to the round and
 // the owner's start is read from its lane (one cross-lane read more per
 // round; measured 0.7 % slower, so only such trees run it).
-// LEAN (closest hit, crowded-leaf trees): every pair loads 36 of the 48 B
-// (ld_tri12); the winning reference's prim id is read once per leaf after
-// the rounds (hair: 528 tests per closest ray through the texture-data path).
-template <bool CLOSEST, bool BIG = false, bool UNI = false, bool LEAN = false>
+template <bool CLOSEST, bool BIG = false, bool UNI = false>
 __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t nref, uint32_t w0, int lane,
                                             unsigned long long* keys, float4* cand, unsigned* otab,
                                             unsigned& ntris, bool& occluded) {
@@ -680,7 +677,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
       float4 A, E1, E2;
       // any-hit: 36 of the record's 48 B (round 3: headline 2907 -> 2920, C2
       // 8191 -> 8274; the prim id is the closest-hit kernel's only)
-      if (CLOSEST && !LEAN) ld_tri(tp, A, E1, E2);
+      if (CLOSEST) ld_tri(tp, A, E1, E2);
       else ld_tri12(tp, A, E1, E2);
       p = __float_as_uint(A.w);
       asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
@@ -712,9 +709,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
         st.Z = c.x;
         st.b1 = c.y;
         st.b2 = c.z;
-        // LEAN: the winner's prim id from its record (single-prim leaves: w0)
-        st.prim = LEAN ? (nref == 1u ? (int)w0 : (int)__float_as_uint(S.ltris[(size_t)(w0 + (uint32_t)kk) * kTriWords + 3]))
-                       : (int)__float_as_uint(c.w);
+        st.prim = (int)__float_as_uint(c.w);
       }
     } else if (kk != ~0ull) {
       occluded = true;
@@ -748,7 +743,7 @@ struct RayCount {
   }
 };
 
-template <bool CLOSEST, int NSEG, bool TS = false, bool BIG = false, bool UNI = false, bool LEAN = false>
+template <bool CLOSEST, int NSEG, bool TS = false, bool BIG = false, bool UNI = false>
 __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx,
                                            RayCount rc, yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
                                            unsigned long long* __restrict__ work, unsigned long long* __restrict__ ctr,
@@ -897,7 +892,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       }
 #endif
       bool occ = false;
-      coop_leaves<CLOSEST, BIG, UNI, LEAN>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, otab, ntris, occ);
+      coop_leaves<CLOSEST, BIG, UNI>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, otab, ntris, occ);
 #ifdef YK_TRAV_STATS
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       {
@@ -1032,13 +1027,6 @@ k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __rest
 #define YK_SHADOW_NSEG 1
 #endif
   trace_body<false, YK_SHADOW_NSEG>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
-}
-// crowded-leaf trees (hair): 36-B leaf tests (coop_leaves LEAN)
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
-k_trace_closest_lean(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
-                     yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
-                     unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<true, 8, false, false, false, true>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 // trees with a leaf of 2^17 references or more (coop_leaves BIG)
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
@@ -1684,11 +1672,12 @@ __global__ void __launch_bounds__(256) k_camera(TileList TL, Batch B, RenderCons
   B.p_rays[c] = r;
 }
 
-// Ray records streamed to the next kernel (shadow slots, bounce queues):
-// YK_NT_RAYS stores them non-temporally (experiment: keep the scene's lines
-// in the caches rather than the batch's streamed rays).
+// Ray records streamed to the next kernel (shadow slots, bounce queues) are
+// stored non-temporally, so they do not displace the scene's node and
+// triangle lines (round 3: headline 2944 -> 2964, C2 8697 -> 8850 Mrays/s;
+// non-temporal loads in the traversal kernels measured slower, §5).
 __device__ __forceinline__ void st_ray(yk_ray* p, const yk_ray& r) {
-#ifdef YK_NT_RAYS
+#ifndef YK_PLAIN_RAY_STORES
   typedef float f4n __attribute__((ext_vector_type(4)));
   f4n* q = reinterpret_cast<f4n*>(p);
   const f4n a = {r.from[0], r.from[1], r.from[2], r.dir[0]}, b = {r.dir[1], r.dir[2], r.tmin, r.tmax};
@@ -2762,7 +2751,6 @@ struct yk_device {
   int cus = 0;
   int per_cu[2] = {1, 1};  // resident trace waves per CU: [0] any-hit, [1] closest
   int per_cu_big[2] = {1, 1};  // the same for the BIG-leaf kernels
-  int per_cu_lean = 1;         // k_trace_closest_lean (crowded-leaf trees)
   hipStream_t stream = nullptr;  // = pipe[0].stream (ray queries, film resolve)
   bool uploaded = false;
   const yk_scene* uploaded_scene = nullptr;  // the scene the resident arrays came from
@@ -3034,17 +3022,12 @@ int refill_min() {
 template <bool CLOSEST>
 void enqueue_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* idx, RayCount n, yk_hit* hits,
                    uint8_t* occ, unsigned long long* work, unsigned long long* acc, hipEvent_t ev0, hipEvent_t ev1) {
-#ifdef YK_LEAN
-  const bool lean = CLOSEST && d->crowded_leaves && !d->big_leaves;
-#else
-  const bool lean = false;  // k_trace_closest_lean pending measurement on the GPU
-#endif
-  const long long per_cu = d->big_leaves ? d->per_cu_big[CLOSEST] : (lean ? d->per_cu_lean : d->per_cu[CLOSEST]);
+  const long long per_cu = d->big_leaves ? d->per_cu_big[CLOSEST] : d->per_cu[CLOSEST];
   const long long grid = (long long)d->cus * per_cu;
   const int ovf_depth = std::max(1, stack_depth(d) - kStackLds);
   P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
   if (ev0) HIPCHK(hipEventRecord(ev0, P.stream));
-  auto kern = CLOSEST ? (d->big_leaves ? k_trace_closest_big : (lean ? k_trace_closest_lean : k_trace_closest))
+  auto kern = CLOSEST ? (d->big_leaves ? k_trace_closest_big : k_trace_closest)
                       : (d->S.uni ? (d->big_leaves ? k_trace_shadow_big_uni : k_trace_shadow_uni)
                                   : (d->big_leaves ? k_trace_shadow_big : k_trace_shadow));
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays, idx, n, hits, occ, work, acc,
@@ -3170,8 +3153,6 @@ int yk_device_open(int32_t ordinal, yk_device** out) {
   d->per_cu_big[0] = std::max(1, blocks);
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_closest_big, 64, 0));
   d->per_cu_big[1] = std::max(1, blocks);
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_closest_lean, 64, 0));
-  d->per_cu_lean = std::max(1, blocks);
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow_ts, 64, 0));
   d->per_cu_ts = std::max(1, blocks);
   upload_qmc();
