@@ -913,7 +913,14 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
         }
         if (done) {
           if (CLOSEST) {
+#ifdef YK_NT_HITS
+            typedef float f4h __attribute__((ext_vector_type(4)));
+            const f4h hv = {__int_as_float(st.prim >= 0 ? st.prim : -1), st.prim >= 0 ? st.Z : 0.f,
+                            st.prim >= 0 ? st.b1 : 0.f, st.prim >= 0 ? st.b2 : 0.f};
+            __builtin_nontemporal_store(hv, reinterpret_cast<f4h*>(hits + rid));
+#else
             hits[rid] = (st.prim >= 0) ? yk_hit{st.prim, st.Z, st.b1, st.b2} : yk_hit{-1, 0.f, 0.f, 0.f};
+#endif
           } else {
             occl[rid] = occ ? 1 : 0;
           }
@@ -1023,10 +1030,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHAD
 k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-#ifndef YK_SHADOW_NSEG
-#define YK_SHADOW_NSEG 1
-#endif
-  trace_body<false, YK_SHADOW_NSEG>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+  trace_body<false, 1>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 // trees with a leaf of 2^17 references or more (coop_leaves BIG)
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
