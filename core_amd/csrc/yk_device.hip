@@ -913,14 +913,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
         }
         if (done) {
           if (CLOSEST) {
-#ifdef YK_NT_HITS
-            typedef float f4h __attribute__((ext_vector_type(4)));
-            const f4h hv = {__int_as_float(st.prim >= 0 ? st.prim : -1), st.prim >= 0 ? st.Z : 0.f,
-                            st.prim >= 0 ? st.b1 : 0.f, st.prim >= 0 ? st.b2 : 0.f};
-            __builtin_nontemporal_store(hv, reinterpret_cast<f4h*>(hits + rid));
-#else
             hits[rid] = (st.prim >= 0) ? yk_hit{st.prim, st.Z, st.b1, st.b2} : yk_hit{-1, 0.f, 0.f, 0.f};
-#endif
           } else {
             occl[rid] = occ ? 1 : 0;
           }
@@ -1405,7 +1398,10 @@ __device__ __forceinline__ bool dirac_illum(const DLight& L, v3 P, v3& ldir, flo
 // wave, each wave goes on at once; else one per block, the wave totals
 // meeting in LDS between two barriers (every wave of the block then waits
 // for the atomic's round trip). Path-tracing shading per wave (round 3,
-// 1024-thread blocks: headline 2838 -> 2917 Mrays/s, C2 8384 -> 8356);
+// 1024-thread blocks: headline 2838 -> 2917 Mrays/s, C2 8384 -> 8356; after
+// the batch and store changes all-per-block measured 2954 / 8916 against
+// 2969 / 8822, and per-block in k_shade_primary or k_shade_bounce alone in
+// between);
 // the photon / final-gather kernels' launches are 33M threads each, and
 // per-block atomics measured 1068 -> 1263 Mrays/s there in round 1.
 #ifndef YK_PT_APPEND_WAVE
@@ -3010,7 +3006,9 @@ void upload_qmc() {
 
 int stack_depth(const yk_device* d) { return d->max_depth + 2; }
 
-// idle lanes a wave collects before it fetches new rays (YK_REFILL to tune)
+// idle lanes a wave collects before it fetches new rays (YK_REFILL to tune;
+// round 3: 16 / 24 / 32 both kernels 2867 / 2915 / 2902, the any-hit kernel
+// alone 2959 / 2971 / 2919 Mrays/s)
 int refill_min() {
   static const int v = [] {
     const char* e = std::getenv("YK_REFILL");
