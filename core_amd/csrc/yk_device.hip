@@ -103,6 +103,7 @@ struct DScene {
   int nlights;
   unsigned nnodes;  // node count, for the pop-time bounds guard
   unsigned chunk_max;  // largest ray hand-out chunk (64 for crowded-leaf scenes, whose rays are costly)
+  unsigned pool_div;   // hand-out chunks per wave (YK_POOL_CHUNKS; 4 for cache-resident trees)
   int uni;             // universal mode (vTriangle_t getSurface: b0 = 0; IntersectS t > tmin)
 };
 
@@ -779,7 +780,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 #endif
   const unsigned kPoolChunk = (unsigned)__builtin_amdgcn_readfirstlane((int)max(
       64u, min(min((unsigned)YK_POOL_CHUNK_MAX, S.chunk_max),
-               (unsigned)(n / ((long long)gridDim.x * YK_POOL_CHUNKS)) & ~63u)));
+               (unsigned)(n / ((long long)gridDim.x * max(1u, S.pool_div))) & ~63u)));
   unsigned xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
   constexpr unsigned kAll = (1u << NSEG) - 1u;
@@ -1373,39 +1374,36 @@ __device__ __forceinline__ bool dirac_illum(const DLight& L, v3 P, v3& ldir, flo
 // ------------------------------------------------------------ queues
 
 // Queue appends (wave_append2): every wave of a launch appends to the same
-// counter word, and the returning atomics serialise on it; one atomic per
-// block measured 1068 -> 1263 Mrays/s in round 1 (photon mapping, 32 gather
-// launches of 33M threads per batch) and 2008 -> 2038 (path tracing), and
-// round 3 found the path-tracing kernels faster per wave again once the
-// block-size changes below had cut their launch count.
-// Block sizes of the kernels that append to ray queues (fewer, larger blocks
-// = fewer returning atomics on the queue word). Measured: path-tracing
-// shading at 1024 threads 2038 -> 2075 Mrays/s (k_shade_primary at 512:
-// 2744 against 2811); the photon / final-gather kernels best at 512
-// (1261 -> 1274; 1024: 1240).
-#ifndef YK_SHADE_BLOCK
-#define YK_SHADE_BLOCK 1024  // round 3: 256 / 512 measured C2 7785-7977 / 7679-7827 against 7932-8090;
-                             // 512 / 256 for k_shade_bounce alone: headline and C2 unchanged; 256 with
-                             // k_shade_bounce at 5 / 6 waves per SIMD (6 / 23 VGPRs spilled): headline
-                             // 2892 / 2777, C2 8326 / 7865 against 2959 / 8429
+// counter word, and the returning atomics serialise on it. PER_WAVE: one
+// returning atomic per wave, and each wave goes on at once; else one per
+// block, the wave totals meeting in LDS between two barriers (every wave of
+// the block then waits for the atomic's round trip). Fewer, larger blocks
+// mean fewer atomics; smaller blocks let a CU overlap two blocks' waits.
+// Measured (round 3, final build, headline / C2 Mrays/s):
+//   k_shade_primary 512 per block, bounce kernels 1024 per wave  2949 / 8897  (kept)
+//   all 1024 per wave                                             2951 / 8801
+//   all 512 per block                                             2920 / 9035
+//   bounce kernels 512 per block / 512 per wave                   2920 / 8973, 2935 / 8798
+//   all 1024 per block                                            2954 / 8916
+//   all 256 per block                                             2880 / 8904
+// Earlier: bounce kernels at 5 / 6 waves per SIMD (6 / 23 VGPRs spilled)
+// 2892 / 2777 and 8326 / 7865 against 2959 / 8429. The photon / final-gather
+// kernels' launches are 33M threads each: 512 per block (1068 -> 1263
+// Mrays/s in round 1 against per wave; 1024: 1240).
+#ifndef YK_PRIMARY_BLOCK
+#define YK_PRIMARY_BLOCK 512  // k_shade_primary
+#endif
+#ifndef YK_PRIMARY_APPEND_WAVE
+#define YK_PRIMARY_APPEND_WAVE false
+#endif
+#ifndef YK_BOUNCE_BLOCK
+#define YK_BOUNCE_BLOCK 1024  // k_path_start, k_shade_bounce
+#endif
+#ifndef YK_BOUNCE_APPEND_WAVE
+#define YK_BOUNCE_APPEND_WAVE true
 #endif
 #ifndef YK_APPEND_BLOCK
-#define YK_APPEND_BLOCK 512
-#endif
-// Reserves m_s shadow-queue and m_b bounce-queue entries: the counter word
-// holds (bounce count << 32) | shadow count. Whole-wave call; returns each
-// lane's first index in both queues. PER_WAVE: one returning atomic per
-// wave, each wave goes on at once; else one per block, the wave totals
-// meeting in LDS between two barriers (every wave of the block then waits
-// for the atomic's round trip). Path-tracing shading per wave (round 3,
-// 1024-thread blocks: headline 2838 -> 2917 Mrays/s, C2 8384 -> 8356; after
-// the batch and store changes all-per-block measured 2954 / 8916 against
-// 2969 / 8822, and per-block in k_shade_primary or k_shade_bounce alone in
-// between);
-// the photon / final-gather kernels' launches are 33M threads each, and
-// per-block atomics measured 1068 -> 1263 Mrays/s there in round 1.
-#ifndef YK_PT_APPEND_WAVE
-#define YK_PT_APPEND_WAVE true
+#define YK_APPEND_BLOCK 512  // photon / final-gather kernels
 #endif
 #ifndef YK_PM_APPEND_WAVE
 #define YK_PM_APPEND_WAVE false
@@ -1889,7 +1887,7 @@ __device__ __forceinline__ yk_ray path_first_segment(const Batch& B, const Rende
 // first segment of sub-path 0 (appended to bounce queue 1).
 // Shading kernels run at the compiler's register choice (128 / 122 VGPRs, 4
 // waves per SIMD); forcing 5 or 6 spilled 124-200 B per lane and lost 2-4 %.
-__global__ void __launch_bounds__(YK_SHADE_BLOCK) k_shade_primary(DScene S, Batch B, RenderConst R, long long nc,
+__global__ void __launch_bounds__(YK_PRIMARY_BLOCK) k_shade_primary(DScene S, Batch B, RenderConst R, long long nc,
                                                        unsigned long long* __restrict__ qword) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = c < nc;
@@ -1965,7 +1963,7 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) k_shade_primary(DScene S, Batc
     if (!emit) B.wlast[c] = 0.f;
   }
   unsigned sbase, q;
-  wave_append2<YK_PT_APPEND_WAVE>(qword, valid ? (unsigned)nr : 0u, emit ? 1u : 0u, sbase, q);
+  wave_append2<YK_PRIMARY_APPEND_WAVE>(qword, valid ? (unsigned)nr : 0u, emit ? 1u : 0u, sbase, q);
   if (valid) flush_shadow(B, c, kend, nr, sbase, traced);
   if (emit) {
     st_ray(&B.q_rays[1][q], seg);
@@ -2039,7 +2037,7 @@ __global__ void __launch_bounds__(256) k_resolve_primary(Batch B, RenderConst R,
 
 // First segment of sub-paths isub >= 1 (sub-path 0 is fused into
 // k_shade_primary).
-__global__ void __launch_bounds__(YK_SHADE_BLOCK) k_path_start(DScene S, Batch B, RenderConst R, long long nc, int isub,
+__global__ void __launch_bounds__(YK_BOUNCE_BLOCK) k_path_start(DScene S, Batch B, RenderConst R, long long nc, int isub,
                                                     unsigned long long* __restrict__ qword) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = c < nc;
@@ -2058,7 +2056,7 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) k_path_start(DScene S, Batch B
     }
   }
   unsigned sbase, q;
-  wave_append2<YK_PT_APPEND_WAVE>(qword, 0u, emit ? 1u : 0u, sbase, q);
+  wave_append2<YK_BOUNCE_APPEND_WAVE>(qword, 0u, emit ? 1u : 0u, sbase, q);
   if (emit) {
     st_ray(&B.q_rays[1][q], r);
     B.q_owner[1][q] = (int)c;
@@ -2069,7 +2067,7 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) k_path_start(DScene S, Batch B
 // (pathtracer.cc:189-298): estimateOneDirectLight shadow rays, emission,
 // and the BSDF sample of the next segment. One thread per live path (entry
 // qi of the input bounce queue, owned by camera sample c).
-__global__ void __launch_bounds__(YK_SHADE_BLOCK) k_shade_bounce(DScene S, Batch B, RenderConst R,
+__global__ void __launch_bounds__(YK_BOUNCE_BLOCK) k_shade_bounce(DScene S, Batch B, RenderConst R,
                                                       const unsigned long long* __restrict__ qin_word, int depth,
                                                       int isub, int qin, unsigned long long* __restrict__ qword) {
   const long long nq = (long long)(*qin_word >> 32);  // live paths (device-side count)
@@ -2094,7 +2092,7 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) k_shade_bounce(DScene S, Batch
       B.pstate[c] = 0;
     }
     int src;
-    valid = pack_block<YK_SHADE_BLOCK>(valid && prim >= 0, src);
+    valid = pack_block<YK_BOUNCE_BLOCK>(valid && prim >= 0, src);
     qi = qb + src;
   }
   const long long c = valid ? B.q_owner[qin][qi] : 0;
@@ -2162,7 +2160,7 @@ __global__ void __launch_bounds__(YK_SHADE_BLOCK) k_shade_bounce(DScene S, Batch
     }
   }
   unsigned sbase, qn;
-  wave_append2<YK_PT_APPEND_WAVE>(qword, valid ? (unsigned)nr : 0u, emit_next ? 1u : 0u, sbase, qn);
+  wave_append2<YK_BOUNCE_APPEND_WAVE>(qword, valid ? (unsigned)nr : 0u, emit_next ? 1u : 0u, sbase, qn);
   if (valid) flush_shadow(B, c, kend, nr, sbase, traced);
   if (emit_next) {
     st_ray(&B.q_rays[qin ^ 1][qn], nxt);
@@ -3103,6 +3101,20 @@ constexpr size_t kMaxNodes = (1u << 30) - 2u;
 // leaves of this many references need the BIG owner keys (coop_leaves)
 constexpr uint32_t kBigLeaf = 1u << 17;
 
+// Ray hand-out per scene: crowded-leaf trees (costly, uneven rays) take
+// 64-ray chunks; a tree small enough to stay in an XCD's L2 (at most 2^16
+// nodes: 1.5 MB of node packets) has cheap rays whose waves grab chunks
+// often, so every wave takes about 4 chunks of a launch instead of 16
+// (C2, the 36-tri Cornell box: round 3 measured 4 against 16 at +2.2 %, the
+// headline 1M tree -0.6 %, 32 chunks -5.4 % on C2).
+#ifndef YK_SMALL_TREE_CHUNKS
+#define YK_SMALL_TREE_CHUNKS YK_POOL_CHUNKS  // pending measurement
+#endif
+void set_handout(yk_device* d, size_t nn) {
+  d->S.chunk_max = d->crowded_leaves ? 64u : (unsigned)YK_POOL_CHUNK_MAX;
+  d->S.pool_div = (!d->crowded_leaves && nn <= (1u << 16)) ? (unsigned)YK_SMALL_TREE_CHUNKS : (unsigned)YK_POOL_CHUNKS;
+}
+
 // Traversal copies of the resident tree: the leaf-ordered triangles
 // (k_gather_leaf_tris) and the node packets (k_pack_nodes).
 // Callers check the node count (kMaxNodes) before they touch any resident
@@ -3313,7 +3325,7 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
     const long long filled = (long long)S.tree.stats.leaves - S.tree.stats.empty_leaves;
     const double mean = filled > 0 ? (double)S.tree.stats.leaf_prims / (double)filled : 0.0;
     d->crowded_leaves = mean > crowd;
-    d->S.chunk_max = d->crowded_leaves ? 64u : (unsigned)YK_POOL_CHUNK_MAX;
+    set_handout(d, nn);
   }
   d->nlights = (int)S.light_states.size();
   d->ntris = nt;
@@ -3791,14 +3803,14 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
         HIPCHK(hipMemsetAsync(d->spec_words.p, 0, d->spec_words.n * sizeof(unsigned long long), P.stream));
         launch = 0;
         trace(true, Bc.p_rays, nullptr, RayCount{nullptr, 0, n}, Bc.p_hits, nullptr);
-        hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(n, YK_SHADE_BLOCK)), dim3(YK_SHADE_BLOCK), 0, P.stream, d->S, Bc, Rc, n, qw(0, 0));
+        hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(n, YK_PRIMARY_BLOCK)), dim3(YK_PRIMARY_BLOCK), 0, P.stream, d->S, Bc, Rc, n, qw(0, 0));
         HIPCHK(hipGetLastError());
         trace(false, Bc.s_rays, Bc.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, Bc.s_occl);
         hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(n)), dim3(256), 0, P.stream, Bc, Rc, n);
         HIPCHK(hipGetLastError());
         for (int isub = 0; isub < (path ? nsub : 0); ++isub) {
           if (isub > 0) {
-            hipLaunchKernelGGL(k_path_start, dim3(grid_for(n, YK_SHADE_BLOCK)), dim3(YK_SHADE_BLOCK), 0, P.stream, d->S, Bc, Rc, n, isub,
+            hipLaunchKernelGGL(k_path_start, dim3(grid_for(n, YK_BOUNCE_BLOCK)), dim3(YK_BOUNCE_BLOCK), 0, P.stream, d->S, Bc, Rc, n, isub,
                                qw(isub, 0));
             HIPCHK(hipGetLastError());
           }
@@ -3807,7 +3819,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
             const unsigned long long* in_w = qw(isub, depth - 1);
             unsigned long long* out_w = qw(isub, depth);
             trace(true, Bc.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, Bc.q_hits[qin], nullptr);
-            hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(n, YK_SHADE_BLOCK)), dim3(YK_SHADE_BLOCK), 0, P.stream, d->S, Bc, Rc, in_w, depth,
+            hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(n, YK_BOUNCE_BLOCK)), dim3(YK_BOUNCE_BLOCK), 0, P.stream, d->S, Bc, Rc, in_w, depth,
                                isub, qin, out_w);
             HIPCHK(hipGetLastError());
             trace(false, Bc.s_rays, Bc.s_idx, RayCount{out_w, 0, 0}, nullptr, Bc.s_occl);
@@ -3852,7 +3864,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     }
     if (!d->spec) {
     trace(true, B.p_rays, nullptr, RayCount{nullptr, 0, nc}, B.p_hits, nullptr);
-    hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(nc, YK_SHADE_BLOCK)), dim3(YK_SHADE_BLOCK), 0, P.stream, d->S, B, R, nc, qw(0, 0));
+    hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(nc, YK_PRIMARY_BLOCK)), dim3(YK_PRIMARY_BLOCK), 0, P.stream, d->S, B, R, nc, qw(0, 0));
     HIPCHK(hipGetLastError());
     trace(false, B.s_rays, B.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, B.s_occl);
     hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
@@ -3863,7 +3875,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     // accumulated in the reference's order (pathtracer.cc:164-298)
     for (int isub = 0; isub < (path ? nsub : 0); ++isub) {
       if (isub > 0) {  // sub-path 0's first segment came out of k_shade_primary
-        hipLaunchKernelGGL(k_path_start, dim3(grid_for(nc, YK_SHADE_BLOCK)), dim3(YK_SHADE_BLOCK), 0, P.stream, d->S, B, R, nc, isub,
+        hipLaunchKernelGGL(k_path_start, dim3(grid_for(nc, YK_BOUNCE_BLOCK)), dim3(YK_BOUNCE_BLOCK), 0, P.stream, d->S, B, R, nc, isub,
                            qw(isub, 0));
         HIPCHK(hipGetLastError());
       }
@@ -3872,7 +3884,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
         const unsigned long long* in_w = qw(isub, depth - 1);
         unsigned long long* out_w = qw(isub, depth);
         trace(true, B.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, B.q_hits[qin], nullptr);
-        hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(nc, YK_SHADE_BLOCK)), dim3(YK_SHADE_BLOCK), 0, P.stream, d->S, B, R, in_w, depth, isub,
+        hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(nc, YK_BOUNCE_BLOCK)), dim3(YK_BOUNCE_BLOCK), 0, P.stream, d->S, B, R, in_w, depth, isub,
                            qin, out_w);
         HIPCHK(hipGetLastError());
         trace(false, B.s_rays, B.s_idx, RayCount{out_w, 0, 0}, nullptr, B.s_occl);
