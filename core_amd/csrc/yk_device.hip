@@ -3108,7 +3108,7 @@ constexpr uint32_t kBigLeaf = 1u << 17;
 // (C2, the 36-tri Cornell box: round 3 measured 4 against 16 at +2.2 %, the
 // headline 1M tree -0.6 %, 32 chunks -5.4 % on C2).
 #ifndef YK_SMALL_TREE_CHUNKS
-#define YK_SMALL_TREE_CHUNKS YK_POOL_CHUNKS  // pending measurement
+#define YK_SMALL_TREE_CHUNKS 4  // C2: 16 / 4 / 2 chunks 8602 / 8729 / 8774 Mrays/s (one box, 2 reps)
 #endif
 void set_handout(yk_device* d, size_t nn) {
   d->S.chunk_max = d->crowded_leaves ? 64u : (unsigned)YK_POOL_CHUNK_MAX;
