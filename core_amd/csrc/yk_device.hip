@@ -779,7 +779,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 #define YK_POOL_CHUNK_MAX 512
 #endif
   const unsigned kPoolChunk = (unsigned)__builtin_amdgcn_readfirstlane((int)max(
-      64u, min(min((unsigned)YK_POOL_CHUNK_MAX, S.chunk_max),
+      64u, min(S.chunk_max,
                (unsigned)(n / ((long long)gridDim.x * max(1u, S.pool_div))) & ~63u)));
   unsigned xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
@@ -3111,8 +3111,9 @@ constexpr uint32_t kBigLeaf = 1u << 17;
 #define YK_SMALL_TREE_CHUNKS 4  // C2: 16 / 4 / 2 chunks 8602 / 8729 / 8774 Mrays/s (one box, 2 reps)
 #endif
 void set_handout(yk_device* d, size_t nn) {
-  d->S.chunk_max = d->crowded_leaves ? 64u : (unsigned)YK_POOL_CHUNK_MAX;
-  d->S.pool_div = (!d->crowded_leaves && nn <= (1u << 16)) ? (unsigned)YK_SMALL_TREE_CHUNKS : (unsigned)YK_POOL_CHUNKS;
+  const bool small = !d->crowded_leaves && nn <= (1u << 16);
+  d->S.chunk_max = d->crowded_leaves ? 64u : (unsigned)YK_POOL_CHUNK_MAX;  // 2048 for small trees: C2 unchanged
+  d->S.pool_div = small ? (unsigned)YK_SMALL_TREE_CHUNKS : (unsigned)YK_POOL_CHUNKS;
 }
 
 // Traversal copies of the resident tree: the leaf-ordered triangles
