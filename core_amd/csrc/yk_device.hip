@@ -103,7 +103,6 @@ struct DScene {
   int nlights;
   unsigned nnodes;  // node count, for the pop-time bounds guard
   unsigned chunk_max;  // largest ray hand-out chunk (64 for crowded-leaf scenes, whose rays are costly)
-  unsigned pool_div;   // hand-out chunks per wave (YK_POOL_CHUNKS; 4 for cache-resident trees)
   int uni;             // universal mode (vTriangle_t getSurface: b0 = 0; IntersectS t > tmin)
 };
 
@@ -779,8 +778,8 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 #define YK_POOL_CHUNK_MAX 512
 #endif
   const unsigned kPoolChunk = (unsigned)__builtin_amdgcn_readfirstlane((int)max(
-      64u, min(S.chunk_max,
-               (unsigned)(n / ((long long)gridDim.x * max(1u, S.pool_div))) & ~63u)));
+      64u, min(min((unsigned)YK_POOL_CHUNK_MAX, S.chunk_max),
+               (unsigned)(n / ((long long)gridDim.x * YK_POOL_CHUNKS)) & ~63u)));
   unsigned xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
   constexpr unsigned kAll = (1u << NSEG) - 1u;
@@ -3102,18 +3101,13 @@ constexpr size_t kMaxNodes = (1u << 30) - 2u;
 constexpr uint32_t kBigLeaf = 1u << 17;
 
 // Ray hand-out per scene: crowded-leaf trees (costly, uneven rays) take
-// 64-ray chunks; a tree small enough to stay in an XCD's L2 (at most 2^16
-// nodes: 1.5 MB of node packets) has cheap rays whose waves grab chunks
-// often, so every wave takes about 4 chunks of a launch instead of 16
-// (C2, the 36-tri Cornell box: round 3 measured 4 against 16 at +2.2 %, the
-// headline 1M tree -0.6 %, 32 chunks -5.4 % on C2).
-#ifndef YK_SMALL_TREE_CHUNKS
-#define YK_SMALL_TREE_CHUNKS 4  // C2: 16 / 4 / 2 chunks 8602 / 8729 / 8774 Mrays/s (one box, 2 reps)
-#endif
+// 64-ray chunks. (Round 3 also tried 4 chunks per wave instead of 16 for trees
+// of at most 2^16 nodes, as a per-scene value: the runtime divisor made the
+// closest-hit kernel spill 9 VGPRs instead of 4, headline 2904 against 2950,
+// for no C2 gain in the same A/B: 8927 against 8925.)
 void set_handout(yk_device* d, size_t nn) {
-  const bool small = !d->crowded_leaves && nn <= (1u << 16);
-  d->S.chunk_max = d->crowded_leaves ? 64u : (unsigned)YK_POOL_CHUNK_MAX;  // 2048 for small trees: C2 unchanged
-  d->S.pool_div = small ? (unsigned)YK_SMALL_TREE_CHUNKS : (unsigned)YK_POOL_CHUNKS;
+  (void)nn;
+  d->S.chunk_max = d->crowded_leaves ? 64u : (unsigned)YK_POOL_CHUNK_MAX;
 }
 
 // Traversal copies of the resident tree: the leaf-ordered triangles
