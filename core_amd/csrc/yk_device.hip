@@ -1379,10 +1379,17 @@ __device__ __forceinline__ bool dirac_illum(const DLight& L, v3 P, v3& ldir, flo
 // the block then waits for the atomic's round trip). Fewer, larger blocks
 // mean fewer atomics; smaller blocks let a CU overlap two blocks' waits.
 // Measured (round 3, final build, headline / C2 Mrays/s):
-//   k_shade_primary 512 per block, bounce kernels 1024 per wave  2949 / 8897  (kept)
+//   k_shade_primary 512 per block, bounce kernels 512 per wave   2970 / 8872  (kept;
+//     5 runs on 2 boxes, each 2969-2980, against 2942-2957 / 8815 for 1024 per wave)
+//   k_shade_primary 512 per block, bounce kernels 1024 per wave  2949 / 8897
+//     (same 2 boxes: 2945 / 8943 with the bounce kernels 1024 per block)
+//   bounce kernels 256 per wave                                   2874 / 8833
+//   k_shade_primary 1024 / 256 per block, 1024 per wave (3 runs,
+//     against 2967 / 8876 on that box)        2894 / 8815, 2940 / 8770, 2945 / 8774
+//   k_shade_primary 512 per wave, bounce kernels 512 per wave    2947 / 8826
 //   all 1024 per wave                                             2951 / 8801
 //   all 512 per block                                             2920 / 9035
-//   bounce kernels 512 per block / 512 per wave                   2920 / 8973, 2935 / 8798
+//   bounce kernels 512 per block                                  2920 / 8973
 //   all 1024 per block                                            2954 / 8916
 //   all 256 per block                                             2880 / 8904
 // Earlier: bounce kernels at 5 / 6 waves per SIMD (6 / 23 VGPRs spilled)
@@ -1396,7 +1403,7 @@ __device__ __forceinline__ bool dirac_illum(const DLight& L, v3 P, v3& ldir, flo
 #define YK_PRIMARY_APPEND_WAVE false
 #endif
 #ifndef YK_BOUNCE_BLOCK
-#define YK_BOUNCE_BLOCK 1024  // k_path_start, k_shade_bounce
+#define YK_BOUNCE_BLOCK 512  // k_path_start, k_shade_bounce
 #endif
 #ifndef YK_BOUNCE_APPEND_WAVE
 #define YK_BOUNCE_APPEND_WAVE true
