@@ -2775,6 +2775,7 @@ struct yk_device {
   void* abort_user = nullptr;
   bool big_leaves = false;  // the resident tree has a leaf of 2^17 references or more: *_big kernels
   bool crowded_leaves = false;  // mean references per non-empty leaf above YK_CROWDED_LEAF: 64-ray hand-out chunks
+  int refill = 24;  // idle lanes before a traversal wave refills (set_handout)
   int per_cu_ts = 1;
   // node store of the specular recursion (k_finish_spec / k_spawn / k_fold)
   DBuf<float> nE, nD, nP, nrcol, nalpha, nmalpha;
@@ -3010,14 +3011,13 @@ void upload_qmc() {
 
 int stack_depth(const yk_device* d) { return d->max_depth + 2; }
 
-// idle lanes a wave collects before it fetches new rays (YK_REFILL to tune;
-// round 3: 16 / 24 / 32 both kernels 2867 / 2915 / 2902, the any-hit kernel
-// alone 2959 / 2971 / 2919 Mrays/s)
-int refill_min() {
+// YK_REFILL (1-64) overrides the per-scene refill threshold (set_handout);
+// 0 = none
+int refill_env() {
   static const int v = [] {
     const char* e = std::getenv("YK_REFILL");
     const int r = e ? std::atoi(e) : 0;
-    return (r >= 1 && r <= 64) ? r : 24;
+    return (r >= 1 && r <= 64) ? r : 0;
   }();
   return v;
 }
@@ -3037,7 +3037,7 @@ void enqueue_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* id
                       : (d->S.uni ? (d->big_leaves ? k_trace_shadow_big_uni : k_trace_shadow_uni)
                                   : (d->big_leaves ? k_trace_shadow_big : k_trace_shadow));
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays, idx, n, hits, occ, work, acc,
-                     P.ovf.p, ovf_depth, refill_min());
+                     P.ovf.p, ovf_depth, d->refill);
   HIPCHK(hipGetLastError());
   if (ev1) HIPCHK(hipEventRecord(ev1, P.stream));
 }
@@ -3051,7 +3051,7 @@ void enqueue_trace_ts(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned*
   P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
   if (ev0) HIPCHK(hipEventRecord(ev0, P.stream));
   hipLaunchKernelGGL(k_trace_shadow_ts, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays, idx, n, occ, filt,
-                     max_depth, work, acc, P.ovf.p, ovf_depth, refill_min());
+                     max_depth, work, acc, P.ovf.p, ovf_depth, d->refill);
   HIPCHK(hipGetLastError());
   if (ev1) HIPCHK(hipEventRecord(ev1, P.stream));
 }
@@ -3108,12 +3108,17 @@ constexpr size_t kMaxNodes = (1u << 30) - 2u;
 constexpr uint32_t kBigLeaf = 1u << 17;
 
 // Ray hand-out per scene: crowded-leaf trees (costly, uneven rays) take
-// 64-ray chunks. (Round 3 also tried 4 chunks per wave instead of 16 for trees
+// 64-ray chunks. Refill threshold (idle lanes a wave collects before it
+// fetches new rays): 24, or 40 for trees of at most 2^16 nodes, whose cheap
+// rays make the refill's two dependent loads a larger share of a wave's time.
+// Round 3, headline (1M tris) at 16 / 24 / 32: 2867 / 2915 / 2902 Mrays/s
+// (any-hit kernel alone 2959 / 2971 / 2919); C2 (36 tris) at 16 / 24 / 32 /
+// 40 / 48 / 56 / 64: 8442 / 8669 / 8710 / 8791 / 8788 / 8716 / 8426. (Round 3 also tried 4 chunks per wave instead of 16 for trees
 // of at most 2^16 nodes, as a per-scene value: the runtime divisor made the
 // closest-hit kernel spill 9 VGPRs instead of 4, headline 2904 against 2950,
 // for no C2 gain in the same A/B: 8927 against 8925.)
 void set_handout(yk_device* d, size_t nn) {
-  (void)nn;
+  d->refill = refill_env() ? refill_env() : (nn <= (1u << 16) ? 40 : 24);
   d->S.chunk_max = d->crowded_leaves ? 64u : (unsigned)YK_POOL_CHUNK_MAX;
 }
 
