@@ -2776,6 +2776,7 @@ struct yk_device {
   bool big_leaves = false;  // the resident tree has a leaf of 2^17 references or more: *_big kernels
   bool crowded_leaves = false;  // mean references per non-empty leaf above YK_CROWDED_LEAF: 64-ray hand-out chunks
   int refill = 24;  // idle lanes before a traversal wave refills (set_handout)
+  int refill_shadow = 24;  // the same for the any-hit kernels
   int per_cu_ts = 1;
   // node store of the specular recursion (k_finish_spec / k_spawn / k_fold)
   DBuf<float> nE, nD, nP, nrcol, nalpha, nmalpha;
@@ -3037,7 +3038,7 @@ void enqueue_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* id
                       : (d->S.uni ? (d->big_leaves ? k_trace_shadow_big_uni : k_trace_shadow_uni)
                                   : (d->big_leaves ? k_trace_shadow_big : k_trace_shadow));
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays, idx, n, hits, occ, work, acc,
-                     P.ovf.p, ovf_depth, d->refill);
+                     P.ovf.p, ovf_depth, CLOSEST ? d->refill : d->refill_shadow);
   HIPCHK(hipGetLastError());
   if (ev1) HIPCHK(hipEventRecord(ev1, P.stream));
 }
@@ -3051,7 +3052,7 @@ void enqueue_trace_ts(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned*
   P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
   if (ev0) HIPCHK(hipEventRecord(ev0, P.stream));
   hipLaunchKernelGGL(k_trace_shadow_ts, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays, idx, n, occ, filt,
-                     max_depth, work, acc, P.ovf.p, ovf_depth, d->refill);
+                     max_depth, work, acc, P.ovf.p, ovf_depth, d->refill_shadow);
   HIPCHK(hipGetLastError());
   if (ev1) HIPCHK(hipEventRecord(ev1, P.stream));
 }
@@ -3109,16 +3110,22 @@ constexpr uint32_t kBigLeaf = 1u << 17;
 
 // Ray hand-out per scene: crowded-leaf trees (costly, uneven rays) take
 // 64-ray chunks. Refill threshold (idle lanes a wave collects before it
-// fetches new rays): 24, or 40 for trees of at most 2^16 nodes, whose cheap
-// rays make the refill's two dependent loads a larger share of a wave's time.
-// Round 3, headline (1M tris) at 16 / 24 / 32: 2867 / 2915 / 2902 Mrays/s
-// (any-hit kernel alone 2959 / 2971 / 2919); C2 (36 tris) at 16 / 24 / 32 /
-// 40 / 48 / 56 / 64: 8442 / 8669 / 8710 / 8791 / 8788 / 8716 / 8426. (Round 3 also tried 4 chunks per wave instead of 16 for trees
+// fetches new rays): 24, and 48 for the any-hit kernels on trees of at most
+// 2^16 nodes, whose cheap shadow rays make the refill's two dependent loads a
+// larger share of a wave's time. Round 3, headline (1M tris) at 16 / 24 / 32:
+// 2867 / 2915 / 2902 Mrays/s (any-hit kernel alone 2959 / 2971 / 2919); C2
+// (36 tris), both kernels at 16 / 24 / 32 / 40 / 48 / 56 / 64: 8442 / 8669 /
+// 8710 / 8791 / 8788 / 8716 / 8426; closest : any-hit at 40:40 / 24:40 /
+// 24:48 / 32:48 / 24:56 (3 runs each, one box): 8784 / 8851 / 8938 / 8928 /
+// 8889. YK_REFILL / YK_REFILL_SHADOW override (tuning). (Round 3 also tried 4 chunks per wave instead of 16 for trees
 // of at most 2^16 nodes, as a per-scene value: the runtime divisor made the
 // closest-hit kernel spill 9 VGPRs instead of 4, headline 2904 against 2950,
 // for no C2 gain in the same A/B: 8927 against 8925.)
 void set_handout(yk_device* d, size_t nn) {
-  d->refill = refill_env() ? refill_env() : (nn <= (1u << 16) ? 40 : 24);
+  const char* e = std::getenv("YK_REFILL_SHADOW");
+  const int rs = e ? std::atoi(e) : 0;
+  d->refill = refill_env() ? refill_env() : 24;
+  d->refill_shadow = (rs >= 1 && rs <= 64) ? rs : (refill_env() ? refill_env() : (nn <= (1u << 16) ? 48 : 24));
   d->S.chunk_max = d->crowded_leaves ? 64u : (unsigned)YK_POOL_CHUNK_MAX;
 }
 
