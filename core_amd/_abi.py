@@ -135,7 +135,8 @@ class yk_stats(C.Structure):
                 ("shadow_nodes", C.c_uint64), ("shadow_tris", C.c_uint64),
                 ("camera_samples", C.c_uint64), ("ms_total", C.c_double),
                 ("ms_closest", C.c_double), ("ms_shadow", C.c_double),
-                ("closest_launches", C.c_uint64), ("shadow_launches", C.c_uint64)]
+                ("closest_launches", C.c_uint64), ("shadow_launches", C.c_uint64),
+                ("ms_reduce", C.c_double)]
 
 
 P = C.c_void_p
@@ -200,6 +201,7 @@ SIGNATURES = {
     "yk_photon_export": (C.c_int, [P, i32, fp, i32, i32p]),
     "yk_device_build_tree": (C.c_int, [P, P, i32, C.POINTER(yk_tree_info)]),
     "yk_device_export_tree": (C.c_int, [P, u32p, i64, u32p, i64, C.POINTER(i64), C.POINTER(i64)]),
+    "yk_device_debug_set_node": (C.c_int, [P, i64, C.c_uint32, C.c_uint32]),
 }
 
 _lib = None
@@ -219,6 +221,8 @@ def lib():
             raise ImportError(f"{LIB_PATH} missing: run __graft_entry__.build() (no fallback path exists)")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("YK_LIB") and not hasattr(L, name):
+                continue  # an older tuning build (A/B runs) may predate a symbol
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

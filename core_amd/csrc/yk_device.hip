@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -101,7 +102,9 @@ struct DScene {
   const float* vn;       // 9 floats per prim: getSurface's vertex normals (smooth scenes only)
   float bound[6];
   int nlights;
-  unsigned nnodes;  // node count, for the pop-time bounds guard
+  unsigned nnodes;  // node count, for the pop-time bounds guard and the per-ray watchdog
+  unsigned depth_cap;  // tree depth + 2: node visits of one valid descent and stack entries of a
+                       // valid traversal (the watchdog's bounds)
   unsigned chunk_max;  // largest ray hand-out chunk (64 for crowded-leaf scenes, whose rays are costly)
   int uni;             // universal mode (vTriangle_t getSurface: b0 = 0; IntersectS t > tmin)
 };
@@ -174,29 +177,54 @@ __device__ __forceinline__ bool bound_cross(const float* bb, v3 from, v3 dir, fl
 // entry stores t itself. The top kStackLds entries of every lane live in an
 // LDS ring; deeper ones spill to a global overflow area (rare: a 1M-tri tree
 // has depth ~40 but a ray rarely holds more than a dozen pending exits).
-constexpr int kStackLds = 8;  // LDS ring depth per lane (16 measured slower: 1807 vs 2054, round 1)
+constexpr int kStackLds = 8;
+// Tree depth limit: the reference caps maxDepth at KD_MAX_STACK = 64
+// (kdtree.cc:42), and yk_device_upload refuses deeper trees, so a descent of
+// a valid tree never takes more than kDescTrips trips of the descent loop (a
+// compile-time bound: the watchdog adds no register to the loop)
+constexpr int kMaxTreeDepth = 64;
+constexpr unsigned kDescTrips = kMaxTreeDepth + 2;
+// The cooperative kernels keep no hit record in registers: a closest hit has
+// been found iff Z < dist (every accepted hit lowers Z below its start,
+// dist), and its (t, b1, b2, prim) stay in the lane's LDS candidate slot
+// (coop_leaves); a corrupt traversal marks the lane with sp = kSpError.
+constexpr int kSpError = -(1 << 20);  // LDS ring depth per lane (16 measured slower: 1807 vs 2054, round 1)
 
 struct LaneStack {
-  uint2* lds;  // [kStackLds][64]
-  uint2* ovf;  // this lane's overflow entries, contiguous (one cache line holds 8)
+  uint2* lds;    // [kStackLds][64]
+  uint2* ovf;    // overflow area of the launch: each lane's entries contiguous (one cache line holds 8)
+  unsigned depth;  // overflow entries per lane
   int lane;
+  // the lane's overflow entry k, addressed on use (rare) instead of a 64-bit
+  // per-lane pointer kept in registers
+  __device__ __forceinline__ uint2* ovf_at(int k) const {
+    return ovf + ((size_t)(blockIdx.x * 64u + (unsigned)lane) * depth + (unsigned)k);
+  }
   __device__ __forceinline__ void push(int sp, uint2 e) const {
     uint2* slot = lds + (sp & (kStackLds - 1)) * 64 + lane;
-    if (sp >= kStackLds) ovf[sp - kStackLds] = *slot;
+    if (sp >= kStackLds) *ovf_at(sp - kStackLds) = *slot;
     *slot = e;
   }
   __device__ __forceinline__ uint2 pop(int sp) const {  // sp = index of the entry to pop
     uint2* slot = lds + (sp & (kStackLds - 1)) * 64 + lane;
     const uint2 e = *slot;
-    if (sp >= kStackLds) *slot = ovf[sp - kStackLds];
+    if (sp >= kStackLds) *slot = *ovf_at(sp - kStackLds);
     return e;
   }
 };
+// Entry and exit points are kept implicitly (no 3-float points in
+// registers): the reference's pb of an entry / exit is from + t*dir on every
+// axis but the one of the split plane it lies on, which is the split itself
+// (kdtree.cc:740-760 computes it so), so a point is (t, split, code) with
+// code 0-2 that axis, 3 none (the tree-bound exit) and, for the entry only,
+// 4 = the ray origin (an entry t < 0, kdtree.cc:699). One coordinate is
+// rebuilt on use with the same float operations, so it is bit-identical to
+// the stored point. (5 registers fewer than two stored points.)
 struct Trav {
   v3 o, d, inv;
   float tmin, dist;
-  float en_t, ex_t, ex_split;
-  v3 en_pb, ex_pb;
+  float en_t, en_split, ex_t, ex_split;
+  uint32_t en_code;
   uint32_t ex_w;  // (exit far node + 1) | axis code << 30; node -1 = the initial exit
   int node, sp;
   float Z, b1, b2;
@@ -221,11 +249,10 @@ __device__ __forceinline__ float sel3(v3 v, uint32_t ax) { return ax == 0u ? v.x
 // registers, never of addresses)
 __device__ __forceinline__ float sel3m(v3 v, bool a0, bool a1) { return a0 ? v.x : (a1 ? v.y : v.z); }
 
-// pb of the current exit: pb[code] = split, other axes from + t*dir
-__device__ __forceinline__ void exit_pb(Trav& st) {
-  const uint32_t code = st.ex_w >> 30;
-  const float x = st.o.x + st.ex_t * st.d.x, y = st.o.y + st.ex_t * st.d.y, z = st.o.z + st.ex_t * st.d.z;
-  st.ex_pb = V3(code == 0u ? st.ex_split : x, code == 1u ? st.ex_split : y, code == 2u ? st.ex_split : z);
+// coordinate ax of an implicit point (t, split, code): oa, da = from[ax], dir[ax]
+__device__ __forceinline__ float pt_coord(float t, float split, uint32_t code, uint32_t ax, float oa, float da) {
+  const float v = oa + t * da;
+  return code == ax ? split : (code == 4u ? oa : v);
 }
 
 // scene_t::intersect (scene.cc:852-879) / isShadowed (scene.cc:881-902)
@@ -258,11 +285,11 @@ __device__ __forceinline__ bool trav_begin(const DScene& S, Trav& st, const yk_r
   if (!bound_cross(S.bound, st.o, st.d, a, b, st.dist)) return false;
   st.inv = V3(1.0f / st.d.x, 1.0f / st.d.y, 1.0f / st.d.z);
   st.en_t = a;
-  st.en_pb = (a >= 0.0f) ? vadd(st.o, vmul(a, st.d)) : st.o;
+  st.en_split = a;
+  st.en_code = (a >= 0.0f) ? 3u : 4u;  // from + a*dir, or the origin itself
   st.ex_t = b;
   st.ex_split = b;          // code 3 entries carry t
   st.ex_w = 3u << 30;       // node -1, code 3
-  exit_pb(st);
   st.node = 0;
   st.sp = 0;
   return true;
@@ -339,23 +366,29 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
   uint2 nd = make_uint2(q.a, q.b), nx = make_uint2(q.c, q.d);
   bool have = true;
   nnodes++;
+  const unsigned n0 = nnodes;
   for (;;) {
     const uint32_t ax = nd.y & 3u;
     if (ax == 3u) break;
+    if (nnodes - n0 > S.depth_cap || st.sp > (int)S.depth_cap) {  // watchdog: no valid descent is this deep
+      st.prim = -2;
+      return true;
+    }
     const float split = __uint_as_float(nd.x);
     const int right = (int)(nd.y >> 2);
-    const float enp = sel3(st.en_pb, ax), exq = sel3(st.ex_pb, ax);
+    const float oa = sel3(st.o, ax), da = sel3(st.d, ax);
+    const float enp = pt_coord(st.en_t, st.en_split, st.en_code, ax, oa, da);
+    const float exq = pt_coord(st.ex_t, st.ex_split, st.ex_w >> 30, ax, oa, da);
     const bool left_first = enp <= split;
     const bool push = left_first ? !(exq <= split) : !(split < exq);
     if (push) {
       const int far_ = left_first ? right : node + 1;
-      const float t = (split - sel3(st.o, ax)) * sel3(st.inv, ax);
+      const float t = (split - oa) * sel3(st.inv, ax);
       stk.push(st.sp, make_uint2(__float_as_uint(st.ex_split), st.ex_w));
       st.sp++;
       st.ex_t = t;
       st.ex_split = split;
       st.ex_w = (uint32_t)(far_ + 1) | (ax << 30);
-      exit_pb(st);
     }
     if (left_first && have) {
       node = node + 1;
@@ -385,10 +418,15 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
   if (CLOSEST && st.prim >= 0 && st.Z <= st.ex_t) return true;
   // pop: entry := exit, exit := previous exit
   st.en_t = st.ex_t;
-  st.en_pb = st.ex_pb;
+  st.en_split = st.ex_split;
+  st.en_code = st.ex_w >> 30;
   st.node = (int)(st.ex_w & 0x3FFFFFFFu) - 1;
   if (st.node < 0) return true;
-  if ((unsigned)st.node >= S.nnodes || st.sp <= 0) {  // corrupt state: never index out of the tree
+  // corrupt state (never index out of the tree or the stack area): a node
+  // outside the tree, or a stack outside [1, depth_cap] -- a valid traversal
+  // holds at most depth_cap entries, and the overflow area has room for one
+  // more descent's pushes than that
+  if ((unsigned)st.node >= S.nnodes || (unsigned)(st.sp - 1) >= S.depth_cap) {
     st.prim = -2;
     return true;
   }
@@ -398,7 +436,6 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
   st.ex_w = e.y;
   const uint32_t code = e.y >> 30;
   st.ex_t = (code == 3u) ? st.ex_split : (st.ex_split - sel3(st.o, code)) * sel3(st.inv, code);
-  exit_pb(st);
   return false;
 }
 
@@ -478,7 +515,9 @@ __device__ __forceinline__ uint32_t desc_decide(Trav& st, const LaneStack& stk, 
   const float split = __uint_as_float(nd.x);
   const uint32_t right = nd.y >> 2;
   const bool a0 = ax == 0u, a1 = ax == 1u;
-  const float enp = sel3m(st.en_pb, a0, a1), exq = sel3m(st.ex_pb, a0, a1);
+  const float oa = sel3m(st.o, a0, a1), da = sel3m(st.d, a0, a1);
+  const float enp = pt_coord(st.en_t, st.en_split, st.en_code, ax, oa, da);
+  const float exq = pt_coord(st.ex_t, st.ex_split, st.ex_w >> 30, ax, oa, da);
   const bool left_first = enp <= split;
   // far child pushed unless the exit stays on the near side; evaluated on
   // wave masks (SALU) instead of per-lane 0/1 selects
@@ -488,15 +527,12 @@ __device__ __forceinline__ uint32_t desc_decide(Trav& st, const LaneStack& stk, 
   const bool push = __builtin_amdgcn_inverse_ballot_w64((m_lf & ~m_c1) | (~m_lf & ~m_c2));
   if (push) {
     const uint32_t far_ = left_first ? right : node + 1u;
-    const float t = (split - sel3m(st.o, a0, a1)) * sel3m(st.inv, a0, a1);
+    const float t = (split - oa) * sel3m(st.inv, a0, a1);
     stk.push(st.sp, make_uint2(__float_as_uint(st.ex_split), st.ex_w));
     st.sp++;
     st.ex_t = t;
     st.ex_split = split;
     st.ex_w = (far_ + 1u) | (ax << 30);
-    // exit point (exit_pb with the axis masks at hand)
-    const float x = st.o.x + t * st.d.x, y = st.o.y + t * st.d.y, z = st.o.z + t * st.d.z;
-    st.ex_pb = V3(a0 ? split : x, a1 ? split : y, (a0 || a1) ? z : split);
   }
   return left_first ? node + 1u : right;
 }
@@ -530,6 +566,12 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
   // current node and resume in the next iteration, so the wave does not loop
   // to its longest descent while the other lanes idle
   const unsigned started = kFrac ? (unsigned)__popcll(__builtin_amdgcn_ballot_w64(true)) : 0u;
+  // watchdog: every trip of this loop takes each descending lane at least one
+  // level down, so in a valid tree no descent outlasts kDescTrips trips (a
+  // wave-uniform count against a constant). A longer one is cut there like a
+  // paused descent; a lane caught in a cycle keeps visiting nodes, which the
+  // per-ray node-visit bound in trace_body turns into an error.
+  unsigned trips = 0;
   // wave-uniform loop: the exit test is a ballot, and lanes whose descent
   // ended sit out the body under the exec mask. (A divergent loop exit makes
   // the compiler copy the descent's live-out registers every step, 13 of ~27
@@ -539,6 +581,7 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
     const unsigned long long m = __builtin_amdgcn_ballot_w64(desc);
     if (m == 0ull) break;
     if (kFrac && (unsigned)__popcll(m) * kFrac < started) break;
+    if (++trips > kDescTrips) break;
     if (!desc) continue;
     uint32_t nxt = desc_decide(st, stk, nd, node, ax);
     // the near child's word is in the packet: decide there too (unless it is
@@ -559,6 +602,10 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
     desc = ax != 3u;
   }
   if (desc) {  // paused: resumes at this node in the next iteration
+    if ((unsigned)st.sp > S.depth_cap) {  // watchdog: a stack no valid traversal reaches
+      st.sp = kSpError;
+      return false;
+    }
     paused = true;
     st.node = (int)node;
     nnodes--;  // counted again when the next descent reloads it
@@ -573,13 +620,18 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
 // True when the ray is finished.
 template <bool CLOSEST>
 __device__ __forceinline__ bool trav_next(const DScene& S, Trav& st, const LaneStack& stk) {
-  if (CLOSEST && st.prim >= 0 && st.Z <= st.ex_t) return true;
+  if (CLOSEST && st.Z < st.dist && st.Z <= st.ex_t) return true;
   st.en_t = st.ex_t;
-  st.en_pb = st.ex_pb;
+  st.en_split = st.ex_split;
+  st.en_code = st.ex_w >> 30;
   st.node = (int)(st.ex_w & 0x3FFFFFFFu) - 1;
   if (st.node < 0) return true;
-  if ((unsigned)st.node >= S.nnodes || st.sp <= 0) {  // corrupt state: never index out of the tree
-    st.prim = -2;
+  // corrupt state (never index out of the tree or the stack area): a node
+  // outside the tree, or a stack outside [1, depth_cap] -- a valid traversal
+  // holds at most depth_cap entries, and the overflow area has room for one
+  // more descent's pushes than that
+  if ((unsigned)st.node >= S.nnodes || (unsigned)(st.sp - 1) >= S.depth_cap) {
+    st.sp = kSpError;
     return true;
   }
   st.sp--;
@@ -588,7 +640,6 @@ __device__ __forceinline__ bool trav_next(const DScene& S, Trav& st, const LaneS
   st.ex_w = e.y;
   const uint32_t code = e.y >> 30;
   st.ex_t = (code == 3u) ? st.ex_split : (st.ex_split - sel3(st.o, code)) * sel3(st.inv, code);
-  exit_pb(st);
   return false;
 }
 
@@ -704,13 +755,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
     const unsigned long long kk = keys[lane];
     if (CLOSEST) {
       ntris += nref;
-      if (kk != ~0ull) {
-        const float4 c = cand[lane];
-        st.Z = c.x;
-        st.b1 = c.y;
-        st.b2 = c.z;
-        st.prim = (int)__float_as_uint(c.w);
-      }
+      if (kk != ~0ull) st.Z = cand[lane].x;  // (t, b1, b2, prim) stay in cand[lane]
     } else if (kk != ~0ull) {
       occluded = true;
       ntris += (unsigned)kk + 1u;
@@ -753,7 +798,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   const int lane = threadIdx.x;
   const long long n = __builtin_amdgcn_readfirstlane((int)rc.get());
   if (blockIdx.x == 0 && lane == 0 && n > 0) atomicAdd(&ctr[3], (unsigned long long)n);  // rays traced
-  const LaneStack stk{lds, ovf + (size_t)(blockIdx.x * 64u + (unsigned)lane) * (unsigned)ovf_depth, lane};
+  const LaneStack stk{lds, ovf, (unsigned)ovf_depth, lane};
   int rid = -1;  // ray of this lane (host guarantees n < 2^31)
   bool exhausted = false;
   Trav st;
@@ -786,7 +831,12 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   const unsigned seg_len = (unsigned)((n + NSEG - 1) / NSEG);
   unsigned pool_next = 0, pool_end = 0;
   unsigned seg_done = 0;  // bit s: segment s has no chunks left
-  unsigned iters = 0;     // wave watchdog: a valid tree never gets near the cap
+  // per-ray watchdog: a valid traversal visits every node at most once, so a
+  // ray whose node visits exceed the tree's node count is looping through a
+  // corrupt tree; checked every 32nd wave iteration against the lane's node
+  // count at the ray's start (kept in LDS, off the register budget)
+  __shared__ unsigned ray_n0[64];
+  unsigned iters = 0;
 #ifdef YK_TRAV_STATS
   // diagnostic build (tools/trav_bench.py only: in the render pipeline ctr[4..]
   // are the other kernel kind's accumulators): wave iterations, active lanes per iteration, wave-level
@@ -835,6 +885,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
           if (TS) st.ts_max = ts_depth;
           if (trav_begin<CLOSEST, TS, UNI>(S, st, ray)) {
             rid = r;
+            ray_n0[lane] = nnodes;
           } else if (CLOSEST) {
             hits[r] = yk_hit{-1, 0.f, 0.f, 0.f};
           } else {
@@ -868,7 +919,8 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       if (__ballot(!exhausted) == 0ull) break;
       continue;
     }
-    const bool runaway = ++iters > (1u << 30);
+    bool runaway = false;
+    if ((++iters & 31u) == 0u) runaway = rid >= 0 && nnodes - ray_n0[lane] > S.nnodes + 2u;
 #ifdef YK_TRAV_STATS
     const unsigned n_before = nnodes, t_before = ntris;
     s_it++;
@@ -904,16 +956,19 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       if (act) {
         bool done = !live || occ || (!paused && trav_next<CLOSEST>(S, st, stk));
         if (runaway) {
-          st.prim = -2;
+          st.sp = kSpError;
           done = true;
         }
-        if (st.prim == -2) {
-          nerr++;
-          st.prim = -1;
-        }
+        const bool err = st.sp == kSpError;
+        if (err) nerr++;
         if (done) {
           if (CLOSEST) {
-            hits[rid] = (st.prim >= 0) ? yk_hit{st.prim, st.Z, st.b1, st.b2} : yk_hit{-1, 0.f, 0.f, 0.f};
+            yk_hit h{-1, 0.f, 0.f, 0.f};
+            if (st.Z < st.dist && !err) {
+              const float4 c = cand[lane];
+              h = yk_hit{(int)__float_as_uint(c.w), c.x, c.y, c.z};
+            }
+            hits[rid] = h;
           } else {
             occl[rid] = occ ? 1 : 0;
           }
@@ -965,7 +1020,6 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       s_lmax += lm;
     }
 #endif
-    if (runaway) exhausted = true;
   }
 #ifdef YK_TRAV_STATS
   if (lane == 0) {
@@ -2514,10 +2568,32 @@ __global__ void __launch_bounds__(256) k_film_gather(FilmConst F, const float4* 
   px[4] = aW;
 }
 
-// acc += src, film sums of another shard (yk_render_multi's reduce)
-__global__ void k_film_add(float* __restrict__ acc, const float* __restrict__ src, long long n) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) acc[i] = acc[i] + src[i];
+// yk_render_multi's reduce: acc = ((f[0] + f[1]) + f[2]) + ... in shard
+// order, one pass over all shard films (each element summed in the order the
+// sequential reduce added them, so the result does not depend on how the
+// copies were scheduled). Four floats per thread where the range allows.
+constexpr int kMaxMultiDev = 16;
+struct FilmShards {
+  const float* f[kMaxMultiDev];
+  int n;
+};
+__global__ void __launch_bounds__(256) k_film_sum(float* __restrict__ acc, FilmShards S, long long n) {
+  const long long i4 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i4 >= n) return;
+  if (i4 + 4 <= n) {
+    float4 a = *reinterpret_cast<const float4*>(S.f[0] + i4);
+    for (int k = 1; k < S.n; ++k) {
+      const float4 b = *reinterpret_cast<const float4*>(S.f[k] + i4);
+      a = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    }
+    *reinterpret_cast<float4*>(acc + i4) = a;
+    return;
+  }
+  for (long long i = i4; i < n; ++i) {
+    float a = S.f[0][i];
+    for (int k = 1; k < S.n; ++k) a = a + S.f[k][i];
+    acc[i] = a;
+  }
 }
 
 // imageFilm_t::nextPass (imagefilm.cc:213-271): flag the pixels whose
@@ -2799,17 +2875,63 @@ struct yk_device {
   std::vector<unsigned> mat_flags;  // bsdfFlags per material
   Pipe pipe[kPipes];
   hipEvent_t gather_ev[kPipes] = {};
+  // device records of the uploaded scene, kept to re-bind the GPU's constant
+  // memory when another handle on the same GPU uploaded a different scene
+  std::vector<DMat> mats_host;
+  DCam cam_host{};
+  // yk_render_multi state, kept across calls (no allocation once sized): this
+  // device's shard film; as the reducing device, the sum, one staging film per
+  // peer GPU and one copy stream + event per peer (each peer's copy drives its
+  // own xGMI link)
+  DBuf<float> mfilm, macc;
+  DBuf<float> mstage[kMaxMultiDev];
+  // render_pass's tile lists (grow-only, so repeated renders allocate nothing)
+  DBuf<int4> tiles_dev;
+  DBuf<int> base_dev, pix_dev, pmap_dev;
+  DBuf<uint8_t> flags_dev;
+  hipStream_t mstream[kMaxMultiDev] = {};
+  hipEvent_t mevent[kMaxMultiDev] = {};
   ~yk_device() {
     for (auto& e : gather_ev)
       if (e) (void)hipEventDestroy(e);
+    for (int i = 0; i < kMaxMultiDev; ++i) {
+      if (mevent[i]) (void)hipEventDestroy(mevent[i]);
+      if (mstream[i]) (void)hipStreamDestroy(mstream[i]);
+    }
   }
 };
 
 namespace {
+// Constant memory (c_mats, c_lights, c_cam) is per GPU, not per handle: the
+// scene generation whose records a GPU's constants hold. A handle whose scene
+// differs re-binds them before it launches (bind_constants).
+std::mutex g_const_mu;
+uint64_t g_const_gen[64] = {};
+
+void bind_constants(yk_device* d) {
+  std::lock_guard<std::mutex> lk(g_const_mu);
+  const int o = d->ordinal & 63;
+  if (g_const_gen[o] == d->uploaded_gen) return;
+  if (!d->mats_host.empty())
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_mats), d->mats_host.data(), d->mats_host.size() * sizeof(DMat)));
+  if (!d->lights_host.empty())
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_lights), d->lights_host.data(), d->lights_host.size() * sizeof(DLight)));
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_cam), &d->cam_host, sizeof(DCam)));
+  g_const_gen[o] = d->uploaded_gen;
+}
+}  // namespace
+
+namespace {
+
+// the traversal watchdog fired (corrupt tree or stack): YK_ERR_INTERNAL
+struct watchdog_error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
 
 #define YK_GUARD_BEGIN try {
 #define YK_GUARD_END                                                                              \
   }                                                                                               \
+  catch (const watchdog_error& e) { return set_error(YK_ERR_INTERNAL, e.what()); }               \
   catch (const std::bad_alloc&) { return set_error(YK_ERR_ALLOC, "out of host memory"); }        \
   catch (const std::invalid_argument& e) { return set_error(YK_ERR_ARG, e.what()); }             \
   catch (const std::runtime_error& e) { return set_error(YK_ERR_HIP, e.what()); }                \
@@ -3010,7 +3132,69 @@ void upload_qmc() {
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_faure), fa.data(), fa.size() * sizeof(int)));
 }
 
-int stack_depth(const yk_device* d) { return d->max_depth + 2; }
+// Structural check of a kd-tree in the export encoding (2 words per node:
+// split bits / single prim / leaf-list offset; axis | right child or count
+// << 2), before it becomes resident: every interior node i has its left child
+// at i + 1 and its right child r with i + 1 < r < nn, every node but the root
+// has exactly one parent, and every leaf references prims (single) or
+// leaf-list entries within range. Such a structure is a tree, so a traversal
+// visits each node at most once and its stack never holds more than the
+// depth. Returns the depth (root = 0), or -1 with *err set.
+int tree_depth(const uint32_t* w, size_t nn, size_t nleaf, size_t nprims, std::string* err) {
+  if (nn == 0) {
+    *err = "empty kd-tree";
+    return -1;
+  }
+  std::vector<uint8_t> parents(nn, 0), depth(nn, 0);
+  int maxd = 0;
+  for (size_t i = 0; i < nn; ++i) {
+    const uint32_t w0 = w[2 * i], w1 = w[2 * i + 1];
+    if ((w1 & 3u) == 3u) {  // leaf
+      const uint64_t cnt = w1 >> 2;
+      if ((cnt == 1 && w0 >= nprims) || (cnt > 1 && (uint64_t)w0 + cnt > nleaf)) {
+        *err = "kd-tree leaf " + std::to_string(i) + " references out of range";
+        return -1;
+      }
+      continue;
+    }
+    const uint64_t r = w1 >> 2;
+    if (i + 1 >= nn || r <= i + 1 || r >= nn) {
+      *err = "kd-tree node " + std::to_string(i) + " has a child out of order or range";
+      return -1;
+    }
+    for (const uint64_t c : {(uint64_t)i + 1, r}) {
+      if (++parents[c] > 1) {
+        *err = "kd-tree node " + std::to_string(c) + " has two parents";
+        return -1;
+      }
+      if (depth[i] >= kMaxTreeDepth) {
+        *err = "kd-tree deeper than 64 levels (KD_MAX_STACK)";
+        return -1;
+      }
+      depth[c] = (uint8_t)(depth[i] + 1);  // parents precede children: one forward pass
+      maxd = std::max(maxd, (int)depth[c]);
+    }
+  }
+  for (size_t i = 1; i < nn; ++i)
+    if (parents[i] != 1) {
+      *err = "kd-tree node " + std::to_string(i) + " is unreachable";
+      return -1;
+    }
+  return maxd;
+}
+
+// Traversal bounds of the resident tree (tree_depth): descents and stacks of
+// a valid traversal stay within depth + 2 (depth_cap); the per-lane overflow
+// area holds one descent's pushes beyond that, so a corrupt tree never
+// writes outside it (stack_depth).
+void set_tree_bounds(yk_device* d, int depth) {
+  d->max_depth = depth;
+  d->S.depth_cap = (unsigned)depth + 2u;
+}
+// a lane's stack is checked against depth_cap at every pop and every paused
+// descent, and one descent pushes at most two entries per trip of its
+// kDescTrips trips
+int stack_depth(const yk_device* d) { return (int)d->S.depth_cap + 2 * (int)kDescTrips + 2; }
 
 // YK_REFILL (1-64) overrides the per-scene refill threshold (set_handout);
 // 0 = none
@@ -3069,7 +3253,7 @@ void launch_trace(yk_device* d, Pipe& P, const yk_ray* rays, long long n, yk_hit
   unsigned long long h[13];
   HIPCHK(hipMemcpyAsync(h, acc, sizeof h, hipMemcpyDeviceToHost, P.stream));
   HIPCHK(hipStreamSynchronize(P.stream));
-  if (h[2]) throw std::runtime_error("kd-tree traversal watchdog fired on " + std::to_string(h[2]) + " rays");
+  if (h[2]) throw watchdog_error("kd-tree traversal watchdog fired on " + std::to_string(h[2]) + " rays");
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, P.ev0, P.ev1));
 #ifdef YK_TRAV_STATS
@@ -3246,6 +3430,10 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   }
   YK_GUARD_BEGIN
   HIPCHK(hipSetDevice(d->ordinal));
+  std::string terr;
+  const int tdepth = tree_depth(S.tree.nodes.data(), S.tree.nodes.size() / 2, S.tree.leaf_prims.size(),
+                                S.tri_material.size(), &terr);
+  if (tdepth < 0) return set_error(YK_ERR_ARG, "yk_device_upload: " + terr);
   // the resident arrays are replaced below: until that has succeeded the
   // device holds no usable scene
   d->uploaded = false;
@@ -3295,7 +3483,6 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
     d->mat_flags.push_back(m.bsdf_flags);
     if (m.bsdf_flags & (BSDF_SPECULAR | BSDF_FILTER)) d->spec = true;
   }
-  if (!mats.empty()) HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_mats), mats.data(), mats.size() * sizeof(DMat)));
   std::vector<DLight> lights;
   int sum_slots = 0;
   for (size_t i = 0; i < S.light_states.size(); ++i) {
@@ -3312,10 +3499,8 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   d->pm_ready = false;
   d->has_bg = S.has_background;
   for (int k = 0; k < 3; ++k) d->bg[k] = S.background[k];
-  if (!lights.empty())
-    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_lights), lights.data(), lights.size() * sizeof(DLight)));
-  const DCam cam = make_cam(S.camera_state);
-  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_cam), &cam, sizeof cam));
+  d->mats_host = mats;
+  d->cam_host = make_cam(S.camera_state);
   d->S.tris = d->tris.p;
   d->S.nodes = d->nodes.p;
   d->S.leaf = d->leaf.p;
@@ -3343,11 +3528,12 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   }
   d->nlights = (int)S.light_states.size();
   d->ntris = nt;
-  d->max_depth = S.tree.max_depth;
+  set_tree_bounds(d, tdepth);
   d->nleaf = S.tree.leaf_prims.size();
   d->uploaded = true;
   d->uploaded_scene = s;
   d->uploaded_gen = S.generation;
+  bind_constants(d);  // materials, lights and camera into the GPU's constant memory
   return YK_OK;
   YK_GUARD_END
 }
@@ -3384,6 +3570,7 @@ int yk_trace_shadow_filtered(yk_device* d, const yk_ray* d_rays, int64_t n, uint
   if (n > 0x7FFFFFFFll - (1ll << 24)) return set_error(YK_ERR_ARG, "ray batch too large");
   YK_GUARD_BEGIN
   HIPCHK(hipSetDevice(d->ordinal));
+  bind_constants(d);  // the transparent-shadow leaf body reads the materials
   Pipe& P = d->pipe[0];
   unsigned long long* work = P.counters.p;
   unsigned long long* acc = P.counters.p + 128;
@@ -3539,6 +3726,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     return set_error(YK_ERR_ARG, "filter_width must be 0 or in [0.501, 4]");
   YK_GUARD_BEGIN
   HIPCHK(hipSetDevice(d->ordinal));
+  bind_constants(d);
   auto t0 = std::chrono::steady_clock::now();
   FilmConst F = make_film(p);
   if (F.tile > 4096) return set_error(YK_ERR_UNSUPPORTED, "tile_size > 4096");
@@ -3672,13 +3860,16 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     nc_of[bi] = nc;
     rect_of[bi] = make_int4(rx0, ry0, rx1, ry1);
   }
-  DBuf<int4> tiles_dev;
-  DBuf<int> base_dev;
+  // tile lists, adaptive-pass pixel lists and flags live on the handle
+  // (grow-only): a repeated render allocates nothing
+  DBuf<int4>& tiles_dev = d->tiles_dev;
+  DBuf<int>& base_dev = d->base_dev;
   tiles_dev.ensure(tiles_all.size());
   base_dev.ensure(base_all.size());
   HIPCHK(hipMemcpy(tiles_dev.p, tiles_all.data(), tiles_all.size() * sizeof(int4), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(base_dev.p, base_all.data(), base_all.size() * sizeof(int), hipMemcpyHostToDevice));
-  DBuf<int> pix_dev, pmap_dev;
+  DBuf<int>& pix_dev = d->pix_dev;
+  DBuf<int>& pmap_dev = d->pmap_dev;
   if (ps.flags) {
     pix_dev.ensure(std::max<size_t>(1, pix_all.size()));
     pmap_dev.ensure(pmap.size());
@@ -3934,6 +4125,19 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     HIPCHK(hipMemcpyAsync(acc[pi], P.words.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, P.stream));
     HIPCHK(hipStreamSynchronize(P.stream));
   }
+  if (std::getenv("YK_LAUNCH_LOG") && !d->spec) {
+    // diagnostic: rays of every traversal launch (queue-count words), per batch
+    for (int bi = 0; bi < nbatch; ++bi) {
+      const int pi = bi % npipes;
+      std::vector<unsigned long long> q((size_t)qwords_per_batch);
+      HIPCHK(hipMemcpy(q.data(), d->pipe[pi].words.p + 8 + words_per_batch * (bi / npipes),
+                       q.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      std::fprintf(stderr, "[launch-log] batch %d samples %lld:", bi, nc_of[bi]);
+      for (int w = 0; w < qwords_per_batch; ++w)
+        std::fprintf(stderr, " d%d shadow %llu next %llu;", w, q[w] & 0xFFFFFFFFull, q[w] >> 32);
+      std::fprintf(stderr, "\n");
+    }
+  }
   yk_stats local{};
   yk_stats* S = st ? st : &local;
   for (int pi = 0; pi < npipes; ++pi) {
@@ -3983,7 +4187,7 @@ int yk_render_shard(yk_device* d, const yk_render_params* p, int32_t shard, int3
   YK_GUARD_BEGIN
   const int w = p->width, h = p->height;
   std::vector<uint8_t> flags((size_t)w * h);
-  DBuf<uint8_t> flags_dev;
+  DBuf<uint8_t>& flags_dev = d->flags_dev;
   flags_dev.ensure(flags.size());
   for (int pass = 1; pass < p->aa_passes; ++pass) {
     const uint8_t* fl = nullptr;  // AA_threshold <= 0: doMoreSamples is always true
@@ -4044,22 +4248,35 @@ int yk_render_film(yk_device* d, const yk_render_params* p, int32_t shard, int32
 int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params* p, float* film_host,
                     yk_stats* st) {
   if (!devs || ndev < 1 || !p || !film_host) return set_error(YK_ERR_ARG, "yk_render_multi: bad arguments");
+  if (ndev > kMaxMultiDev) return set_error(YK_ERR_UNSUPPORTED, "yk_render_multi: at most 16 devices");
   for (int i = 0; i < ndev; ++i) {
     if (!devs[i]) return set_error(YK_ERR_ARG, "yk_render_multi: NULL device");
     if (!devs[i]->uploaded) return set_error(YK_ERR_STATE, "yk_render_multi: a device has no scene uploaded");
     for (int j = 0; j < i; ++j)
       if (devs[j] == devs[i]) return set_error(YK_ERR_ARG, "yk_render_multi: a device handle is listed twice");
+    // one frame = one scene: the same uploaded scene generation everywhere
+    // (handles on one GPU share its constant memory, and shards of different
+    // scenes would be summed into one film)
+    if (devs[i]->uploaded_gen != devs[0]->uploaded_gen)
+      return set_error(YK_ERR_STATE, "yk_render_multi: the devices hold different scenes (upload the same scene to all)");
+    const bool maps = p->integrator == YK_INTEGRATOR_PHOTON ||
+                      (p->integrator == YK_INTEGRATOR_PATH &&
+                       (p->caustic_type == YK_CAUSTIC_PHOTON || p->caustic_type == YK_CAUSTIC_BOTH));
+    if (maps && (!devs[i]->pm_ready || devs[i]->pm_integrator != p->integrator ||
+                 std::memcmp(&devs[i]->pm_params, &p->photon, sizeof(yk_photon_params)) != 0))
+      return set_error(YK_ERR_STATE, "yk_render_multi: device " + std::to_string(i) +
+                                         " has no photon maps built with these parameters (yk_photon_build)");
   }
   if (p->aa_passes < 1) return set_error(YK_ERR_ARG, "AA_passes must be >= 1");
   if (p->width <= 0 || p->height <= 0) return set_error(YK_ERR_ARG, "empty render area");
   YK_GUARD_BEGIN
   const size_t npx = (size_t)p->width * p->height, nfl = npx * 5;
   yk_device* d0 = devs[0];
-  std::vector<DBuf<float>> film(ndev);
+  // shard films and reduce buffers live on the handles: sized once, reused
   for (int i = 0; i < ndev; ++i) {
     HIPCHK(hipSetDevice(devs[i]->ordinal));
-    film[i].ensure(nfl);
-    HIPCHK(hipMemsetAsync(film[i].p, 0, nfl * sizeof(float), devs[i]->stream));
+    devs[i]->mfilm.ensure(nfl);
+    HIPCHK(hipMemsetAsync(devs[i]->mfilm.p, 0, nfl * sizeof(float), devs[i]->stream));
     HIPCHK(hipStreamSynchronize(devs[i]->stream));
     if (devs[i]->ordinal != d0->ordinal) {  // direct xGMI access where the pair allows it
       int can = 0;
@@ -4073,10 +4290,23 @@ int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params
     }
   }
   HIPCHK(hipSetDevice(d0->ordinal));
-  DBuf<float> acc, stage;
-  acc.ensure(nfl);
-  if (ndev > 1) stage.ensure(nfl);
+  d0->macc.ensure(nfl);
+  FilmShards FS{};
+  FS.n = ndev;
+  for (int i = 0; i < ndev; ++i) {
+    // a shard on d0's own GPU is read in place; a peer GPU's film is copied
+    // into a staging film first, on a copy stream of its own
+    if (devs[i]->ordinal == d0->ordinal) {
+      FS.f[i] = devs[i]->mfilm.p;
+      continue;
+    }
+    d0->mstage[i].ensure(nfl);
+    if (!d0->mstream[i]) HIPCHK(hipStreamCreateWithFlags(&d0->mstream[i], hipStreamNonBlocking));
+    if (!d0->mevent[i]) HIPCHK(hipEventCreateWithFlags(&d0->mevent[i], hipEventDisableTiming));
+    FS.f[i] = d0->mstage[i].p;
+  }
   std::vector<yk_stats> sts(ndev);
+  double ms_reduce = 0.0;
   // one pass on every device, each in its own host thread
   auto run = [&](const PassSpec& ps) -> int {
     std::vector<int> rc(ndev, YK_OK);
@@ -4084,7 +4314,7 @@ int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params
     std::vector<std::thread> th;
     for (int i = 0; i < ndev; ++i)
       th.emplace_back([&, i] {
-        rc[i] = render_pass(devs[i], p, i, ndev, film[i].p, &sts[i], ps);
+        rc[i] = render_pass(devs[i], p, i, ndev, devs[i]->mfilm.p, &sts[i], ps);
         if (rc[i] != YK_OK) msg[i] = yk_last_error();
       });
     for (auto& t : th) t.join();
@@ -4096,21 +4326,24 @@ int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params
     }
     return out;
   };
-  // acc = film[0] + film[1] + ... (shard order) on device 0
+  // acc = film[0] + film[1] + ... (shard order) on device 0: every peer copy
+  // is in flight at once (one stream each), then one summing pass
   auto reduce = [&]() {
+    const auto t0 = std::chrono::steady_clock::now();
     HIPCHK(hipSetDevice(d0->ordinal));
     hipStream_t s0 = d0->stream;
-    HIPCHK(hipMemcpyAsync(acc.p, film[0].p, nfl * sizeof(float), hipMemcpyDeviceToDevice, s0));
     for (int i = 1; i < ndev; ++i) {
-      if (devs[i]->ordinal == d0->ordinal)
-        HIPCHK(hipMemcpyAsync(stage.p, film[i].p, nfl * sizeof(float), hipMemcpyDeviceToDevice, s0));
-      else
-        HIPCHK(hipMemcpyPeerAsync(stage.p, d0->ordinal, film[i].p, devs[i]->ordinal, nfl * sizeof(float), s0));
-      hipLaunchKernelGGL(k_film_add, dim3(grid_for((long long)nfl)), dim3(256), 0, s0, acc.p, stage.p,
-                         (long long)nfl);
-      HIPCHK(hipGetLastError());
+      if (devs[i]->ordinal == d0->ordinal) continue;
+      HIPCHK(hipMemcpyPeerAsync(d0->mstage[i].p, d0->ordinal, devs[i]->mfilm.p, devs[i]->ordinal, nfl * sizeof(float),
+                                d0->mstream[i]));
+      HIPCHK(hipEventRecord(d0->mevent[i], d0->mstream[i]));
+      HIPCHK(hipStreamWaitEvent(s0, d0->mevent[i], 0));
     }
+    hipLaunchKernelGGL(k_film_sum, dim3(grid_for(((long long)nfl + 3) / 4)), dim3(256), 0, s0, d0->macc.p, FS,
+                       (long long)nfl);
+    HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s0));
+    ms_reduce += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   };
   const int n0 = std::max(1, p->aa_samples);  // scene_t::setAntialiasing, scene.cc:736-742
   const bool multipass = p->aa_passes > 1;
@@ -4121,7 +4354,7 @@ int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params
     const int inc = p->aa_inc_samples > 0 ? p->aa_inc_samples : n0;
     const int w = p->width, h = p->height;
     std::vector<uint8_t> flags(npx);
-    DBuf<uint8_t> flags_dev;
+    DBuf<uint8_t>& flags_dev = d0->flags_dev;
     flags_dev.ensure(npx);
     for (int pass = 1; pass < p->aa_passes; ++pass) {
       const uint8_t* fl = nullptr;  // AA_threshold <= 0: doMoreSamples is always true
@@ -4130,7 +4363,7 @@ int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params
         HIPCHK(hipMemsetAsync(flags_dev.p, 0, npx, d0->stream));
         if (w > 1 && h > 1) {
           hipLaunchKernelGGL(k_aa_flags, dim3(grid_for((long long)(w - 1) * (h - 1))), dim3(256), 0, d0->stream,
-                             acc.p, w, h, p->aa_threshold, flags_dev.p);
+                             d0->macc.p, w, h, p->aa_threshold, flags_dev.p);
           HIPCHK(hipGetLastError());
         }
         HIPCHK(hipMemcpyAsync(flags.data(), flags_dev.p, npx, hipMemcpyDeviceToHost, d0->stream));
@@ -4144,7 +4377,7 @@ int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params
     }
   }
   HIPCHK(hipSetDevice(d0->ordinal));
-  HIPCHK(hipMemcpy(film_host, acc.p, nfl * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(film_host, d0->macc.p, nfl * sizeof(float), hipMemcpyDeviceToHost));
   if (st) {
     for (const yk_stats& x : sts) {
       st->closest_rays += x.closest_rays;
@@ -4160,6 +4393,7 @@ int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params
       st->closest_launches += x.closest_launches;
       st->shadow_launches += x.shadow_launches;
     }
+    st->ms_reduce += ms_reduce;
   }
   if (rc == YK_ERR_ABORTED) return set_error(rc, "render aborted by the abort callback (film holds the finished batches)");
   return YK_OK;

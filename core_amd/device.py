@@ -102,13 +102,19 @@ class Device:
     @staticmethod
     def render_multi(devices, params, stats=None):
         """Whole frame on several devices (yk_render_multi: tiles t % n on
-        devices[i], film reduced on devices[0]) -> (h, w, 5) float32 film sums."""
+        devices[i], film reduced on devices[0]) -> ((h, w, 5) float32 film
+        sums, yk_stats). An abort (YK_ERR_ABORTED) is not an error here, as
+        in the C API: the film holds the finished batches and st.aborted is
+        True."""
         for d in devices:
             torch.cuda.synchronize(d.torch_device)
         arr = (C.c_void_p * len(devices))(*[d._p.value for d in devices])
         out = np.zeros((params.height, params.width, 5), np.float32)
         st = stats if stats is not None else A.yk_stats()
-        A.check(A.lib().yk_render_multi(arr, len(devices), C.byref(params), out.ctypes.data_as(A.fp), C.byref(st)))
+        rc = A.lib().yk_render_multi(arr, len(devices), C.byref(params), out.ctypes.data_as(A.fp), C.byref(st))
+        st.aborted = rc == A.YK_ERR_ABORTED
+        if not st.aborted:
+            A.check(rc)
         return out, st
 
     def film_resolve(self, params, film):

@@ -185,6 +185,8 @@ typedef struct yk_stats {
   double ms_closest;       /* summed kernel time of the closest-hit kernels        */
   double ms_shadow;        /* summed kernel time of the any-hit kernels            */
   uint64_t closest_launches, shadow_launches;
+  double ms_reduce;        /* yk_render_multi: wall time of the film reduces (peer
+                              copies + sum), included in the call's time          */
 } yk_stats;
 
 typedef struct yk_scene yk_scene;   /* host scene + kd-tree (no GPU needed) */
@@ -380,8 +382,16 @@ int yk_render_film(yk_device* d, const yk_render_params* p, int32_t shard, int32
  * With AA_passes > 1 the reduced film gives every pass's imageFilm_t::nextPass
  * flags (imagefilm.cc:213-289), so adaptive passes work across devices (per
  * pixel the result equals the 1-device film up to float summation order).
- * Every device must hold the same uploaded scene; a device handle may appear
- * only once, but two handles may be opened on one GPU. */
+ * Every device must hold the same uploaded scene (YK_ERR_STATE otherwise) and,
+ * for photon mapping / photon caustics, maps built with p->photon; a device
+ * handle may appear only once, but two handles may be opened on one GPU.
+ * The peer copies run concurrently (one stream per source GPU) and one pass
+ * sums the films in shard order; the films and staging buffers stay on the
+ * handles, so repeated calls allocate nothing. st->ms_reduce gets the reduce
+ * time. Handles opened on one GPU share its constant memory (materials,
+ * lights, camera): a handle re-binds it from its own upload before it
+ * renders, so handles on one GPU that hold different scenes must not render
+ * at the same time. */
 int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params* p, float* film_host,
                     yk_stats* st);
 /* convenience: whole frame on one device, RGBA float image to host memory */
@@ -437,6 +447,15 @@ int yk_device_build_tree(yk_device* d, const yk_scene* s, int32_t flags, yk_tree
  * aim rays at the split planes of the tree actually traversed. */
 int yk_device_export_tree(yk_device* d, uint32_t* nodes, int64_t node_cap, uint32_t* leaf, int64_t leaf_cap,
                           int64_t* nnodes_out, int64_t* nleaf_out);
+/* Test hook for the traversal watchdog: overwrites node `index` of the
+ * device's resident kd-tree with the export-encoding words (w0, w1), as a
+ * memory fault would, past the structural check yk_device_upload applies.
+ * Child and leaf ranges must still lie inside the tree (YK_ERR_ARG
+ * otherwise), so the damage is structural (a cycle, a shared subtree, a
+ * deeper descent); ray queries and renders on the damaged tree must then
+ * return YK_ERR_INTERNAL within seconds, never hang or fault. A fresh
+ * yk_device_upload restores the device. */
+int yk_device_debug_set_node(yk_device* d, int64_t index, uint32_t w0, uint32_t w1);
 
 #ifdef __cplusplus
 }

@@ -52,22 +52,73 @@ def _one_device_film(gpu_device, s, p):
     return film.cpu().numpy(), st
 
 
-@pytest.mark.parametrize("ndev", [2, 3])
+def _shard_sum(gpu_device, s, p, ndev):
+    """The sequential reduce: film of shard 0, plus shard 1, plus shard 2 ...
+    (each shard rendered alone with yk_render_shard), in float32."""
+    gpu_device.upload(s)
+    acc = None
+    for i in range(ndev):
+        film = gpu_device.new_film(p)
+        gpu_device.render_shard(p, film, i, ndev)
+        f = film.cpu().numpy()
+        acc = f.copy() if acc is None else acc + f
+    return acc
+
+
+@pytest.mark.parametrize("ndev", [2, 3, 8])
 def test_render_multi_equals_one_device(gpu_device, ndev):
+    """yk_render_multi with n handles: bit-identical to the shard films summed
+    in shard order (the concurrent copies + one summing pass change nothing),
+    equal to the one-device film up to summation order, counters exact; a
+    repeated call gives the same bits and allocates no device memory."""
+    import torch
     s, p = _bumpy(480, 270, 8)
     f1, st1 = _one_device_film(gpu_device, s, p)
+    ref = _shard_sum(gpu_device, s, p, ndev)
     devs = [gpu_device] + [Device(0) for _ in range(ndev - 1)]
     try:
         for d in devs:
             d.upload(s)
         fn, stn = Device.render_multi(devs, p)
+        free0 = torch.cuda.mem_get_info(0)[0]
+        fn2, _ = Device.render_multi(devs, p)
+        free1 = torch.cuda.mem_get_info(0)[0]
     finally:
         for d in devs[1:]:
             d.close()
     for f in ("closest_rays", "shadow_rays", "closest_nodes", "closest_tris", "shadow_nodes", "shadow_tris",
               "camera_samples"):
         assert getattr(stn, f) == getattr(st1, f), f
+    assert stn.ms_reduce > 0.0
+    assert (fn.view(np.uint32) == ref.view(np.uint32)).all()
+    assert (fn2.view(np.uint32) == fn.view(np.uint32)).all()
+    assert free1 == free0, (free0, free1)  # the second call allocated nothing
     _compare_films(f1, fn, p.tile_size or 32)
+
+
+def test_render_multi_refuses_mixed_scenes(gpu_device):
+    """handles holding different scenes are refused (their shards
+    would be summed into one film), and a handle re-binds the GPU's constant
+    memory from its own upload, so an interleaved upload elsewhere on the GPU
+    does not leak into its renders."""
+    s1, p = probe_scene("cornell_pt", 16, 16)
+    s2, _ = probe_scene("bumpy", 16, 16, 40, 21)
+    d2 = Device(0)
+    try:
+        gpu_device.upload(s1)
+        d2.upload(s2)
+        with pytest.raises(A.YkError) as e:
+            Device.render_multi([gpu_device, d2], p)
+        assert e.value.code == A.YK_ERR_STATE
+        # gpu_device renders s1 although d2 uploaded s2 (new constants) last
+        film = gpu_device.new_film(p)
+        gpu_device.render_shard(p, film)
+        d2.upload(s1)
+        ref = gpu_device.new_film(p)
+        d2.render_shard(p, ref)
+        assert (film.cpu().numpy().view(np.uint32) == ref.cpu().numpy().view(np.uint32)).all()
+    finally:
+        d2.close()
 
 
 def test_render_multi_adaptive_passes(gpu_device):

@@ -1,0 +1,105 @@
+#!/bin/bash
+# One parametrised GPU measurement script (run under gpurun):
+#   tools/gpu.sh OUTDIR STEP [STEP ...]
+# Every step runs under its own time limit; set -e stops at the first failure,
+# so nothing else touches the GPU after a fault, abort or timeout.
+# Steps (VARIANT = base for core_amd/libyk.so, else tune/libyk_VARIANT.so):
+#   test                 pytest -m gpu (one process, per-test timeout)
+#   smoke                __graft_entry__.smoke()
+#   bench                headline bench.py (1M tris, 1080p, 256 spp)
+#   c2 | pm | hair       BASELINE configs[1] Cornell / photon mapping / C5 hair benches
+#   prof                 rocprofv3 --kernel-trace --stats of the one-pipe headline frame
+#   prof_c2 | prof_hair  the same for the Cornell / hair frames
+#   pmc                  FETCH_SIZE and WRITE_SIZE passes of the one-pipe headline frame
+#   pmc_c2 | pmc_hair    the same for Cornell / hair
+#   tb:VARIANT           traversal microbenchmark (tools/trav_bench.py)
+#   ab:V1,V2,...         A/B: trav bench + headline bench per variant, two interleaved reps
+#   abc2:V1,V2,...       A/B on the Cornell (C2) bench
+#   tbab:V1,V2,...       A/B of the traversal microbenchmark only, three interleaved reps
+#   coh:VARIANT          primary-shadow ray-order experiment (tools/coherence_bench.py)
+#   multi                tests/test_multi_device.py + tests/test_0_multi_process.py
+set -e
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/$1
+shift
+mkdir -p $O
+lib() { if [ "$1" = base ]; then echo $PWD/core_amd/libyk.so; else echo $PWD/tune/libyk_$1.so; fi; }
+C2="--scene cornell --width 1024 --height 1024 --spp 64"
+HAIR="--scene hair --spp 16"
+P1="--pipes 1 --steps 1 --warmup 0 --no-cpu --no-roofline-frame"
+for s in "$@"; do
+  case $s in
+  test)
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gputest.txt 2>&1
+    tail -3 $O/gputest.txt ;;
+  smoke)
+    timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1
+    tail -1 $O/smoke.txt ;;
+  bench)
+    timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err
+    head -c 400 $O/bench.json; echo ;;
+  c2)
+    timeout -k 10 300 python -u bench.py $C2 > $O/bench_c2.json 2> $O/bench_c2.err
+    head -c 300 $O/bench_c2.json; echo ;;
+  pm)
+    timeout -k 10 400 python -u bench.py --integrator photon --spp 16 > $O/bench_pm.json 2> $O/bench_pm.err
+    head -c 300 $O/bench_pm.json; echo ;;
+  hair)
+    timeout -k 10 500 python -u bench.py $HAIR --no-cpu > $O/bench_hair.json 2> $O/bench_hair.err
+    head -c 300 $O/bench_hair.json; echo ;;
+  prof|prof_c2|prof_hair)
+    A=""; [ $s = prof_c2 ] && A="$C2"; [ $s = prof_hair ] && A="$HAIR"
+    timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$s -o p1 -- python3 bench.py $A $P1 > $O/$s.log 2>&1
+    echo "$s done" ;;
+  pmc|pmc_c2|pmc_hair)
+    A=""; [ $s = pmc_c2 ] && A="$C2"; [ $s = pmc_hair ] && A="$HAIR"
+    timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/${s}_fetch -o f -- python3 bench.py $A $P1 > $O/${s}_fetch.log 2>&1
+    timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/${s}_write -o w -- python3 bench.py $A $P1 > $O/${s}_write.log 2>&1
+    echo "$s done" ;;
+  tb:*)
+    v=${s#tb:}
+    YK_LIB=$(lib $v) timeout -k 10 200 python -u tools/trav_bench.py --spp 4 > $O/tb_$v.json 2> $O/tb_$v.err
+    cat $O/tb_$v.json ;;
+  ab:*|abc2:*)
+    VS=$(echo ${s#*:} | tr , ' ')
+    BA="--no-cpu --steps 2 --warmup 1 --no-roofline-frame"; [ ${s%%:*} = abc2 ] && BA="$BA $C2"
+    for rep in 1 2; do
+      for v in $VS; do
+        L=$(lib $v)
+        if [ ${s%%:*} = ab ]; then
+          YK_LIB=$L timeout -k 10 200 python -u tools/trav_bench.py --spp 4 > $O/ab_tb_${v}_$rep.json 2> $O/ab_tb_${v}_$rep.err
+        fi
+        YK_LIB=$L timeout -k 10 300 python -u bench.py $BA > $O/${s%%:*}_b_${v}_$rep.json 2> $O/${s%%:*}_b_${v}_$rep.err
+        python3 - $O ${s%%:*} $v $rep <<'EOF'
+import json, os, sys
+o, kind, v, rep = sys.argv[1:]
+b = json.load(open(f"{o}/{kind}_b_{v}_{rep}.json"))
+line = f"{v} rep{rep} bench {b['value']}"
+tb = f"{o}/ab_tb_{v}_{rep}.json"
+if kind == "ab" and os.path.exists(tb):
+    d = json.load(open(tb))
+    line += f" tb {d['total_Mrays_s']} " + str([d[k]['Mrays_s'] for k in ('camera', 'bounce', 'shadow1', 'shadow2')])
+print(line)
+EOF
+      done
+    done ;;
+  tbab:*)
+    VS=$(echo ${s#*:} | tr , ' ')
+    for rep in 1 2 3; do
+      for v in $VS; do
+        YK_LIB=$(lib $v) timeout -k 10 200 python -u tools/trav_bench.py --spp 4 > $O/tbab_${v}_$rep.json 2> $O/tbab_${v}_$rep.err
+        python3 -c "import json;d=json.load(open('$O/tbab_${v}_$rep.json'));print('$v rep$rep', d['total_Mrays_s'], [d[k]['Mrays_s'] for k in ('camera','bounce','shadow1','shadow2')])"
+      done
+    done ;;
+  coh:*)
+    v=${s#coh:}
+    YK_LIB=$(lib $v) timeout -k 10 300 python -u tools/coherence_bench.py > $O/coh_$v.json 2> $O/coh_$v.err
+    cat $O/coh_$v.json ;;
+  multi)
+    timeout -k 10 600 python -u -m pytest tests/test_multi_device.py tests/test_0_multi_process.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/multi.txt 2>&1
+    tail -3 $O/multi.txt ;;
+  *)
+    echo "unknown step $s"; exit 2 ;;
+  esac
+done
