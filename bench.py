@@ -63,8 +63,9 @@ def main():
                     help="replace the reference kd-tree by the device-built binned-SAH tree (yk_device_build_tree, "
                          "documented tie-break; not the parity default)")
     ap.add_argument("--traffic", default=None,
-                    help="PMC HBM-traffic summary (tools/pmc_traffic.py output) to attach; default "
-                         "profiles/traffic.json (bumpy) or profiles/traffic_hair.json (hair), path tracing only")
+                    help="PMC HBM-traffic summary (tools/pmc_traffic.py output of the one-pipe frame) to attach; "
+                         "default profiles/traffic.json (bumpy), traffic_hair.json (hair), traffic_c2.json "
+                         "(cornell), path tracing only")
     ap.add_argument("--pipes", type=int, default=0,
                     help="batch pipelines of the timed frames (default: libyk's 4; 1 serialises the kernels)")
     ap.add_argument("--no-roofline-frame", action="store_true",
@@ -254,35 +255,43 @@ def roofline_line(args, w, ms_c, ms_s, rst, elapsed, pt):
         k["gbs"] = k["bytes"] / (k["ms"] * 1e-3) / 1e9 if k["ms"] > 0 else 0.0
         k["avg_ms"] = k["ms"] / max(k["launches"], 1)
     dom, other = (kc, ks) if kc["ms"] >= ks["ms"] else (ks, kc)
-    traffic = traffic_note = None
-    tfile = args.traffic or (os.path.join(ROOT, "profiles", {"bumpy": "traffic.json", "hair": "traffic_hair.json"}
-                                          .get(args.scene, "")) if pt else "")
-    if tfile and os.path.isfile(tfile):  # PMC summary of this scene's PT frame
+    traffic = traffic_raw = traffic_note = None
+    tfile = args.traffic or (os.path.join(ROOT, "profiles", {"bumpy": "traffic.json", "hair": "traffic_hair.json",
+                                                             "cornell": "traffic_c2.json"}[args.scene]) if pt else "")
+    key = "closest" if dom is kc else "shadow"
+    if tfile and os.path.isfile(tfile):  # PMC summary of this scene's one-pipe PT frame
         with open(tfile) as f:
             tj = json.load(f)
-        key = "closest" if dom is kc else "shadow"
-        if key in tj:
+        # only a pass over the same launch partition as the roofline frame
+        # (one pipe: same batches, same launches) is comparable per launch
+        if key in tj and (rst is None or int(tj[key].get("launches", -1)) == int(dom["launches"])):
             traffic = tj[key].get("hbm_bytes_per_launch")
+            traffic_raw = tj[key].get("hbm_bytes_per_launch_raw")
             traffic_note = tj.get("source")
-    out = {"bound": "hbm", "achieved": round(dom["gbs"], 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
+    # the HBM roofline, unless the algorithmic rate is above the HBM peak: then
+    # the re-reads are served by L2 / the Infinity Cache and L2 bandwidth (34.5
+    # TB/s aggregate, MI355X_MICROARCH.md "L2 (per XCD)") is the bound
+    l2_bound = dom["gbs"] > HBM_PEAK_GBS
+    peak = L2_PEAK_GBS if l2_bound else HBM_PEAK_GBS
+    out = {"bound": "l2" if l2_bound else "hbm", "achieved": round(dom["gbs"], 2), "peak": peak, "unit": "GB/s",
+           "frac": round(dom["gbs"] / peak, 4), "traffic": traffic,
            "kernel": dom["name"], "avg_launch_ms": round(dom["avg_ms"], 4), "launches": int(dom["launches"]),
            "algorithmic_bytes_per_launch": round(dom["bytes"] / max(dom["launches"], 1)), "timing": timing,
            "other_kernel": {"name": other["name"], "achieved": round(other["gbs"], 2),
                             "avg_launch_ms": round(other["avg_ms"], 4),
                             "frac": round(other["gbs"] / HBM_PEAK_GBS, 4)}}
     if traffic:
-        # counter view: measured HBM bytes per launch over the same duration
+        # counter view: measured HBM bytes per launch of the same launch
+        # partition over the same launch duration; (2*FETCH + WRITE) with the
+        # guide's gfx950 FETCH correction, and the raw (FETCH + WRITE) beside
+        # it -- the correction is calibrated on wide streaming reads only
+        out["traffic_raw"] = traffic_raw
         out["traffic_gbs"] = round(traffic / (dom["avg_ms"] * 1e-3) / 1e9, 2)
+        out["traffic_gbs_raw"] = round((traffic_raw or 0) / (dom["avg_ms"] * 1e-3) / 1e9, 2)
         out["frac_traffic"] = round(out["traffic_gbs"] / HBM_PEAK_GBS, 4)
         out["traffic_source"] = traffic_note
-    # L2 view (34.5 TB/s aggregate, MI355X_MICROARCH.md "L2 (per XCD)"): the
-    # node / triangle re-reads are served by L2 and the Infinity Cache, so the
-    # algorithmic rate can pass the HBM peak (the hair scene: frac > 1)
+    out["hbm"] = {"peak": HBM_PEAK_GBS, "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4)}
     out["l2"] = {"peak": L2_PEAK_GBS, "frac": round(dom["gbs"] / L2_PEAK_GBS, 4)}
-    if dom["gbs"] > HBM_PEAK_GBS:
-        out["l2"]["note"] = ("algorithmic bytes above the HBM peak: the re-reads come from L2 / Infinity Cache, "
-                             "so L2 bandwidth is the roofline that bounds this kernel")
     # all traversal bytes of the timed frames over their wall time
     out["traversal_achieved_wall"] = round((algorithmic_bytes(w[0], w[2], w[3], 16) +
                                             algorithmic_bytes(w[1], w[4], w[5], 1)) / elapsed / 1e9, 2)

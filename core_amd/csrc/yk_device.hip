@@ -177,7 +177,14 @@ __device__ __forceinline__ bool bound_cross(const float* bb, v3 from, v3 dir, fl
 // entry stores t itself. The top kStackLds entries of every lane live in an
 // LDS ring; deeper ones spill to a global overflow area (rare: a 1M-tri tree
 // has depth ~40 but a ray rarely holds more than a dozen pending exits).
-constexpr int kStackLds = 8;
+constexpr int kStackLds = 8;  // LDS ring depth per lane (16 measured slower: 1807 vs 2054, round 1)
+// accumulator words per traversal kernel kind ({nodes, triangle tests, errors,
+// rays}; the YK_TRAV_STATS diagnostic build adds its cycle counters, ctr[4..12])
+#ifdef YK_TRAV_STATS
+constexpr int kAccWords = 16;
+#else
+constexpr int kAccWords = 4;
+#endif
 // Tree depth limit: the reference caps maxDepth at KD_MAX_STACK = 64
 // (kdtree.cc:42), and yk_device_upload refuses deeper trees, so a descent of
 // a valid tree never takes more than kDescTrips trips of the descent loop (a
@@ -188,25 +195,50 @@ constexpr unsigned kDescTrips = kMaxTreeDepth + 2;
 // been found iff Z < dist (every accepted hit lowers Z below its start,
 // dist), and its (t, b1, b2, prim) stay in the lane's LDS candidate slot
 // (coop_leaves); a corrupt traversal marks the lane with sp = kSpError.
-constexpr int kSpError = -(1 << 20);  // LDS ring depth per lane (16 measured slower: 1807 vs 2054, round 1)
+constexpr int kSpError = -16;  // an inline constant: no register holds it
 
+// A constant materialised where it is used (the compiler otherwise keeps
+// non-inline constants in VGPRs for the whole traversal loop).
+template <unsigned C>
+__device__ __forceinline__ unsigned vconst() {
+  unsigned v;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "i"(C));
+  return v;
+}
+// x of lane src (ds_bpermute; __shfl adds a lane-dependent term for narrow
+// widths that the compiler keeps live)
+__device__ __forceinline__ float bperm(float x, int src) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(x)));
+}
+__device__ __forceinline__ unsigned bperm(unsigned x, int src) {
+  return (unsigned)__builtin_amdgcn_ds_bpermute(src << 2, (int)x);
+}
+// The lane index, recomputed where it is used (two VALU ops) instead of
+// kept live: the compiler hoists a lane index and every lane address derived
+// from it (LDS slots, a 64-bit overflow pointer) out of the traversal loop,
+// and in the any-hit kernel those invariants held ~8 VGPRs for its whole
+// life -- the difference between 6 and 7 waves per SIMD. The volatile asm
+// keeps the compiler from hoisting it.
+__device__ __forceinline__ int lane_fresh() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
 struct LaneStack {
   uint2* lds;    // [kStackLds][64]
   uint2* ovf;    // overflow area of the launch: each lane's entries contiguous (one cache line holds 8)
   unsigned depth;  // overflow entries per lane
-  int lane;
-  // the lane's overflow entry k, addressed on use (rare) instead of a 64-bit
-  // per-lane pointer kept in registers
+  // the lane's overflow entry k, addressed on use (rare)
   __device__ __forceinline__ uint2* ovf_at(int k) const {
-    return ovf + ((size_t)(blockIdx.x * 64u + (unsigned)lane) * depth + (unsigned)k);
+    return ovf + ((size_t)(blockIdx.x * 64u + (unsigned)lane_fresh()) * depth + (unsigned)k);
   }
   __device__ __forceinline__ void push(int sp, uint2 e) const {
-    uint2* slot = lds + (sp & (kStackLds - 1)) * 64 + lane;
+    uint2* slot = lds + (sp & (kStackLds - 1)) * 64 + lane_fresh();
     if (sp >= kStackLds) *ovf_at(sp - kStackLds) = *slot;
     *slot = e;
   }
   __device__ __forceinline__ uint2 pop(int sp) const {  // sp = index of the entry to pop
-    uint2* slot = lds + (sp & (kStackLds - 1)) * 64 + lane;
+    uint2* slot = lds + (sp & (kStackLds - 1)) * 64 + lane_fresh();
     const uint2 e = *slot;
     if (sp >= kStackLds) *slot = *ovf_at(sp - kStackLds);
     return e;
@@ -265,13 +297,13 @@ __device__ __forceinline__ bool trav_begin(const DScene& S, Trav& st, const yk_r
   if (CLOSEST) {
     st.o = V3(r.from[0], r.from[1], r.from[2]);
     st.tmin = r.tmin;
-    st.dist = (r.tmax < 0.f) ? INFINITY : r.tmax;
+    st.dist = (r.tmax < 0.f) ? __uint_as_float(vconst<0x7f800000u>()) : r.tmax;
   } else {
     st.o = V3(r.from[0] + r.tmin * st.d.x, r.from[1] + r.tmin * st.d.y, r.from[2] + r.tmin * st.d.z);
     // IntersectS accepts t >= 0 (universal: t > tmin); IntersectTS keeps the
     // ray's tmin in both modes (kdtree.cc:1061, ray_kdtree.cc identical)
     st.tmin = TS ? r.tmin : (UNI ? nextafterf(r.tmin, INFINITY) : 0.f);
-    st.dist = (r.tmax < 0.f) ? INFINITY : r.tmax - 2.0f * r.tmin;
+    st.dist = (r.tmax < 0.f) ? __uint_as_float(vconst<0x7f800000u>()) : r.tmax - 2.0f * r.tmin;
   }
   if (TS) {
     st.filt = C3(1.f, 1.f, 1.f);
@@ -676,9 +708,10 @@ __device__ __forceinline__ unsigned dpp_max_scan(unsigned x) {
 // the owner's start is read from its lane (one cross-lane read more per
 // round; measured 0.7 % slower, so only such trees run it).
 template <bool CLOSEST, bool BIG = false, bool UNI = false>
-__device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t nref, uint32_t w0, int lane,
+__device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t nref, uint32_t w0,
                                             unsigned long long* keys, float4* cand, unsigned* otab,
                                             unsigned& ntris, bool& occluded) {
+  const int lane = lane_fresh();
   unsigned x = nref;  // inclusive prefix sum of the lanes' reference counts
   // DPP scan: row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15 / 31
   // carry the row totals (out-of-row sources read 0)
@@ -691,7 +724,10 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
   const unsigned pre = x - nref;
   const unsigned total = (unsigned)__builtin_amdgcn_readlane((int)x, 63);
   if (total == 0u) return;
-  keys[lane] = ~0ull;
+  {
+    const unsigned m1 = vconst<0xFFFFFFFFu>();
+    keys[lane] = ((unsigned long long)m1 << 32) | m1;
+  }
   __syncthreads();  // one wave per block: orders the LDS traffic of the phase
   const float zlim = CLOSEST ? st.Z : st.dist;
   unsigned carry = 0u;  // ((start + 1) << 8 | lane) of the range covering the previous slot
@@ -711,13 +747,13 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
     const unsigned okey = ov ? ov : carry;
     carry = (unsigned)__builtin_amdgcn_readlane((int)okey, 63);
     const int own = (int)(okey & 0xFFu);
-    const unsigned pown = BIG ? (unsigned)__shfl((int)pre, own) : (okey >> 8) - 1u;
+    const unsigned pown = BIG ? bperm(pre, own) : (okey >> 8) - 1u;
     const unsigned k = sc - pown;
-    const uint32_t ow0 = (uint32_t)__shfl((int)w0, own), on = (uint32_t)__shfl((int)nref, own);
-    const v3 ro = V3(__shfl(st.o.x, own), __shfl(st.o.y, own), __shfl(st.o.z, own));
-    const v3 rd = V3(__shfl(st.d.x, own), __shfl(st.d.y, own), __shfl(st.d.z, own));
-    const float rz = __shfl(zlim, own);
-    const float rtmin = (CLOSEST || UNI) ? __shfl(st.tmin, own) : 0.f;
+    const uint32_t ow0 = bperm(w0, own), on = bperm(nref, own);
+    const v3 ro = V3(bperm(st.o.x, own), bperm(st.o.y, own), bperm(st.o.z, own));
+    const v3 rd = V3(bperm(st.d.x, own), bperm(st.d.y, own), bperm(st.d.z, own));
+    const float rz = bperm(zlim, own);
+    const float rtmin = (CLOSEST || UNI) ? bperm(st.tmin, own) : 0.f;
     bool valid = false;
     unsigned long long key = 0;
     float th = 0.f, u = 0.f, v = 0.f;
@@ -798,7 +834,12 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   const int lane = threadIdx.x;
   const long long n = __builtin_amdgcn_readfirstlane((int)rc.get());
   if (blockIdx.x == 0 && lane == 0 && n > 0) atomicAdd(&ctr[3], (unsigned long long)n);  // rays traced
-  const LaneStack stk{lds, ovf, (unsigned)ovf_depth, lane};
+  // Small launches (the later bounces: 0.1-2.5M rays on a grid of ~6k waves)
+  // engage only the waves they can fill with a 64-ray chunk each: the others
+  // leave at once instead of contending on the queue and counter atomics
+  // (each wave's end-of-launch adds; a tail of ~0.3 ms per small launch)
+  if ((long long)blockIdx.x * 64 >= n + 63) return;
+  const LaneStack stk{lds, ovf, (unsigned)ovf_depth};
   int rid = -1;  // ray of this lane (host guarantees n < 2^31)
   bool exhausted = false;
   Trav st;
@@ -838,8 +879,8 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   __shared__ unsigned ray_n0[64];
   unsigned iters = 0;
 #ifdef YK_TRAV_STATS
-  // diagnostic build (tools/trav_bench.py only: in the render pipeline ctr[4..]
-  // are the other kernel kind's accumulators): wave iterations, active lanes per iteration, wave-level
+  // diagnostic build (ctr holds kAccWords = 16 words per kernel kind there):
+  // wave iterations, active lanes per iteration, wave-level
   // descent / leaf-loop trips (max over lanes), refills
   unsigned long long s_it = 0, s_act = 0, s_dmax = 0, s_lmax = 0, s_refill = 0;
   // cycles per phase (clock64 deltas, wave-uniform): refill, descent, leaf test, pop
@@ -873,7 +914,9 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
         }
       }
       if (rid < 0 && !exhausted) {
-        const unsigned rank = (unsigned)__popcll(want & ((1ull << lane) - 1ull));
+        // lanes of `want` below this one (mbcnt: no lane mask kept live)
+        const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(want >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((unsigned)want, 0u));
         long long q = -1;
         if (rank < avail) q = pool_next + rank;
         else if (rank - avail < ce - cb) q = cb + (rank - avail);
@@ -885,7 +928,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
           if (TS) st.ts_max = ts_depth;
           if (trav_begin<CLOSEST, TS, UNI>(S, st, ray)) {
             rid = r;
-            ray_n0[lane] = nnodes;
+            ray_n0[lane_fresh()] = nnodes;
           } else if (CLOSEST) {
             hits[r] = yk_hit{-1, 0.f, 0.f, 0.f};
           } else {
@@ -920,7 +963,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       continue;
     }
     bool runaway = false;
-    if ((++iters & 31u) == 0u) runaway = rid >= 0 && nnodes - ray_n0[lane] > S.nnodes + 2u;
+    if ((++iters & 31u) == 0u) runaway = rid >= 0 && nnodes - ray_n0[lane_fresh()] > S.nnodes + 2u;
 #ifdef YK_TRAV_STATS
     const unsigned n_before = nnodes, t_before = ntris;
     s_it++;
@@ -944,7 +987,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       }
 #endif
       bool occ = false;
-      coop_leaves<CLOSEST, BIG, UNI>(S, st, (live && !paused) ? nref : 0u, w0, lane, keys, cand, otab, ntris, occ);
+      coop_leaves<CLOSEST, BIG, UNI>(S, st, (live && !paused) ? nref : 0u, w0, keys, cand, otab, ntris, occ);
 #ifdef YK_TRAV_STATS
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       {
@@ -965,7 +1008,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
           if (CLOSEST) {
             yk_hit h{-1, 0.f, 0.f, 0.f};
             if (st.Z < st.dist && !err) {
-              const float4 c = cand[lane];
+              const float4 c = cand[lane_fresh()];
               h = yk_hit{(int)__float_as_uint(c.w), c.x, c.y, c.z};
             }
             hits[rid] = h;
@@ -1041,31 +1084,36 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
     a += shfl_u64(a, lane ^ off);
     b += shfl_u64(b, lane ^ off);
   }
-  if (lane == 0) {
+  if (lane == 0 && (a | b)) {  // waves that traced nothing add nothing
     atomicAdd(&ctr[0], a);
     atomicAdd(&ctr[1], b);
   }
   if (nerr) atomicAdd(&ctr[2], (unsigned long long)nerr);
 }
 
-// Occupancy targets (measured on MI355X, 1M-tri scene, cooperative leaves):
-// closest-hit at 5 waves/SIMD (96 VGPRs; 6 / 4 waves measured 2644 / 2593
-// against 2810 Mrays/s) with per-XCD ray segments (+12 % from L2 locality);
-// any-hit at 5 (92 VGPRs, no spill: at 6 it spilled 13-17 VGPRs and moved
-// between 2806 and 2636 with unrelated code changes; round 3: 6 waves with 17
-// spills 2668, 4 waves 2781 against 2835) with one shared segment (per-XCD
-// segments: 2700 against 2719 in round 2, 2806 against 2800 in round 3).
-// Non-temporal ray / result accesses measured 2775 against 2824; resident
-// grids below the occupancy limit (room for the other pipes' shading) lost
-// 2-4 %. PMC (round 3, tools/gpu_pmc_tb.sh): the any-hit kernel's texture
-// data path is busy 85 % of its cycles, 58 % of them stalled on L1 misses
-// (L1 hit 68 %, L2 hit 65 %, 360-cycle L2 latency). Crowded-leaf scenes (hair)
-// run the same kernels with 64-ray hand-out chunks (DScene.chunk_max).
+// Occupancy targets (measured on MI355X, 1M-tri scene, cooperative leaves).
+// Round 4 cut the kernels' registers (implicit entry / exit points: -5; lane
+// index and constants recomputed at use instead of held as loop invariants:
+// -8 any-hit, -6 closest-hit; hit record in LDS: -3 closest-hit), which let
+// the any-hit kernel run at 7 waves per SIMD (72 VGPRs, 2 spilled to scratch
+// on rare paths): same-box A/B, traversal microbenchmark camera-hit shadow
+// rays 2479 (5 waves, round 3) -> 2614 (6 waves) -> 2661 (7 waves) Mrays/s,
+// the centre crop at 64 spp (112 nodes per ray) 2086 -> 2455, headline
+// 2976 -> 3076 (6) -> 3114 (7); 8 waves (18 spills) fell to 1715 on the
+// microbenchmark. Closest-hit stays at 5 waves (88 VGPRs; round 3 measured 6
+// waves with spills at 2657 against 2835) with per-XCD ray segments (+12 %
+// from L2 locality). Earlier: any-hit per-XCD segments 2700 / 2719 (round 2),
+// 2806 / 2800 (round 3); non-temporal ray / result accesses 2775 against
+// 2824; resident grids below the occupancy limit lost 2-4 %. PMC (round 3):
+// the any-hit kernel's texture data path is busy 85 % of its cycles, 58 % of
+// them stalled on L1 misses (L1 hit 68 %, L2 hit 65 %, 360-cycle L2 latency),
+// which more resident waves hide better. Crowded-leaf scenes (hair) run the
+// same kernels with 64-ray hand-out chunks (DScene.chunk_max).
 #ifndef YK_CLOSEST_WAVES
 #define YK_CLOSEST_WAVES 5
 #endif
 #ifndef YK_SHADOW_WAVES
-#define YK_SHADOW_WAVES 5
+#define YK_SHADOW_WAVES 7
 #endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
 k_trace_closest(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
@@ -3878,8 +3926,8 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     HIPCHK(hipMemcpy(pmap_dev.p, pmap.data(), pmap.size() * sizeof(int), hipMemcpyHostToDevice));
   }
 
-  // ---- per-pipe device words: [0,8) accumulators {closest nodes, tris,
-  // errors, rays; any-hit ...}; then per batch: queue-count words
+  // ---- per-pipe device words: [0, 2 kAccWords) accumulators {closest
+  // nodes, tris, errors, rays; any-hit ...}; then per batch: queue-count words
   // (isub, depth) and one 128-word ray-segment block per trace launch.
   // All zeroed once; no launch needs a reset or a host round trip.
   const int qwords_per_batch = nsub * (bounces + 1);
@@ -3889,7 +3937,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   for (int pi = 0; pi < npipes; ++pi) {
     Pipe& P = d->pipe[pi];
     const int nb_here = (nbatch - pi + npipes - 1) / npipes;
-    P.words.ensure((size_t)(8 + (d->spec ? 0 : words_per_batch * nb_here)));
+    P.words.ensure((size_t)(2 * kAccWords + (d->spec ? 0 : words_per_batch * nb_here)));
     HIPCHK(hipMemsetAsync(P.words.p, 0, P.words.n * sizeof(unsigned long long), P.stream));
     Bp[pi] = P.bind(maxc, K, tiles_per_batch, R.ps != 0, p->transp_shadows != 0);
     if (R.pm_fg) {
@@ -3942,7 +3990,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
       }
     }
     const long long nc = nc_of[bi];
-    unsigned long long* bw = d->spec ? d->spec_words.p : P.words.p + 8 + words_per_batch * (bi / npipes);
+    unsigned long long* bw = d->spec ? d->spec_words.p : P.words.p + 2 * kAccWords + words_per_batch * (bi / npipes);
     auto qw = [&](int isub, int depth) { return bw + isub * (bounces + 1) + depth; };
     int launch = 0;
     auto trace = [&](bool closest, const yk_ray* rays, const unsigned* idx, RayCount n, yk_hit* hits,
@@ -3953,8 +4001,8 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
       evn[pi] += 2;
       if (closest) enqueue_trace<true>(d, P, rays, idx, n, hits, occ, work, P.words.p, e0, e1);
       else if (B.ts)  // transparent shadows: IntersectTS, filter colour into the slot
-        enqueue_trace_ts(d, P, rays, idx, n, occ, B.s_filt, p->shadow_depth, work, P.words.p + 4, e0, e1);
-      else enqueue_trace<false>(d, P, rays, idx, n, hits, occ, work, P.words.p + 4, e0, e1);
+        enqueue_trace_ts(d, P, rays, idx, n, occ, B.s_filt, p->shadow_depth, work, P.words.p + kAccWords, e0, e1);
+      else enqueue_trace<false>(d, P, rays, idx, n, hits, occ, work, P.words.p + kAccWords, e0, e1);
     };
     // photonIntegrator_t::integrate after the direct light: show_map /
     // diffuse-map estimate, final gathering, caustics (photonintegr.cc:819-852)
@@ -4119,10 +4167,10 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     HIPCHK(hipEventRecord(d->gather_ev[bi % kPipes], P.stream));
     samples_total += nc;
   }
-  unsigned long long acc[kPipes][8] = {};
+  unsigned long long acc[kPipes][2 * kAccWords] = {};
   for (int pi = 0; pi < npipes; ++pi) {
     Pipe& P = d->pipe[pi];
-    HIPCHK(hipMemcpyAsync(acc[pi], P.words.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, P.stream));
+    HIPCHK(hipMemcpyAsync(acc[pi], P.words.p, sizeof acc[pi], hipMemcpyDeviceToHost, P.stream));
     HIPCHK(hipStreamSynchronize(P.stream));
   }
   if (std::getenv("YK_LAUNCH_LOG") && !d->spec) {
@@ -4130,7 +4178,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     for (int bi = 0; bi < nbatch; ++bi) {
       const int pi = bi % npipes;
       std::vector<unsigned long long> q((size_t)qwords_per_batch);
-      HIPCHK(hipMemcpy(q.data(), d->pipe[pi].words.p + 8 + words_per_batch * (bi / npipes),
+      HIPCHK(hipMemcpy(q.data(), d->pipe[pi].words.p + 2 * kAccWords + words_per_batch * (bi / npipes),
                        q.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
       std::fprintf(stderr, "[launch-log] batch %d samples %lld:", bi, nc_of[bi]);
       for (int w = 0; w < qwords_per_batch; ++w)
@@ -4141,14 +4189,14 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   yk_stats local{};
   yk_stats* S = st ? st : &local;
   for (int pi = 0; pi < npipes; ++pi) {
-    if (acc[pi][2] || acc[pi][6])
+    if (acc[pi][2] || acc[pi][kAccWords + 2])
       return set_error(YK_ERR_INTERNAL, "kd-tree traversal watchdog fired (corrupt tree or stack)");
     S->closest_nodes += acc[pi][0];
     S->closest_tris += acc[pi][1];
     S->closest_rays += acc[pi][3];
-    S->shadow_nodes += acc[pi][4];
-    S->shadow_tris += acc[pi][5];
-    S->shadow_rays += acc[pi][7];
+    S->shadow_nodes += acc[pi][kAccWords];
+    S->shadow_tris += acc[pi][kAccWords + 1];
+    S->shadow_rays += acc[pi][kAccWords + 3];
   }
   for (const Timed& t : timed) {
     float ms = 0.f;

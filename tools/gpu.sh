@@ -17,6 +17,7 @@
 #   abc2:V1,V2,...       A/B on the Cornell (C2) bench
 #   tbab:V1,V2,...       A/B of the traversal microbenchmark only, three interleaved reps
 #   coh:VARIANT          primary-shadow ray-order experiment (tools/coherence_bench.py)
+#   pmctb:VARIANT        PMC counter passes over the traversal microbenchmark (tools/pmc_dump.py summary)
 #   multi                tests/test_multi_device.py + tests/test_0_multi_process.py
 set -e
 cd $GRAFT_REPO_ROOT
@@ -95,7 +96,26 @@ EOF
   coh:*)
     v=${s#coh:}
     YK_LIB=$(lib $v) timeout -k 10 300 python -u tools/coherence_bench.py > $O/coh_$v.json 2> $O/coh_$v.err
-    cat $O/coh_$v.json ;;
+    cat $O/coh_$v.json
+    YK_LIB=$(lib $v) timeout -k 10 300 python -u tools/coherence_bench.py --bounce > $O/cohb_$v.json 2> $O/cohb_$v.err
+    cat $O/cohb_$v.json ;;
+  pmctb:*)
+    # issue / wait / LDS / L1-TA-TD / L2 counters of the traversal kernels over
+    # the traversal microbenchmark, one rocprofv3 pass per counter set
+    v=${s#pmctb:}
+    P=$O/pmctb_$v
+    mkdir -p $P
+    YK_LIB=$(lib $v) timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $P/kt -o kt -- python3 tools/trav_bench.py --reps 1 > $P/kt.log 2>&1
+    i=0
+    for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM" \
+             "SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TD_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum" \
+             "SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM_RD SQ_INST_CYCLES_VMEM_RD SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_LEVEL_WAVES TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum" \
+             "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_SMEM SQ_INST_LEVEL_LDS SQ_INSTS_LDS_ATOMIC SQ_LDS_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL SQ_INSTS_VSKIPPED"; do
+      i=$((i+1))
+      YK_LIB=$(lib $v) timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $P/p$i -o p$i -- python3 tools/trav_bench.py --reps 1 > $P/p$i.log 2>&1
+    done
+    python3 tools/pmc_dump.py $P > $P/summary.txt
+    echo "pmctb $v done" ;;
   multi)
     timeout -k 10 600 python -u -m pytest tests/test_multi_device.py tests/test_0_multi_process.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/multi.txt 2>&1
     tail -3 $O/multi.txt ;;
