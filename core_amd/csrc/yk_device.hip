@@ -709,7 +709,7 @@ __device__ __forceinline__ unsigned dpp_max_scan(unsigned x) {
 // round; measured 0.7 % slower, so only such trees run it).
 template <bool CLOSEST, bool BIG = false, bool UNI = false>
 __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t nref, uint32_t w0,
-                                            unsigned long long* keys, float4* cand, unsigned* otab,
+                                            unsigned long long* keys, float4* cand, unsigned* otab, const float* s_tmin,
                                             unsigned& ntris, bool& occluded) {
   const int lane = lane_fresh();
   unsigned x = nref;  // inclusive prefix sum of the lanes' reference counts
@@ -739,21 +739,26 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
     // fewer than 2^17 references (64 lanes x 2^17 < 2^24)
     otab[lane] = 0u;
     if (nref > 0u && pre >= base && pre - base < 64u)
-      otab[pre - base] = ((BIG ? pre - base + 1u : pre + 1u) << 8) | (unsigned)lane;
+      otab[pre - base] = ((BIG ? pre - base : pre) << 8) + (vconst<0x100u>() | (unsigned)lane);
     __syncthreads();
     const unsigned ov = dpp_max_scan(otab[lane]);
     // slots before the round's first range start continue the range that
     // covered the previous round's last slot
     const unsigned okey = ov ? ov : carry;
     carry = (unsigned)__builtin_amdgcn_readlane((int)okey, 63);
-    const int own = (int)(okey & 0xFFu);
+    // owner lane, extracted once into a plain register (folded into SDWA
+    // shifts the compiler would keep 2, 3 and 4 in VGPRs for the whole loop)
+    int own;
+    asm volatile("v_and_b32 %0, 0xff, %1" : "=v"(own) : "v"(okey));
     const unsigned pown = BIG ? bperm(pre, own) : (okey >> 8) - 1u;
     const unsigned k = sc - pown;
     const uint32_t ow0 = bperm(w0, own), on = bperm(nref, own);
     const v3 ro = V3(bperm(st.o.x, own), bperm(st.o.y, own), bperm(st.o.z, own));
     const v3 rd = V3(bperm(st.d.x, own), bperm(st.d.y, own), bperm(st.d.z, own));
     const float rz = bperm(zlim, own);
-    const float rtmin = (CLOSEST || UNI) ? bperm(st.tmin, own) : 0.f;
+    // the owner's tmin (closest hits, universal any-hit) from LDS: one
+    // register fewer for the whole traversal than keeping it in Trav
+    const float rtmin = (CLOSEST || UNI) ? s_tmin[own] : 0.f;
     bool valid = false;
     unsigned long long key = 0;
     float th = 0.f, u = 0.f, v = 0.f;
@@ -802,7 +807,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
 }
 
 __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int src) {
-  unsigned lo = __shfl((unsigned)v, src), hi = __shfl((unsigned)(v >> 32), src);
+  const unsigned lo = bperm((unsigned)v, src), hi = bperm((unsigned)(v >> 32), src);
   return ((unsigned long long)hi << 32) | lo;
 }
 
@@ -830,7 +835,11 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
                                            unsigned long long* __restrict__ work, unsigned long long* __restrict__ ctr,
                                            uint2* __restrict__ ovf, int ovf_depth, int refill_min,
                                            float* __restrict__ tsf = nullptr, int ts_depth = 0) {
+  // LDS of the cooperative leaf test first: its owner table then sits at
+  // offset 0, and its addresses need no base register
+  __shared__ unsigned otab[64];
   __shared__ uint2 lds[kStackLds * 64];
+  __shared__ float s_tmin[(CLOSEST || UNI) ? 64 : 1];  // the lanes' tmin, read by the cooperative leaf test
   const int lane = threadIdx.x;
   const long long n = __builtin_amdgcn_readfirstlane((int)rc.get());
   if (blockIdx.x == 0 && lane == 0 && n > 0) atomicAdd(&ctr[3], (unsigned long long)n);  // rays traced
@@ -897,6 +906,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       const unsigned avail = pool_end - pool_next;
       unsigned cb = 0, ce = 0;  // newly grabbed chunk [cb, ce)
       if (avail < cnt && seg_done != kAll) {
+#pragma unroll 1  // rolled: an unrolled search held every segment's bounds in SGPRs (spilled to VGPR lanes)
         for (unsigned k = 0; k < (unsigned)NSEG; ++k) {
           const unsigned sgi = (xcc + k) % (unsigned)NSEG;
           if (seg_done & (1u << sgi)) continue;
@@ -929,6 +939,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
           if (trav_begin<CLOSEST, TS, UNI>(S, st, ray)) {
             rid = r;
             ray_n0[lane_fresh()] = nnodes;
+            if (CLOSEST || UNI) s_tmin[lane_fresh()] = st.tmin;
           } else if (CLOSEST) {
             hits[r] = yk_hit{-1, 0.f, 0.f, 0.f};
           } else {
@@ -972,7 +983,6 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
     if constexpr (!TS) {
       __shared__ unsigned long long keys[64];
       __shared__ float4 cand[CLOSEST ? 64 : 1];
-      __shared__ unsigned otab[64];
       const bool act = rid >= 0;
       bool live = false;
       uint32_t w0 = 0, nref = 0;
@@ -987,7 +997,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       }
 #endif
       bool occ = false;
-      coop_leaves<CLOSEST, BIG, UNI>(S, st, (live && !paused) ? nref : 0u, w0, keys, cand, otab, ntris, occ);
+      coop_leaves<CLOSEST, BIG, UNI>(S, st, (live && !paused) ? nref : 0u, w0, keys, cand, otab, s_tmin, ntris, occ);
 #ifdef YK_TRAV_STATS
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       {
@@ -1808,23 +1818,32 @@ __device__ __forceinline__ void put_ray(yk_ray& r, v3 f, v3 d, float tmin, float
 // (resolve_light), so slots without it store the flag alone: on C2 the
 // shading kernels are write-bound (k_shade_bounce writes ~280 B per path
 // vertex) and most MIS-half slots carry no contribution.
-typedef float f3v __attribute__((ext_vector_type(3)));
+// 12-B records at float offset 3*slot: copied as exactly 12 bytes (one
+// dwordx3 access), never through a vec3 type whose size and alignment are 16
+// (a 16-B access would touch the next slot's red channel)
 __device__ __forceinline__ void put_slot(const Batch& B, long long slot, uint8_t fl, c3 v) {
   B.sl_flags[slot] = fl;
   if (fl & SL_ADDS) {
-    f3v x;
-    x.x = v.r;
-    x.y = v.g;
-    x.z = v.b;
-    *reinterpret_cast<f3v*>(B.sl_contrib + 3 * slot) = x;
+    const float x[3] = {v.r, v.g, v.b};
+    __builtin_memcpy(B.sl_contrib + 3 * slot, x, 12);
   }
 }
 __device__ __forceinline__ c3 get_contrib(const Batch& B, long long slot) {
-  const f3v x = *reinterpret_cast<const f3v*>(B.sl_contrib + 3 * slot);
-  return C3(x.x, x.y, x.z);
+  float x[3];
+  __builtin_memcpy(x, B.sl_contrib + 3 * slot, 12);
+  return C3(x[0], x[1], x[2]);
 }
 __device__ __forceinline__ void put_aux(const Batch& B, long long slot, float a, float b, float c, float d) {
   *reinterpret_cast<float4*>(B.sl_aux + 4 * slot) = make_float4(a, b, c, d);
+}
+
+// a shadow ray of slot `slot`, stored for the any-hit launch: bit kbit of
+// `traced`, one queued ray
+__device__ __forceinline__ int emit_shadow(const Batch& B, long long slot, const yk_ray& sr, int kbit,
+                                           unsigned long long& traced) {
+  st_ray(&B.s_rays[slot], sr);
+  if (kbit < 64) traced |= 1ull << kbit;
+  return 1;
 }
 
 // mcIntegrator_t::doLightEstimation (area light), mcintegrator.cc:73-195, split
@@ -1846,24 +1865,24 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
       put_slot(B, slot, 0, black);
       return 0;
     }
+    int nq;
     {
       yk_ray sr;
       put_ray(sr, sp.P, ldir, YK_SHADOW_BIAS, ltmax);
-      st_ray(&B.s_rays[slot], sr);
+      nq = emit_shadow(B, slot, sr, k0, traced);
     }
-    if (k0 < 64) traced |= 1ull << k0;
     const c3 surf = mat_eval(M, sp, wo, ldir);
     const float f = fabsf(vdot(sp.N, ldir));
     if (B.ts) {  // lcol *= scol first (mcintegrator.cc:94): keep the parts
       put_slot(B, slot, SL_TRACED | SL_ADDS, surf);
       put_aux(B, slot, f, lc.r, lc.g, lc.b);
-      return 1;
+      return nq;
     }
     // compiled form of surfCol*lcol*|N.l|*transmitCol (transmitCol = 1):
     // R,G (lcol*surf)*f, B surf*(lcol*f)
     put_slot(B, slot, SL_TRACED | SL_ADDS,
              C3((lc.r * surf.r) * f, (lc.g * surf.g) * f, surf.b * (lc.b * f)));
-    return 1;
+    return nq;
   }
   const int n = L.samples;
   const unsigned offs = (unsigned)(n * (int)pixelSample) + soffs + loffs * 4567u;
@@ -1885,10 +1904,8 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
     {
       yk_ray sr;
       put_ray(sr, sp.P, ldir, YK_SHADOW_BIAS, ltmax);
-      st_ray(&B.s_rays[slot], sr);
+      nr += emit_shadow(B, slot, sr, k0 + i, traced);
     }
-    ++nr;
-    if (k0 + i < 64) traced |= 1ull << (k0 + i);
     if (!(lpdf > 1e-6f)) {
       put_slot(B, slot, SL_TRACED, black);
       continue;
@@ -1932,10 +1949,8 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
     {
       yk_ray sr;
       put_ray(sr, sp.P, bdir, YK_MIN_RAYDIST, bt);
-      st_ray(&B.s_rays[slot], sr);
+      nr += emit_shadow(B, slot, sr, k0 + n + i, traced);
     }
-    ++nr;
-    if (k0 + n + i < 64) traced |= 1ull << (k0 + n + i);
     if (!(lightPdf > 1e-6f)) {
       put_slot(B, slot, SL_TRACED, black);
       continue;
@@ -3335,6 +3350,7 @@ void launch_trace(yk_device* d, Pipe& P, const yk_ray* rays, long long n, yk_hit
 }
 
 inline unsigned grid_for(long long n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+
 // traversal stack entries hold (node + 1) in 30 bits
 constexpr size_t kMaxNodes = (1u << 30) - 2u;
 // leaves of this many references need the BIG owner keys (coop_leaves)
@@ -3353,6 +3369,18 @@ constexpr uint32_t kBigLeaf = 1u << 17;
 // of at most 2^16 nodes, as a per-scene value: the runtime divisor made the
 // closest-hit kernel spill 9 VGPRs instead of 4, headline 2904 against 2950,
 // for no C2 gain in the same A/B: 8927 against 8925.)
+// crowded-leaf trees (mean references per non-empty leaf above
+// YK_CROWDED_LEAF, default 8): the hair scene's; one threshold for the host
+// and the device-built tree
+bool crowded(long long filled_leaves, long long leaf_refs) {
+  static const double crowd = [] {
+    const char* e = std::getenv("YK_CROWDED_LEAF");
+    return e ? std::atof(e) : 8.0;
+  }();
+  const double mean = filled_leaves > 0 ? (double)leaf_refs / (double)filled_leaves : 0.0;
+  return mean > crowd;
+}
+
 void set_handout(yk_device* d, size_t nn) {
   const char* e = std::getenv("YK_REFILL_SHADOW");
   const int rs = e ? std::atoi(e) : 0;
@@ -3565,13 +3593,8 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
     install_traversal(d, nn, S.tree.leaf_prims.size(), max_refs);
   }
   {
-    static const double crowd = [] {
-      const char* e = std::getenv("YK_CROWDED_LEAF");
-      return e ? std::atof(e) : 8.0;
-    }();
     const long long filled = (long long)S.tree.stats.leaves - S.tree.stats.empty_leaves;
-    const double mean = filled > 0 ? (double)S.tree.stats.leaf_prims / (double)filled : 0.0;
-    d->crowded_leaves = mean > crowd;
+    d->crowded_leaves = crowded(filled, (long long)S.tree.stats.leaf_prims);
     set_handout(d, nn);
   }
   d->nlights = (int)S.light_states.size();
