@@ -9,7 +9,7 @@
 #   bench                headline bench.py (1M tris, 1080p, 256 spp)
 #   c2 | pm | hair       BASELINE configs[1] Cornell / photon mapping / C5 hair benches
 #   prof                 rocprofv3 --kernel-trace --stats of the one-pipe headline frame
-#   prof_c2 | prof_hair  the same for the Cornell / hair frames
+#   prof_c2 | prof_hair | prof_pm  the same for the Cornell / hair / photon-mapping frames
 #   pmc                  FETCH_SIZE and WRITE_SIZE passes of the one-pipe headline frame
 #   pmc_c2 | pmc_hair    the same for Cornell / hair
 #   tb:VARIANT           traversal microbenchmark (tools/trav_bench.py)
@@ -28,6 +28,7 @@ mkdir -p $O
 lib() { if [ "$1" = base ]; then echo $PWD/core_amd/libyk.so; else echo $PWD/tune/libyk_$1.so; fi; }
 C2="--scene cornell --width 1024 --height 1024 --spp 64"
 HAIR="--scene hair --spp 16"
+PM="--integrator photon --spp 16"
 P1="--pipes 1 --steps 1 --warmup 0 --no-cpu --no-roofline-frame"
 for s in "$@"; do
   case $s in
@@ -44,13 +45,13 @@ for s in "$@"; do
     timeout -k 10 300 python -u bench.py $C2 > $O/bench_c2.json 2> $O/bench_c2.err
     head -c 300 $O/bench_c2.json; echo ;;
   pm)
-    timeout -k 10 400 python -u bench.py --integrator photon --spp 16 > $O/bench_pm.json 2> $O/bench_pm.err
+    timeout -k 10 400 python -u bench.py $PM > $O/bench_pm.json 2> $O/bench_pm.err
     head -c 300 $O/bench_pm.json; echo ;;
   hair)
     timeout -k 10 500 python -u bench.py $HAIR --no-cpu > $O/bench_hair.json 2> $O/bench_hair.err
     head -c 300 $O/bench_hair.json; echo ;;
-  prof|prof_c2|prof_hair)
-    A=""; [ $s = prof_c2 ] && A="$C2"; [ $s = prof_hair ] && A="$HAIR"
+  prof|prof_c2|prof_hair|prof_pm)
+    A=""; [ $s = prof_c2 ] && A="$C2"; [ $s = prof_hair ] && A="$HAIR"; [ $s = prof_pm ] && A="$PM"
     timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$s -o p1 -- python3 bench.py $A $P1 > $O/$s.log 2>&1
     echo "$s done" ;;
   pmc|pmc_c2|pmc_hair)
