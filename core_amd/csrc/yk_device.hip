@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -177,7 +178,10 @@ __device__ __forceinline__ bool bound_cross(const float* bb, v3 from, v3 dir, fl
 // entry stores t itself. The top kStackLds entries of every lane live in an
 // LDS ring; deeper ones spill to a global overflow area (rare: a 1M-tri tree
 // has depth ~40 but a ray rarely holds more than a dozen pending exits).
-constexpr int kStackLds = 8;  // LDS ring depth per lane (16 measured slower: 1807 vs 2054, round 1)
+#ifndef YK_STACK_LDS
+#define YK_STACK_LDS 8
+#endif
+constexpr int kStackLds = YK_STACK_LDS;  // LDS ring depth per lane (16 measured slower: 1807 vs 2054, round 1)
 // accumulator words per traversal kernel kind ({nodes, triangle tests, errors,
 // rays}; the YK_TRAV_STATS diagnostic build adds its cycle counters, ctr[4..12])
 #ifdef YK_TRAV_STATS
@@ -709,7 +713,8 @@ __device__ __forceinline__ unsigned dpp_max_scan(unsigned x) {
 // round; measured 0.7 % slower, so only such trees run it).
 template <bool CLOSEST, bool BIG = false, bool UNI = false>
 __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t nref, uint32_t w0,
-                                            unsigned long long* keys, float4* cand, unsigned* otab, const float* s_tmin,
+                                            std::conditional_t<CLOSEST, unsigned long long, unsigned>* keys,
+                                            float4* cand, unsigned* otab, const float* s_tmin,
                                             unsigned& ntris, bool& occluded) {
   const int lane = lane_fresh();
   unsigned x = nref;  // inclusive prefix sum of the lanes' reference counts
@@ -726,7 +731,8 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
   if (total == 0u) return;
   {
     const unsigned m1 = vconst<0xFFFFFFFFu>();
-    keys[lane] = ((unsigned long long)m1 << 32) | m1;
+    if (CLOSEST) keys[lane] = ((unsigned long long)m1 << 32) | m1;
+    else keys[lane] = m1;  // any-hit keys are reference indices: 32 bits
   }
   __syncthreads();  // one wave per block: orders the LDS traffic of the phase
   const float zlim = CLOSEST ? st.Z : st.dist;
@@ -781,7 +787,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
             key = ((unsigned long long)ord_key(th) << 32) | k;
             atomicMin(&keys[own], key);
           } else {
-            atomicMin(&keys[own], (unsigned long long)k);
+            atomicMin(&keys[own], k);
           }
         }
       }
@@ -793,7 +799,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
   }
   __syncthreads();
   if (nref > 0u) {
-    const unsigned long long kk = keys[lane];
+    const unsigned long long kk = CLOSEST ? (unsigned long long)keys[lane] : (keys[lane] == ~0u ? ~0ull : keys[lane]);
     if (CLOSEST) {
       ntris += nref;
       if (kk != ~0ull) st.Z = cand[lane].x;  // (t, b1, b2, prim) stay in cand[lane]
@@ -840,6 +846,9 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   __shared__ unsigned otab[64];
   __shared__ uint2 lds[kStackLds * 64];
   __shared__ float s_tmin[(CLOSEST || UNI) ? 64 : 1];  // the lanes' tmin, read by the cooperative leaf test
+  // any-hit results awaiting their store: (ray index << 1) | occluded
+  __shared__ unsigned res_slot[(!CLOSEST && !TS) ? 128 : 1];
+  unsigned npend = 0;  // wave-uniform
   const int lane = threadIdx.x;
   const long long n = __builtin_amdgcn_readfirstlane((int)rc.get());
   if (blockIdx.x == 0 && lane == 0 && n > 0) atomicAdd(&ctr[3], (unsigned long long)n);  // rays traced
@@ -981,7 +990,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
     s_act += (unsigned long long)__popcll(__ballot(rid >= 0));
 #endif
     if constexpr (!TS) {
-      __shared__ unsigned long long keys[64];
+      __shared__ std::conditional_t<CLOSEST, unsigned long long, unsigned> keys[64];
       __shared__ float4 cand[CLOSEST ? 64 : 1];
       const bool act = rid >= 0;
       bool live = false;
@@ -1006,6 +1015,8 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
         c_t0 = t;
       }
 #endif
+      bool fin = false;  // any-hit: a result to stage
+      int fin_rid = 0;
       if (act) {
         bool done = !live || occ || (!paused && trav_next<CLOSEST>(S, st, stk));
         if (runaway) {
@@ -1023,9 +1034,34 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
             }
             hits[rid] = h;
           } else {
-            occl[rid] = occ ? 1 : 0;
+            fin = true;
+            fin_rid = rid;
           }
           rid = -1;
+        }
+      }
+      if (!CLOSEST) {
+        // Any-hit results are staged in LDS and written 64 at a time: one
+        // store instruction then covers the consecutive slots of the rays
+        // that just finished (mostly a few cache lines), where a 1-B store
+        // per finishing lane left ~33 B of partial-line HBM writes per ray
+        // (round 3 PMC: 30x the result bytes)
+        const unsigned long long fm = __builtin_amdgcn_ballot_w64(fin);
+        if (fm) {
+          const unsigned rk = __builtin_amdgcn_mbcnt_hi((unsigned)(fm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)fm, 0u));
+          if (fin) {
+            res_slot[npend + rk] = ((unsigned)fin_rid << 1) | (occ ? 1u : 0u);
+          }
+          npend += (unsigned)__popcll(fm);
+          if (npend >= 64u) {
+            __syncthreads();
+            const int l = lane_fresh();
+            const unsigned e = res_slot[l];
+            occl[e >> 1] = (uint8_t)(e & 1u);
+            if (l + 64u < npend) res_slot[l] = res_slot[l + 64];
+            npend -= 64u;
+            __syncthreads();
+          }
         }
       }
 #ifdef YK_TRAV_STATS
@@ -1087,6 +1123,14 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
     atomicAdd(&ctr[12], c_pop);
   }
 #endif
+  if (!CLOSEST && !TS && npend) {  // the staged results left
+    __syncthreads();
+    const int l = lane_fresh();
+    if ((unsigned)l < npend) {
+      const unsigned e = res_slot[l];
+      occl[e >> 1] = (uint8_t)(e & 1u);
+    }
+  }
   // wave-reduced work counters (nodes visited, triangle tests)
   unsigned long long a = nnodes, b = ntris;
 #pragma unroll
@@ -1629,6 +1673,7 @@ struct Batch {
   uint8_t* sl_flags;    // 1 per slot
   float4* samples;      // final RGBA per camera sample
   float2* sxy;          // (dx, dy) of the sample inside its pixel
+  char4* pext;          // per pixel slot: footprint extent of its samples (k_pixel_extent)
   int K;
   long long cap;  // samples per batch: the stride of the shadow-slot arrays
   // specular recursion (recursiveRaytrace) only, see k_spawn / k_fold
@@ -2537,6 +2582,37 @@ __device__ __forceinline__ int round2int(double v) { return (int)(v + (0.5 - 1.4
 constexpr int kGatherGroup = 8;  // samples loaded per group (16 measured equal)
 __device__ __forceinline__ int floor2int(double v) { return (int)floor(v); }
 
+// Footprint extent of every source pixel of a batch: over its samples, the
+// smallest dx0 / dy0 and the largest dx1 / dy1 of addSample's target window
+// (the same Round2Int expressions as the gather). A target offset outside
+// them can take no sample of the pixel, so the gather skips the pixel's
+// sample loop: with a box filter a pixel's samples reach its 8 neighbours
+// almost never, and those loops were ~8/9 of the gather's work. One wave per
+// pixel slot (slot i = samples [i*spp, (i+1)*spp) of the batch).
+__global__ void __launch_bounds__(256) k_pixel_extent(FilmConst F, const float2* __restrict__ sxy,
+                                                      char4* __restrict__ ext, long long npix) {
+  const long long slot = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (slot >= npix) return;
+  int x0 = 127, x1 = -128, y0 = 127, y1 = -128;
+  for (int s = lane; s < F.spp; s += 64) {
+    const float2 d = sxy[slot * F.spp + s];
+    const double dx = d.x, dy = d.y;
+    x0 = min(x0, round2int(dx - F.filterw));
+    x1 = max(x1, round2int(dx + F.filterw - 1.0));
+    y0 = min(y0, round2int(dy - F.filterw));
+    y1 = max(y1, round2int(dy + F.filterw - 1.0));
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    x0 = min(x0, __shfl_xor(x0, off));
+    x1 = max(x1, __shfl_xor(x1, off));
+    y0 = min(y0, __shfl_xor(y0, off));
+    y1 = max(y1, __shfl_xor(y1, off));
+  }
+  if (lane == 0) ext[slot] = make_char4((signed char)x0, (signed char)x1, (signed char)y0, (signed char)y1);
+}
+
 // imageFilm_t::addSample as a gather (imagefilm.cc:453-511): each thread owns
 // one target pixel and adds every covering sample of the batch in the
 // reference's single-thread order -- tiles row-major, then rows, columns and
@@ -2546,7 +2622,8 @@ __device__ __forceinline__ int floor2int(double v) { return (int)floor(v); }
 // columns.
 __global__ void __launch_bounds__(256) k_film_gather(FilmConst F, const float4* __restrict__ samples,
                                                      const float2* __restrict__ sxy, const int* __restrict__ tile_base,
-                                                     float* __restrict__ film, int rx0, int ry0, int rw, int rh) {
+                                                     const char4* __restrict__ ext, float* __restrict__ film,
+                                                     int rx0, int ry0, int rw, int rh) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (tid >= rw * rh) return;
   const int tx = rx0 + tid % rw, ty = ry0 + tid / rw;
@@ -2581,6 +2658,10 @@ __global__ void __launch_bounds__(256) k_film_gather(FilmConst F, const float4* 
             cbase = tb + (long long)((sy - Y) * W + (sx - X)) * F.spp;
           }
           const int ox = tx - sx, oy = ty - sy;
+          {  // no sample of this source pixel reaches the target (k_pixel_extent)
+            const char4 e = ext[cbase / F.spp];
+            if (ox < e.x || ox > e.y || oy < e.z || oy > e.w) continue;
+          }
           // samples in groups of kGatherGroup: the group's positions, then the
           // colours of the accepted ones, are loaded together (independent
           // loads in flight instead of one dependent round trip per sample);
@@ -2774,10 +2855,12 @@ struct Pipe {
   DBuf<uint8_t> sl_flags, s_occl;
   DBuf<float4> samples;
   DBuf<float2> sxy;
+  DBuf<char4> pext;
   DBuf<unsigned> psample;
   DBuf<uint8_t> incl, caus;
   DBuf<float> emit0;
   DBuf<float> fgl, fglen;  // final gathering: lcol (3 per sample) and path length
+  DBuf<float4> lkq;        // final gathering: radiance-map lookup queue (point | owner, normal)
   DBuf<float> s_filt, sl_aux;  // transparent shadows
   void create() {
     HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -2826,6 +2909,7 @@ struct Pipe {
     sl_flags.ensure(maxc * K);
     samples.ensure(maxc);
     sxy.ensure(maxc);
+    pext.ensure(maxc);  // one per pixel slot; maxc bounds the slots of any spp
     tiles.ensure(tiles_per_batch);
     tile_base.ensure(tiles_per_batch + 1);
     Batch B{};
@@ -2855,6 +2939,7 @@ struct Pipe {
     B.sl_flags = sl_flags.p;
     B.samples = samples.p;
     B.sxy = sxy.p;
+    B.pext = pext.p;
     B.K = K;
     B.cap = maxc;
     if (ts) {
@@ -2917,6 +3002,7 @@ struct yk_device {
   int refill = 24;  // idle lanes before a traversal wave refills (set_handout)
   int refill_shadow = 24;  // the same for the any-hit kernels
   int per_cu_ts = 1;
+  int per_cu_lookup[2] = {1, 1};  // k_pm_lookup<false / true> resident waves per CU
   // node store of the specular recursion (k_finish_spec / k_spawn / k_fold)
   DBuf<float> nE, nD, nP, nrcol, nalpha, nmalpha;
   DBuf<int> nflags, nchild, noverflow;
@@ -3443,6 +3529,10 @@ int yk_device_open(int32_t ordinal, yk_device** out) {
   d->per_cu_big[1] = std::max(1, blocks);
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow_ts, 64, 0));
   d->per_cu_ts = std::max(1, blocks);
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_pm_lookup<false>, 64, 0));
+  d->per_cu_lookup[0] = std::max(1, blocks);
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_pm_lookup<true>, 64, 0));
+  d->per_cu_lookup[1] = std::max(1, blocks);
   upload_qmc();
   *out = d;
   return YK_OK;
@@ -3951,11 +4041,12 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
 
   // ---- per-pipe device words: [0, 2 kAccWords) accumulators {closest
   // nodes, tris, errors, rays; any-hit ...}; then per batch: queue-count words
-  // (isub, depth) and one 128-word ray-segment block per trace launch.
+  // (isub, depth), the final gather's lookup-queue counts (isub, depth) and
+  // one 128-word hand-out block per trace or lookup launch.
   // All zeroed once; no launch needs a reset or a host round trip.
   const int qwords_per_batch = nsub * (bounces + 1);
-  const int launches_per_batch = 2 + 2 * nsub * bounces;
-  const long long words_per_batch = qwords_per_batch + 128ll * launches_per_batch;
+  const int launches_per_batch = 2 + 2 * nsub * bounces + (R.pm_fg ? nsub * bounces : 0);
+  const long long words_per_batch = 2ll * qwords_per_batch + 128ll * launches_per_batch;
   Batch Bp[kPipes];
   for (int pi = 0; pi < npipes; ++pi) {
     Pipe& P = d->pipe[pi];
@@ -3966,6 +4057,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     if (R.pm_fg) {
       P.fgl.ensure(3 * maxc);
       P.fglen.ensure(maxc);
+      P.lkq.ensure(2 * maxc);
     }
   }
   NodeStore NS{};
@@ -4018,7 +4110,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     int launch = 0;
     auto trace = [&](bool closest, const yk_ray* rays, const unsigned* idx, RayCount n, yk_hit* hits,
                      uint8_t* occ) {
-      unsigned long long* work = bw + qwords_per_batch + 128ll * launch++;
+      unsigned long long* work = bw + 2ll * qwords_per_batch + 128ll * launch++;
       const hipEvent_t e0 = P.event(evn[pi]), e1 = P.event(evn[pi] + 1);
       timed.push_back(Timed{pi, evn[pi], closest});
       evn[pi] += 2;
@@ -4045,11 +4137,20 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
           const unsigned long long* in_w = qw(isub, it);
           unsigned long long* out_w = qw(isub, it + 1);
           trace(true, Bc.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, Bc.q_hits[qin], nullptr);
-          hipLaunchKernelGGL(d->rm_depth <= kLdsPStack ? k_fg_hit<true> : k_fg_hit<false>, dim3(grid_for(n, YK_APPEND_BLOCK)), dim3(YK_APPEND_BLOCK), 0,
+          unsigned long long* lk_w = qw(isub, it) + qwords_per_batch;  // lookup-queue count
+          hipLaunchKernelGGL(k_fg_hit, dim3(grid_for(n, YK_APPEND_BLOCK)), dim3(YK_APPEND_BLOCK), 0,
                              P.stream, d->S, Bc, Rc, PMC, in_w, it, isub, qin,
-                             P.fgl.p, P.fglen.p, out_w);
+                             P.fgl.p, P.fglen.p, out_w, P.lkq.p, lk_w);
           HIPCHK(hipGetLastError());
           if (it < p->photon.fg_bounces) trace(false, Bc.s_rays, Bc.s_idx, RayCount{out_w, 0, 0}, nullptr, Bc.s_occl);
+          {
+            const bool lds = d->rm_depth <= kLdsPStack;
+            unsigned long long* work = bw + 2ll * qwords_per_batch + 128ll * launch++;
+            hipLaunchKernelGGL(lds ? k_pm_lookup<true> : k_pm_lookup<false>,
+                               dim3((unsigned)((long long)d->cus * d->per_cu_lookup[lds ? 1 : 0])), dim3(64), 0,
+                               P.stream, PMC.rmap, PMC.lookup_rad, P.lkq.p, lk_w, P.fgl.p, work);
+            HIPCHK(hipGetLastError());
+          }
           hipLaunchKernelGGL(k_fg_resolve, dim3(grid_for(n)), dim3(256), 0, P.stream, Bc, Rc, in_w, qin, P.fgl.p);
           HIPCHK(hipGetLastError());
           qin ^= 1;
@@ -4183,8 +4284,11 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     const int gx1 = std::min(F.cx1, rc.z + F.ohi_x), gy1 = std::min(F.cy1, rc.w + F.ohi_y);
     const int gw = gx1 - gx0, gh = gy1 - gy0;
     if (gw > 0 && gh > 0) {
+      const long long npix = nc / spp;  // the batch's pixel slots (spp samples each)
+      hipLaunchKernelGGL(k_pixel_extent, dim3(grid_for(npix * 64)), dim3(256), 0, P.stream, Fb, B.sxy, B.pext, npix);
+      HIPCHK(hipGetLastError());
       hipLaunchKernelGGL(k_film_gather, dim3(grid_for((long long)gw * gh)), dim3(256), 0, P.stream, Fb, B.samples,
-                         B.sxy, TL.base, d_film, gx0, gy0, gw, gh);
+                         B.sxy, TL.base, B.pext, d_film, gx0, gy0, gw, gh);
       HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(d->gather_ev[bi % kPipes], P.stream));

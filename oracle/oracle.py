@@ -2,6 +2,10 @@
 
 TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
 cpu_baseline leg of bench.py, never by the product (core_amd/).
+
+Parity unpinned under this tier's rule (no reference golden vectors, no
+oracle/_ref build): the oracle equals every survey-build reference output in
+tests/golden/ bit for bit, which DESIGN.md §6 records as evidence only.
 """
 import ctypes as C
 import os

@@ -15,6 +15,7 @@
 #   tb:VARIANT           traversal microbenchmark (tools/trav_bench.py)
 #   ab:V1,V2,...         A/B: trav bench + headline bench per variant, two interleaved reps
 #   abc2:V1,V2,...       A/B on the Cornell (C2) bench
+#   abpm:V1,V2,...       A/B on the photon-mapping bench
 #   tbab:V1,V2,...       A/B of the traversal microbenchmark only, three interleaved reps
 #   coh:VARIANT          primary-shadow ray-order experiment (tools/coherence_bench.py)
 #   pmctb:VARIANT        PMC counter passes over the traversal microbenchmark (tools/pmc_dump.py summary)
@@ -63,9 +64,9 @@ for s in "$@"; do
     v=${s#tb:}
     YK_LIB=$(lib $v) timeout -k 10 200 python -u tools/trav_bench.py --spp 4 > $O/tb_$v.json 2> $O/tb_$v.err
     cat $O/tb_$v.json ;;
-  ab:*|abc2:*)
+  ab:*|abc2:*|abpm:*)
     VS=$(echo ${s#*:} | tr , ' ')
-    BA="--no-cpu --steps 2 --warmup 1 --no-roofline-frame"; [ ${s%%:*} = abc2 ] && BA="$BA $C2"
+    BA="--no-cpu --steps 2 --warmup 1 --no-roofline-frame"; [ ${s%%:*} = abc2 ] && BA="$BA $C2"; [ ${s%%:*} = abpm ] && BA="$BA $PM"
     for rep in 1 2; do
       for v in $VS; do
         L=$(lib $v)
