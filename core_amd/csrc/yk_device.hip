@@ -3018,9 +3018,11 @@ struct yk_device {
   yk_photon_params pm_params{};
   DBuf<uint2> dm_nodes, rm_nodes, cm_nodes;
   DBuf<float4> dm_pos, dm_dir, dm_col, rm_pos, rm_dir, rm_col, cm_pos, cm_dir, cm_col;
+  DBuf<uint4> rm_pk;  // radiance tree as 16-B nodes (k_pm_lookup): split | axis, right; leaf: position | photon
   std::vector<float> dm_host, rm_host, cm_host;  // 9 floats per photon, photon-vector order
   int dm_paths = 0, cm_paths = 0;
   int rm_depth = 0;  // radiance kd-tree depth (k_fg_hit keeps its lookup stack in LDS up to kLdsPStack)
+  size_t rm_nnodes = 0;  // radiance kd-tree nodes
   std::vector<unsigned> mat_flags;  // bsdfFlags per material
   Pipe pipe[kPipes];
   hipEvent_t gather_ev[kPipes] = {};
@@ -3390,6 +3392,11 @@ void enqueue_trace_ts(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned*
   if (ev1) HIPCHK(hipEventRecord(ev1, P.stream));
 }
 
+// k_pm_lookup keeps its stack in LDS (6 B per entry, depth entries per lane)
+// for radiance trees of < 2^16 nodes and depth <= kLdsPStack; else scratch.
+bool lookup_lds(const yk_device* d) { return d->rm_depth <= kLdsPStack && d->rm_nnodes < 65536; }
+size_t lookup_lds_bytes(int depth) { return (size_t)std::max(1, depth) * 64 * (sizeof(float) + sizeof(unsigned short)); }
+
 // Ray-query entry points: one launch, synchronised, statistics added to st.
 template <bool CLOSEST>
 void launch_trace(yk_device* d, Pipe& P, const yk_ray* rays, long long n, yk_hit* hits, uint8_t* occ, yk_stats* st) {
@@ -3531,8 +3538,6 @@ int yk_device_open(int32_t ordinal, yk_device** out) {
   d->per_cu_ts = std::max(1, blocks);
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_pm_lookup<false>, 64, 0));
   d->per_cu_lookup[0] = std::max(1, blocks);
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_pm_lookup<true>, 64, 0));
-  d->per_cu_lookup[1] = std::max(1, blocks);
   upload_qmc();
   *out = d;
   return YK_OK;
@@ -4144,11 +4149,12 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
           HIPCHK(hipGetLastError());
           if (it < p->photon.fg_bounces) trace(false, Bc.s_rays, Bc.s_idx, RayCount{out_w, 0, 0}, nullptr, Bc.s_occl);
           {
-            const bool lds = d->rm_depth <= kLdsPStack;
+            const bool lds = lookup_lds(d);
             unsigned long long* work = bw + 2ll * qwords_per_batch + 128ll * launch++;
             hipLaunchKernelGGL(lds ? k_pm_lookup<true> : k_pm_lookup<false>,
-                               dim3((unsigned)((long long)d->cus * d->per_cu_lookup[lds ? 1 : 0])), dim3(64), 0,
-                               P.stream, PMC.rmap, PMC.lookup_rad, P.lkq.p, lk_w, P.fgl.p, work);
+                               dim3((unsigned)((long long)d->cus * d->per_cu_lookup[lds ? 1 : 0])), dim3(64),
+                               lds ? lookup_lds_bytes(d->rm_depth) : 0, P.stream, PMC.rmap, PMC.lookup_rad,
+                               d->rm_depth, P.lkq.p, lk_w, P.fgl.p, work);
             HIPCHK(hipGetLastError());
           }
           hipLaunchKernelGGL(k_fg_resolve, dim3(grid_for(n)), dim3(256), 0, P.stream, Bc, Rc, in_w, qin, P.fgl.p);
