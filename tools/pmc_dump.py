@@ -1,5 +1,5 @@
 """Per-kernel sums of every counter in rocprofv3 --pmc counter_collection.csv
-files under DIR/p*/ (tools/gpu_pmc_tb.sh), with kernel durations from
+files under DIR/p*/ (tools/gpu.sh pmctb:VARIANT), with kernel durations from
 DIR/kt and a few derived ratios.  python tools/pmc_dump.py DIR [kernel-regex, default "trace"]"""
 import csv
 import glob
