@@ -1564,6 +1564,11 @@ __device__ __forceinline__ bool dirac_illum(const DLight& L, v3 P, v3& ldir, flo
 #ifndef YK_BOUNCE_APPEND_WAVE
 #define YK_BOUNCE_APPEND_WAVE true
 #endif
+#ifdef YK_BOUNCE_WAVES  // occupancy target of k_shade_bounce (A/B builds)
+#define YK_BOUNCE_ATTR __attribute__((amdgpu_waves_per_eu(YK_BOUNCE_WAVES)))
+#else
+#define YK_BOUNCE_ATTR
+#endif
 #ifndef YK_APPEND_BLOCK
 #define YK_APPEND_BLOCK 512  // photon / final-gather kernels
 #endif
@@ -2235,7 +2240,7 @@ __global__ void __launch_bounds__(YK_BOUNCE_BLOCK) k_path_start(DScene S, Batch 
 // (pathtracer.cc:189-298): estimateOneDirectLight shadow rays, emission,
 // and the BSDF sample of the next segment. One thread per live path (entry
 // qi of the input bounce queue, owned by camera sample c).
-__global__ void __launch_bounds__(YK_BOUNCE_BLOCK) k_shade_bounce(DScene S, Batch B, RenderConst R,
+__global__ void __launch_bounds__(YK_BOUNCE_BLOCK) YK_BOUNCE_ATTR k_shade_bounce(DScene S, Batch B, RenderConst R,
                                                       const unsigned long long* __restrict__ qin_word, int depth,
                                                       int isub, int qin, unsigned long long* __restrict__ qword) {
   const long long nq = (long long)(*qin_word >> 32);  // live paths (device-side count)
