@@ -73,6 +73,9 @@ CASES = [
     ("spec", {"caustic_photons": 20000, "caustic_radius": 0.1, "caustic_mix": 20}),
     ("spec", {"caustic_photons": 20000, "caustic_radius": 0.1, "final_gather": 0, "fg_min_pathlen": 0.5}),
     ("spec_bg", {"caustic_photons": 30000, "caustic_radius": 0.08, "fg_min_pathlen": 0.6, "fg_bounces": 3}),
+    # 35.9k radiance photons: a radiance tree of >= 2^16 nodes, whose final-gather
+    # lookups (k_pm_lookup) keep their stack in scratch instead of LDS
+    ("cornell", {"photons": 300000, "diffuse_radius": 0.02, "search": 20}),
 ]
 
 
