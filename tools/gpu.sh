@@ -20,6 +20,7 @@
 #   coh:VARIANT          primary-shadow ray-order experiment (tools/coherence_bench.py)
 #   pmctb:VARIANT        PMC counter passes over the traversal microbenchmark (tools/pmc_dump.py summary)
 #   multi                tests/test_multi_device.py + tests/test_0_multi_process.py
+#   mallocs              hipMalloc count of 1 vs 3 yk_render_multi calls (rocprofv3 --hip-trace)
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -118,6 +119,17 @@ EOF
     done
     python3 tools/pmc_dump.py $P > $P/summary.txt
     echo "pmctb $v done" ;;
+  mallocs)
+    for k in 1 3; do
+      timeout -k 10 300 rocprofv3 --hip-trace --output-format csv -d $O/mallocs_$k -o m -- python3 tools/multi_malloc_trace.py --calls $k > $O/mallocs_$k.log 2>&1
+      python3 - $O/mallocs_$k $k <<'PY'
+import csv, glob, sys
+n = 0
+for f in glob.glob(sys.argv[1] + "/**/*hip_api_trace.csv", recursive=True):
+    n += sum(1 for r in csv.DictReader(open(f)) if "Malloc" in r.get("Function", ""))
+print(f"{sys.argv[2]} render_multi call(s): {n} hipMalloc* calls")
+PY
+    done ;;
   multi)
     timeout -k 10 600 python -u -m pytest tests/test_multi_device.py tests/test_0_multi_process.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/multi.txt 2>&1
     tail -3 $O/multi.txt ;;
