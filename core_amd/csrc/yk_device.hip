@@ -1163,6 +1163,10 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 // them stalled on L1 misses (L1 hit 68 %, L2 hit 65 %, 360-cycle L2 latency),
 // which more resident waves hide better. Crowded-leaf scenes (hair) run the
 // same kernels with 64-ray hand-out chunks (DScene.chunk_max).
+// per-XCD ray segments of the any-hit kernel (A/B builds; 1 = one queue)
+#ifndef YK_SHADOW_SEGS
+#define YK_SHADOW_SEGS 1
+#endif
 #ifndef YK_CLOSEST_WAVES
 #define YK_CLOSEST_WAVES 5
 #endif
@@ -1179,7 +1183,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHAD
 k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false, 1>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+  trace_body<false, YK_SHADOW_SEGS>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 // trees with a leaf of 2^17 references or more (coop_leaves BIG)
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
