@@ -1154,10 +1154,12 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 // rays 2479 (5 waves, round 3) -> 2614 (6 waves) -> 2661 (7 waves) Mrays/s,
 // the centre crop at 64 spp (112 nodes per ray) 2086 -> 2455, headline
 // 2976 -> 3076 (6) -> 3114 (7); 8 waves (18 spills) fell to 1715 on the
-// microbenchmark. Closest-hit stays at 5 waves (88 VGPRs; round 3 measured 6
-// waves with spills at 2657 against 2835) with per-XCD ray segments (+12 %
-// from L2 locality). Earlier: any-hit per-XCD segments 2700 / 2719 (round 2),
-// 2806 / 2800 (round 3); non-temporal ray / result accesses 2775 against
+// microbenchmark. Closest-hit: the attribute asks for at least 5 waves; its
+// diet (80 VGPRs, 6.4 KB LDS per wave) lets it run 6 (round 3 measured a
+// forced 6 with spills at 2657 against 2835), with per-XCD ray segments (+12 %
+// from L2 locality). Any-hit per-XCD segments: 2700 / 2719 (round 2),
+// 2806 / 2800 (round 3), +0.3 % at 7 waves (round 4, YK_SHADOW_SEGS=8: under
+// the 2 % bar); non-temporal ray / result accesses 2775 against
 // 2824; resident grids below the occupancy limit lost 2-4 %. PMC (round 3):
 // the any-hit kernel's texture data path is busy 85 % of its cycles, 58 % of
 // them stalled on L1 misses (L1 hit 68 %, L2 hit 65 %, 360-cycle L2 latency),
