@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <chrono>
 #include <cmath>
@@ -29,6 +30,7 @@
 #include <vector>
 
 #include "../../include/yk_api.h"
+#include "../../include/yk_test_hooks.h"
 #include "photon_map.h"
 #include "scene.h"
 #include "yk_internal.h"
@@ -107,6 +109,7 @@ struct DScene {
   unsigned depth_cap;  // tree depth + 2: node visits of one valid descent and stack entries of a
                        // valid traversal (the watchdog's bounds)
   unsigned chunk_max;  // largest ray hand-out chunk (64 for crowded-leaf scenes, whose rays are costly)
+  unsigned rbits;      // bits of a packet word's right-child field: 28 with empty-child bits (k_pack_nodes), else 30
   int uni;             // universal mode (vTriangle_t getSurface: b0 = 0; IntersectS t > tmin)
 };
 
@@ -512,19 +515,42 @@ __device__ __forceinline__ void ld_packet(const char* base, uint32_t i, uint4& p
   p0 = *reinterpret_cast<const uint4*>(a);
   r = *reinterpret_cast<const uint2*>(a + 16);
 }
-__global__ void k_pack_nodes(const uint2* __restrict__ nodes, uint32_t* __restrict__ pk, unsigned n) {
+// Empty-child bits (trees of fewer than 2^28 nodes): every interior word of a
+// packet carries in bit 30 / 31 whether its left / right child is an empty
+// leaf (word.y == 3: axis 3, no references), so the any-hit descent knows it
+// at the decision, with no load (desc_decide); the right-child field is then
+// bits 2..29 (DScene.rbits = 28). Packets are copies: the node array keeps
+// the plain encoding.
+__device__ __forceinline__ uint32_t empty_bits(const uint2* __restrict__ nodes, uint32_t idx, uint2 w) {
+  if ((w.y & 3u) == 3u) return w.y;
+  const uint32_t el = nodes[idx + 1].y == 3u ? 1u : 0u, er = nodes[w.y >> 2].y == 3u ? 1u : 0u;
+  return w.y | (el << 30) | (er << 31);
+}
+__global__ void k_pack_nodes(const uint2* __restrict__ nodes, uint32_t* __restrict__ pk, unsigned n, int bits) {
   const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint2 w = nodes[i];
   uint2 l = make_uint2(0u, 0u), r = make_uint2(0u, 0u);
+  uint32_t wy = w.y;
   if ((w.y & 3u) != 3u) {
     l = nodes[i + 1];
     r = nodes[w.y >> 2];
+    if (bits) {
+      wy = empty_bits(nodes, i, w);
+      l.y = empty_bits(nodes, i + 1, l);
+      r.y = empty_bits(nodes, w.y >> 2, r);
+    }
   }
   uint32_t* o = pk + (size_t)i * kPkWords;
-  *reinterpret_cast<uint4*>(o) = make_uint4(w.x, w.y, l.x, l.y);
+  *reinterpret_cast<uint4*>(o) = make_uint4(w.x, wy, l.x, l.y);
   *reinterpret_cast<uint2*>(o + 4) = r;
 }
+#ifndef YK_ELIDE
+#define YK_ELIDE 0  // any-hit empty-leaf elision (desc_decide): 1 near, 2 far (loop), 4 far (one skip), 0 off
+#endif
+// flagged stack entry: the pushed far child is an empty leaf (its node field;
+// kMaxNodes keeps every real node's field below it)
+constexpr uint32_t kEmptyFar = 0x3FFFFFFFu;
 
 // Leaf-ordered triangles: a copy of every leaf-list entry's
 // triangle (a, e1, e2 as in S.tris) in leaf-list order, with the primitive id
@@ -546,10 +572,26 @@ __global__ void k_gather_leaf_tris(const float* __restrict__ tris, const uint32_
 // One descent decision at interior node `node` (word nd, axis ax): the near /
 // far choice of kdtree.cc:711-761 plus the push of the far child (exit :=
 // split point). Returns the near child.
+//
+// ELIDE (any-hit, IntersectS kdtree.cc:820-947), with the packet word's
+// empty-child bits:
+//  * near child an empty leaf and the far child pushed: the reference visits
+//    the empty leaf, tests nothing, pops the far child (entry := the split
+//    point just computed, exit := the previous exit) and checks dist <
+//    entry.t at the loop top (:853). The same happens here in registers, with
+//    no push and no pop: the near visit is counted, the entry becomes the
+//    split point, and the far child is returned; fin = dist < entry.t ends
+//    the ray (no occluder) without visiting it.
+//  * far child an empty leaf: pushed with the kEmptyFar node field, which
+//    trav_next pops through (its visit counted, after the same dist test)
+//    instead of starting a descent at it.
+// Node visits and the answer stay the reference's; only where the work
+// happens moves (no wave iteration ends at such a leaf).
+template <bool ELIDE = false>
 __device__ __forceinline__ uint32_t desc_decide(Trav& st, const LaneStack& stk, uint2 nd, uint32_t node,
-                                                uint32_t ax) {
+                                                uint32_t ax, unsigned rbits, unsigned& nnodes) {
   const float split = __uint_as_float(nd.x);
-  const uint32_t right = nd.y >> 2;
+  const uint32_t right = __builtin_amdgcn_ubfe(nd.y, 2u, rbits);
   const bool a0 = ax == 0u, a1 = ax == 1u;
   const float oa = sel3m(st.o, a0, a1), da = sel3m(st.d, a0, a1);
   const float enp = pt_coord(st.en_t, st.en_split, st.en_code, ax, oa, da);
@@ -564,11 +606,32 @@ __device__ __forceinline__ uint32_t desc_decide(Trav& st, const LaneStack& stk, 
   if (push) {
     const uint32_t far_ = left_first ? right : node + 1u;
     const float t = (split - oa) * sel3m(st.inv, a0, a1);
-    stk.push(st.sp, make_uint2(__float_as_uint(st.ex_split), st.ex_w));
-    st.sp++;
-    st.ex_t = t;
-    st.ex_split = split;
-    st.ex_w = (far_ + 1u) | (ax << 30);
+    if (ELIDE) {
+      // bit 30: left child empty, bit 31: right child empty
+      const uint32_t nb = left_first ? 30u : 31u;  // the near child's bit; the far one's is 61 - nb
+      if ((YK_ELIDE & 1) && ((nd.y >> nb) & 1u)) {  // near child an empty leaf: visit it, enter the far child
+        nnodes++;
+        st.en_t = t;
+        st.en_split = split;
+        st.en_code = ax;
+        return far_;
+      }
+      stk.push(st.sp, make_uint2(__float_as_uint(st.ex_split), st.ex_w));
+      st.sp++;
+      st.ex_t = t;
+      st.ex_split = split;
+#if YK_ELIDE & 4  // flag in bit 29 of the node field (nodes < 2^28 whenever the packet bits exist)
+      st.ex_w = (far_ + 1u) | (((nd.y >> (61u - nb)) & 1u) << 29) | (ax << 30);
+#else
+      st.ex_w = (((YK_ELIDE & 2) && ((nd.y >> (61u - nb)) & 1u)) ? kEmptyFar : far_ + 1u) | (ax << 30);
+#endif
+    } else {
+      stk.push(st.sp, make_uint2(__float_as_uint(st.ex_split), st.ex_w));
+      st.sp++;
+      st.ex_t = t;
+      st.ex_split = split;
+      st.ex_w = (far_ + 1u) | (ax << 30);
+    }
   }
   return left_first ? node + 1u : right;
 }
@@ -612,6 +675,9 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
   // ended sit out the body under the exec mask. (A divergent loop exit makes
   // the compiler copy the descent's live-out registers every step, 13 of ~27
   // VALU ops; removing them measured equal: the loop waits on its loads.)
+  constexpr bool kElide = !CLOSEST && YK_ELIDE;
+  // an elision that moves the entry past dist ends the ray (no occluder):
+  // dist < en_t, which no descent otherwise produces (checked on entry)
   bool desc = ax != 3u;
   for (;;) {
     const unsigned long long m = __builtin_amdgcn_ballot_w64(desc);
@@ -619,24 +685,28 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
     if (kFrac && (unsigned)__popcll(m) * kFrac < started) break;
     if (++trips > kDescTrips) break;
     if (!desc) continue;
-    uint32_t nxt = desc_decide(st, stk, nd, node, ax);
-    // the near child's word is in the packet: decide there too (unless it is
-    // a leaf), then load the packet of the node that decision picks
+    uint32_t nxt = desc_decide<kElide>(st, stk, nd, node, ax, S.rbits, nnodes);
+    // the near child's word is in the packet (so is the far child's, which an
+    // elision returns): decide there too (unless it is a leaf), then load the
+    // packet of the node that decision picks
     const bool left = nxt == node + 1u;
     nd = left ? make_uint2(p0.z, p0.w) : p1;
     node = nxt;
-    nnodes++;
+    bool go = !kElide || !(st.dist < st.en_t);
+    if (go) nnodes++;
     ax = nd.y & 3u;
-    if (ax != 3u) {
-      nxt = desc_decide(st, stk, nd, node, ax);
+    if (ax != 3u && go) {
+      nxt = desc_decide<kElide>(st, stk, nd, node, ax, S.rbits, nnodes);
       ld_packet(nbase, nxt, p0, p1);
       nd = make_uint2(p0.x, p0.y);
       node = nxt;
-      nnodes++;
+      go = !kElide || !(st.dist < st.en_t);
+      if (go) nnodes++;
       ax = nd.y & 3u;
     }
-    desc = ax != 3u;
+    desc = ax != 3u && go;
   }
+  if (kElide && st.dist < st.en_t) return false;  // finished inside the descent: not occluded
   if (desc) {  // paused: resumes at this node in the next iteration
     if ((unsigned)st.sp > S.depth_cap) {  // watchdog: a stack no valid traversal reaches
       st.sp = kSpError;
@@ -655,28 +725,66 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
 // After the leaf: the closest-hit stop test, then pop (kdtree.cc:802-812).
 // True when the ray is finished.
 template <bool CLOSEST>
-__device__ __forceinline__ bool trav_next(const DScene& S, Trav& st, const LaneStack& stk) {
+__device__ __forceinline__ bool trav_next(const DScene& S, Trav& st, const LaneStack& stk, unsigned& nnodes) {
   if (CLOSEST && st.Z < st.dist && st.Z <= st.ex_t) return true;
-  st.en_t = st.ex_t;
-  st.en_split = st.ex_split;
-  st.en_code = st.ex_w >> 30;
-  st.node = (int)(st.ex_w & 0x3FFFFFFFu) - 1;
-  if (st.node < 0) return true;
-  // corrupt state (never index out of the tree or the stack area): a node
-  // outside the tree, or a stack outside [1, depth_cap] -- a valid traversal
-  // holds at most depth_cap entries, and the overflow area has room for one
-  // more descent's pushes than that
-  if ((unsigned)st.node >= S.nnodes || (unsigned)(st.sp - 1) >= S.depth_cap) {
-    st.sp = kSpError;
-    return true;
+#if YK_ELIDE & 4
+  // flagged empty far leaf (bit 29 of the node field): at most one skipped
+  // per call (a second flagged entry is entered as an ordinary node)
+  constexpr int kSkips = CLOSEST ? 1 : 2;
+#pragma unroll
+  for (int k = 0; k < kSkips; ++k) {
+    st.en_t = st.ex_t;
+    st.en_split = st.ex_split;
+    st.en_code = st.ex_w >> 30;
+    const uint32_t field = st.ex_w & 0x3FFFFFFFu;
+    const bool flagged = !CLOSEST && S.rbits == 28u && (field & 0x20000000u);
+    st.node = (int)(field & (flagged ? 0x1FFFFFFFu : 0x3FFFFFFFu)) - 1;
+    if (st.node < 0) return true;
+    if ((unsigned)st.node >= S.nnodes || (unsigned)(st.sp - 1) >= S.depth_cap) {
+      st.sp = kSpError;
+      return true;
+    }
+    st.sp--;
+    const uint2 e = stk.pop(st.sp);
+    st.ex_split = __uint_as_float(e.x);
+    st.ex_w = e.y;
+    const uint32_t code = e.y >> 30;
+    st.ex_t = (code == 3u) ? st.ex_split : (st.ex_split - sel3(st.o, code)) * sel3(st.inv, code);
+    if (!flagged || k == kSkips - 1) return false;
+    if (st.dist < st.en_t) return true;
+    nnodes++;
   }
-  st.sp--;
-  const uint2 e = stk.pop(st.sp);
-  st.ex_split = __uint_as_float(e.x);
-  st.ex_w = e.y;
-  const uint32_t code = e.y >> 30;
-  st.ex_t = (code == 3u) ? st.ex_split : (st.ex_split - sel3(st.o, code)) * sel3(st.inv, code);
   return false;
+#else
+  for (;;) {
+    st.en_t = st.ex_t;
+    st.en_split = st.ex_split;
+    st.en_code = st.ex_w >> 30;
+    const uint32_t field = st.ex_w & 0x3FFFFFFFu;
+    st.node = (int)field - 1;
+    if (st.node < 0) return true;
+    const bool empty_far = !CLOSEST && (YK_ELIDE & 2) && field == kEmptyFar;
+    // corrupt state (never index out of the tree or the stack area): a node
+    // outside the tree, or a stack outside [1, depth_cap] -- a valid traversal
+    // holds at most depth_cap entries, and the overflow area has room for one
+    // more descent's pushes than that
+    if (((unsigned)st.node >= S.nnodes && !empty_far) || (unsigned)(st.sp - 1) >= S.depth_cap) {
+      st.sp = kSpError;
+      return true;
+    }
+    st.sp--;
+    const uint2 e = stk.pop(st.sp);
+    st.ex_split = __uint_as_float(e.x);
+    st.ex_w = e.y;
+    const uint32_t code = e.y >> 30;
+    st.ex_t = (code == 3u) ? st.ex_split : (st.ex_split - sel3(st.o, code)) * sel3(st.inv, code);
+    if (!empty_far) return false;
+    // an empty far leaf (desc_decide): the reference's loop top tests dist
+    // against its entry (kdtree.cc:853), then visits it and pops again
+    if (st.dist < st.en_t) return true;
+    nnodes++;
+  }
+#endif
 }
 
 // total-order key of a float (for t >= 0 the raw bits; -0 is made +0 first so
@@ -1018,7 +1126,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       bool fin = false;  // any-hit: a result to stage
       int fin_rid = 0;
       if (act) {
-        bool done = !live || occ || (!paused && trav_next<CLOSEST>(S, st, stk));
+        bool done = !live || occ || (!paused && trav_next<CLOSEST>(S, st, stk, nnodes));
         if (runaway) {
           st.sp = kSpError;
           done = true;
@@ -2994,6 +3102,7 @@ struct yk_device {
   bool uploaded = false;
   const yk_scene* uploaded_scene = nullptr;  // the scene the resident arrays came from
   uint64_t uploaded_gen = 0;                 // its Scene::generation at upload
+  uint64_t const_token = 0;                  // unique per yk_device_upload (bind_constants)
   size_t nleaf = 0;                          // leaf-list entries of the resident tree
   // scene
   DBuf<float> tris;  // triangle records (kTriWords floats per prim)
@@ -3065,21 +3174,38 @@ struct yk_device {
 
 namespace {
 // Constant memory (c_mats, c_lights, c_cam) is per GPU, not per handle: the
-// scene generation whose records a GPU's constants hold. A handle whose scene
-// differs re-binds them before it launches (bind_constants).
+// upload whose records a GPU's constants hold. Every yk_device_upload takes a
+// fresh process-wide token (the scene's generation alone is not enough: the
+// camera can change on a built scene, yk_scene_set_camera, and a re-upload
+// must then reach c_cam). A handle whose token differs re-binds them before
+// it launches (bind_constants).
 std::mutex g_const_mu;
-uint64_t g_const_gen[64] = {};
+uint64_t g_const_token[64] = {};
+std::atomic<uint64_t> g_upload_token{1};
 
 void bind_constants(yk_device* d) {
   std::lock_guard<std::mutex> lk(g_const_mu);
   const int o = d->ordinal & 63;
-  if (g_const_gen[o] == d->uploaded_gen) return;
+  if (g_const_token[o] == d->const_token) return;
   if (!d->mats_host.empty())
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_mats), d->mats_host.data(), d->mats_host.size() * sizeof(DMat)));
   if (!d->lights_host.empty())
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_lights), d->lights_host.data(), d->lights_host.size() * sizeof(DLight)));
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_cam), &d->cam_host, sizeof(DCam)));
-  g_const_gen[o] = d->uploaded_gen;
+  g_const_token[o] = d->const_token;
+}
+
+// two handles render one frame only if their constant records are the same
+// (same scene generation is checked separately; this catches a camera, light
+// or material changed between the two uploads)
+bool same_constants(const yk_device* a, const yk_device* b) {
+  return a->mats_host.size() == b->mats_host.size() && a->lights_host.size() == b->lights_host.size() &&
+         std::memcmp(&a->cam_host, &b->cam_host, sizeof(DCam)) == 0 &&
+         (a->mats_host.empty() ||
+          std::memcmp(a->mats_host.data(), b->mats_host.data(), a->mats_host.size() * sizeof(DMat)) == 0) &&
+         (a->lights_host.empty() ||
+          std::memcmp(a->lights_host.data(), b->lights_host.data(), a->lights_host.size() * sizeof(DLight)) == 0) &&
+         a->has_bg == b->has_bg && std::memcmp(a->bg, b->bg, sizeof a->bg) == 0;
 }
 }  // namespace
 
@@ -3493,6 +3619,17 @@ void set_handout(yk_device* d, size_t nn) {
   d->S.chunk_max = d->crowded_leaves ? 64u : (unsigned)YK_POOL_CHUNK_MAX;
 }
 
+// Node packets of the resident tree (k_pack_nodes); with fewer than 2^28
+// nodes every interior word carries its empty-child bits (rbits 28).
+void pack_nodes(yk_device* d, size_t nn) {
+  const bool bits = nn < (1u << 28);
+  d->S.rbits = bits ? 28u : 30u;
+  hipLaunchKernelGGL(k_pack_nodes, dim3(grid_for((long long)nn)), dim3(256), 0, d->stream, d->nodes.p, d->pk.p,
+                     (unsigned)nn, bits ? 1 : 0);
+  HIPCHK(hipGetLastError());
+  d->S.pk = d->pk.p;
+}
+
 // Traversal copies of the resident tree: the leaf-ordered triangles
 // (k_gather_leaf_tris) and the node packets (k_pack_nodes).
 // Callers check the node count (kMaxNodes) before they touch any resident
@@ -3508,10 +3645,7 @@ void install_traversal(yk_device* d, size_t nn, size_t nleaf, uint32_t max_leaf_
   }
   d->S.ltris = nleaf ? d->ltris.p : nullptr;
   d->pk.ensure(kPkWords * nn);
-  hipLaunchKernelGGL(k_pack_nodes, dim3(grid_for((long long)nn)), dim3(256), 0, d->stream, d->nodes.p, d->pk.p,
-                     (unsigned)nn);
-  HIPCHK(hipGetLastError());
-  d->S.pk = d->pk.p;
+  pack_nodes(d, nn);
   HIPCHK(hipStreamSynchronize(d->stream));
 }
 
@@ -3710,6 +3844,7 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   d->uploaded = true;
   d->uploaded_scene = s;
   d->uploaded_gen = S.generation;
+  d->const_token = g_upload_token.fetch_add(1);
   bind_constants(d);  // materials, lights and camera into the GPU's constant memory
   return YK_OK;
   YK_GUARD_END
@@ -3775,12 +3910,11 @@ int yk_trace_shadow_filtered(yk_device* d, const yk_ray* d_rays, int64_t n, uint
 // build's compiled forms: Gauss folds -6*log2(e) into one constant and drops
 // fExp2's upper clamp (the argument is never positive); Lanczos2 uses the
 // FAST_TRIG fSin (yk::host_fsin) on (float)(x*pi) and (float)(x*pi/2).
-static float filter_gauss(float dx, float dy) {
-  const float r2 = dx * dx + dy * dy;
-  float k;
-  const uint32_t kbits = 0xc10a7facu;  // (float)(-6 * (float)M_LOG2E)
-  std::memcpy(&k, &kbits, 4);
-  float x = r2 * k;
+// fExp2, mathOptimizations.h:100-114 (POLYEXP :85); pinned bit for bit to
+// the reference's own fExp2 compiled in the build container
+// (oracle/ref_check.cc, tests/test_ref_pinning.py through yk_debug_qmc_probe)
+static float host_fexp2(float x) {
+  x = (x < 129.00000f) ? x : 129.00000f;    // f_HI
   x = (x > -126.99999f) ? x : -126.99999f;  // f_LOW
   const int ip = (int)(x - 0.5f);
   const float fp = x - (float)ip;
@@ -3789,7 +3923,15 @@ static float filter_gauss(float dx, float dy) {
   std::memcpy(&e, &eb, 4);
   const float poly = ((((1.8775767e-3f * fp + 8.9893397e-3f) * fp + 5.5826318e-2f) * fp + 2.4015361e-1f) * fp +
                       6.9315308e-1f) * fp + 9.9999994e-1f;
-  const float v = (float)((double)(e * poly) - 0.00247875);
+  return e * poly;
+}
+static float filter_gauss(float dx, float dy) {
+  const float r2 = dx * dx + dy * dy;
+  float k;
+  const uint32_t kbits = 0xc10a7facu;  // (float)(-6 * (float)M_LOG2E)
+  std::memcpy(&k, &kbits, 4);
+  // r2 * k <= 0: the upper clamp the compiled form drops is a no-op
+  const float v = (float)((double)host_fexp2(r2 * k) - 0.00247875);
   return (v > 0.f) ? v : 0.f;
 }
 static float filter_lanczos(float dx, float dy) {
@@ -3866,6 +4008,7 @@ int yk_film_filter_from_table(const float* table, float filterw, yk_render_param
 
 #include "yk_photon_host.inc"
 #include "yk_kdtree_gpu.inc"
+#include "yk_test_hooks.inc"
 
 // One renderPass (integrator.cc:172-224): n samples per pixel from pixel
 // sample `off`; flags (film-local bytes, host) restricts it to the pixels
@@ -4449,7 +4592,7 @@ int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params
     // one frame = one scene: the same uploaded scene generation everywhere
     // (handles on one GPU share its constant memory, and shards of different
     // scenes would be summed into one film)
-    if (devs[i]->uploaded_gen != devs[0]->uploaded_gen)
+    if (devs[i]->uploaded_gen != devs[0]->uploaded_gen || !same_constants(devs[i], devs[0]))
       return set_error(YK_ERR_STATE, "yk_render_multi: the devices hold different scenes (upload the same scene to all)");
     const bool maps = p->integrator == YK_INTEGRATOR_PHOTON ||
                       (p->integrator == YK_INTEGRATOR_PATH &&
@@ -4485,10 +4628,17 @@ int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params
   d0->macc.ensure(nfl);
   FilmShards FS{};
   FS.n = ndev;
+  // YK_MULTI_STAGE_ALL=1 (test only): shards on d0's own GPU also take the
+  // peer path (staging film, copy stream, event), so one-GPU boxes run it
+  const bool stage_all = [] {
+    const char* e = std::getenv("YK_MULTI_STAGE_ALL");
+    return e && e[0] == '1';
+  }();
+  auto staged = [&](int i) { return i > 0 && (devs[i]->ordinal != d0->ordinal || stage_all); };
   for (int i = 0; i < ndev; ++i) {
     // a shard on d0's own GPU is read in place; a peer GPU's film is copied
     // into a staging film first, on a copy stream of its own
-    if (devs[i]->ordinal == d0->ordinal) {
+    if (!staged(i)) {
       FS.f[i] = devs[i]->mfilm.p;
       continue;
     }
@@ -4525,7 +4675,7 @@ int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params
     HIPCHK(hipSetDevice(d0->ordinal));
     hipStream_t s0 = d0->stream;
     for (int i = 1; i < ndev; ++i) {
-      if (devs[i]->ordinal == d0->ordinal) continue;
+      if (!staged(i)) continue;
       HIPCHK(hipMemcpyPeerAsync(d0->mstage[i].p, d0->ordinal, devs[i]->mfilm.p, devs[i]->ordinal, nfl * sizeof(float),
                                 d0->mstream[i]));
       HIPCHK(hipEventRecord(d0->mevent[i], d0->mstream[i]));

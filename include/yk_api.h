@@ -391,7 +391,11 @@ int yk_render_film(yk_device* d, const yk_render_params* p, int32_t shard, int32
  * time. Handles opened on one GPU share its constant memory (materials,
  * lights, camera): a handle re-binds it from its own upload before it
  * renders, so handles on one GPU that hold different scenes must not render
- * at the same time. */
+ * at the same time. "Same uploaded scene" means the same built scene and the
+ * same camera, lights and materials at upload time (a camera changed between
+ * two handles' uploads is refused). At most 16 handles (YK_ERR_UNSUPPORTED).
+ * Memory: devs[0] keeps one staging film per peer-GPU shard and the sum film
+ * (width*height*5 floats each) until yk_device_close. */
 int yk_render_multi(yk_device* const* devs, int32_t ndev, const yk_render_params* p, float* film_host,
                     yk_stats* st);
 /* convenience: whole frame on one device, RGBA float image to host memory */
@@ -447,15 +451,8 @@ int yk_device_build_tree(yk_device* d, const yk_scene* s, int32_t flags, yk_tree
  * aim rays at the split planes of the tree actually traversed. */
 int yk_device_export_tree(yk_device* d, uint32_t* nodes, int64_t node_cap, uint32_t* leaf, int64_t leaf_cap,
                           int64_t* nnodes_out, int64_t* nleaf_out);
-/* Test hook for the traversal watchdog: overwrites node `index` of the
- * device's resident kd-tree with the export-encoding words (w0, w1), as a
- * memory fault would, past the structural check yk_device_upload applies.
- * Child and leaf ranges must still lie inside the tree (YK_ERR_ARG
- * otherwise), so the damage is structural (a cycle, a shared subtree, a
- * deeper descent); ray queries and renders on the damaged tree must then
- * return YK_ERR_INTERNAL within seconds, never hang or fault. A fresh
- * yk_device_upload restores the device. */
-int yk_device_debug_set_node(yk_device* d, int64_t index, uint32_t w0, uint32_t w1);
+/* Test-only hooks (the watchdog's tree damage) are declared in
+ * yk_test_hooks.h, not here, and are disabled unless YK_DEBUG_HOOKS=1. */
 
 #ifdef __cplusplus
 }

@@ -28,6 +28,7 @@
  * that builder reproduces the reference's recorded tree statistics exactly.
  */
 #include <math.h>
+#include <xmmintrin.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -2202,17 +2203,24 @@ static rgba pm_integrate(rstate* st, const yk_render_params* P, v3 from, v3 dir,
 static float f_box(float dx, float dy) { (void)dx; (void)dy; return 1.f; }
 /* Gauss, imagefilm.cc:97-101: compiled form folds -6*log2(e) into one
  * constant (bits 0xc10a7fac) and drops fExp2's upper clamp */
-static float f_gauss(float dx, float dy) {
-  float r2 = dx * dx + dy * dy;
-  union { uint32_t u; float f; } k = {0xc10a7facu}, e;
-  float x = r2 * k.f;
+/* fExp2, mathOptimizations.h:100-114 (POLYEXP :85). Pinned bit for bit to
+ * the reference's own fExp2 compiled here (oracle/ref_check.cc). */
+static float fExp2(float x) {
+  union { uint32_t u; float f; } e;
+  x = (x < 129.00000f) ? x : 129.00000f;
   x = (x > -126.99999f) ? x : -126.99999f;
   int ip = (int)(x - 0.5f);
   float fp = x - (float)ip;
   e.u = (uint32_t)(ip + 127) << 23;
   float poly = ((((1.8775767e-3f * fp + 8.9893397e-3f) * fp + 5.5826318e-2f) * fp + 2.4015361e-1f) * fp +
                 6.9315308e-1f) * fp + 9.9999994e-1f;
-  float v = (float)((double)(e.f * poly) - 0.00247875);
+  return e.f * poly;
+}
+static float f_gauss(float dx, float dy) {
+  float r2 = dx * dx + dy * dy;
+  union { uint32_t u; float f; } k = {0xc10a7facu};
+  /* x <= 0, so the dropped upper clamp is a no-op */
+  float v = (float)((double)fExp2(r2 * k.f) - 0.00247875);
   return (v > 0.f) ? v : 0.f;
 }
 /* Lanczos2, imagefilm.cc:104-119 */
@@ -2596,6 +2604,20 @@ float orc_ri_s(unsigned i, unsigned r) { return RI_S(i, r); }
 float orc_ri_lp(unsigned i, unsigned r) { return RI_LP(i, r); }
 unsigned orc_fnv(unsigned v) { return fnv_32a_buf(v); }
 float orc_fsin(float x) { return fSin(x); }
+float orc_fcos(float x) { return fCos(x); }
+/* The reference's process computes with MXCSR FTZ+DAZ set (crtfastmath's
+ * constructor in every object GCC 11 links with -ffast-math). The oracle
+ * keeps IEEE denormals, like the GPU; tests switch the calling thread to the
+ * reference's environment with this to show that a difference is only the
+ * flush (tests/test_ref_pinning.py). Returns the previous state. */
+int orc_set_ftz(int on) {
+  unsigned c = _mm_getcsr();
+  _mm_setcsr(on ? (c | 0x8040u) : (c & ~0x8040u));
+  return (c & 0x8040u) ? 1 : 0;
+}
+float orc_fexp2(float x) { return fExp2(x); }
+int orc_round2int(double v) { return Round2Int(v); }
+int orc_floor2int(double v) { return Floor2Int(v); }
 void orc_halton_seq(int base, unsigned start, int n, float* out) {
   halton h;
   hal_init(&h, base);

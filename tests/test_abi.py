@@ -12,8 +12,8 @@ from core_amd.scene import Scene, probe_scene
 from tests.conftest import ROOT
 
 
-def declared_functions():
-    src = open(os.path.join(ROOT, "include", "yk_api.h")).read()
+def declared_functions(header="yk_api.h"):
+    src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(yk_[a-z0-9_]+)\s*\(", src)))
 
@@ -25,7 +25,20 @@ def test_every_declared_symbol_is_exported_and_bound():
     for n in names:
         assert hasattr(raw, n), f"libyk.so does not export {n}"
         assert n in A.SIGNATURES, f"_abi.SIGNATURES lacks {n}"
-    assert set(A.SIGNATURES) <= set(names)
+    hooks = declared_functions("yk_test_hooks.h")
+    assert hooks == ["yk_debug_qmc_probe", "yk_device_debug_set_node"] and not set(hooks) & set(names)
+    for n in hooks:
+        assert hasattr(raw, n) and n in A.SIGNATURES
+    assert set(A.SIGNATURES) <= set(names) | set(hooks)
+
+
+def test_debug_hook_disabled_without_env(monkeypatch):
+    """the watchdog's tree-damage hook is not in the
+    product header and refuses to run unless YK_DEBUG_HOOKS=1."""
+    monkeypatch.delenv("YK_DEBUG_HOOKS", raising=False)
+    rc = A.lib().yk_device_debug_set_node(None, 0, 0, 0)
+    assert rc == A.YK_ERR_UNSUPPORTED
+    assert b"YK_DEBUG_HOOKS" in A.lib().yk_last_error()
 
 
 def test_struct_sizes_match_header_layout():

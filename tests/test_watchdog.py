@@ -22,6 +22,13 @@ from core_amd.scene import probe_scene
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _hooks_on(monkeypatch):
+    """the damage hook is test-only and off unless YK_DEBUG_HOOKS=1
+    (include/yk_test_hooks.h)"""
+    monkeypatch.setenv("YK_DEBUG_HOOKS", "1")
+
+
 def _setup(gpu_device):
     s, p = probe_scene("bumpy", 64, 48, 200, 101)
     gpu_device.upload(s)
