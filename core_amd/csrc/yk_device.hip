@@ -109,7 +109,6 @@ struct DScene {
   unsigned depth_cap;  // tree depth + 2: node visits of one valid descent and stack entries of a
                        // valid traversal (the watchdog's bounds)
   unsigned chunk_max;  // largest ray hand-out chunk (64 for crowded-leaf scenes, whose rays are costly)
-  unsigned rbits;      // bits of a packet word's right-child field: 28 with empty-child bits (k_pack_nodes), else 30
   int uni;             // universal mode (vTriangle_t getSurface: b0 = 0; IntersectS t > tmin)
 };
 
@@ -514,43 +513,25 @@ __device__ __forceinline__ void ld_packet(const char* base, uint32_t i, uint4& p
   const char* a = base + (size_t)i * (4 * kPkWords);
   p0 = *reinterpret_cast<const uint4*>(a);
   r = *reinterpret_cast<const uint2*>(a + 16);
+#ifdef YK_XLOAD  // experiment: one more load instruction per packet (cost of a lane-load)
+  uint32_t x;
+  asm volatile("global_load_dword %0, %1, off offset:4\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(a) : "memory");
+  asm volatile("" ::"v"(x));
+#endif
 }
-// Empty-child bits (trees of fewer than 2^28 nodes): every interior word of a
-// packet carries in bit 30 / 31 whether its left / right child is an empty
-// leaf (word.y == 3: axis 3, no references), so the any-hit descent knows it
-// at the decision, with no load (desc_decide); the right-child field is then
-// bits 2..29 (DScene.rbits = 28). Packets are copies: the node array keeps
-// the plain encoding.
-__device__ __forceinline__ uint32_t empty_bits(const uint2* __restrict__ nodes, uint32_t idx, uint2 w) {
-  if ((w.y & 3u) == 3u) return w.y;
-  const uint32_t el = nodes[idx + 1].y == 3u ? 1u : 0u, er = nodes[w.y >> 2].y == 3u ? 1u : 0u;
-  return w.y | (el << 30) | (er << 31);
-}
-__global__ void k_pack_nodes(const uint2* __restrict__ nodes, uint32_t* __restrict__ pk, unsigned n, int bits) {
+__global__ void k_pack_nodes(const uint2* __restrict__ nodes, uint32_t* __restrict__ pk, unsigned n) {
   const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint2 w = nodes[i];
   uint2 l = make_uint2(0u, 0u), r = make_uint2(0u, 0u);
-  uint32_t wy = w.y;
   if ((w.y & 3u) != 3u) {
     l = nodes[i + 1];
     r = nodes[w.y >> 2];
-    if (bits) {
-      wy = empty_bits(nodes, i, w);
-      l.y = empty_bits(nodes, i + 1, l);
-      r.y = empty_bits(nodes, w.y >> 2, r);
-    }
   }
   uint32_t* o = pk + (size_t)i * kPkWords;
-  *reinterpret_cast<uint4*>(o) = make_uint4(w.x, wy, l.x, l.y);
+  *reinterpret_cast<uint4*>(o) = make_uint4(w.x, w.y, l.x, l.y);
   *reinterpret_cast<uint2*>(o + 4) = r;
 }
-#ifndef YK_ELIDE
-#define YK_ELIDE 0  // any-hit empty-leaf elision (desc_decide): 1 near, 2 far (loop), 4 far (one skip), 0 off
-#endif
-// flagged stack entry: the pushed far child is an empty leaf (its node field;
-// kMaxNodes keeps every real node's field below it)
-constexpr uint32_t kEmptyFar = 0x3FFFFFFFu;
 
 // Leaf-ordered triangles: a copy of every leaf-list entry's
 // triangle (a, e1, e2 as in S.tris) in leaf-list order, with the primitive id
@@ -572,26 +553,13 @@ __global__ void k_gather_leaf_tris(const float* __restrict__ tris, const uint32_
 // One descent decision at interior node `node` (word nd, axis ax): the near /
 // far choice of kdtree.cc:711-761 plus the push of the far child (exit :=
 // split point). Returns the near child.
-//
-// ELIDE (any-hit, IntersectS kdtree.cc:820-947), with the packet word's
-// empty-child bits:
-//  * near child an empty leaf and the far child pushed: the reference visits
-//    the empty leaf, tests nothing, pops the far child (entry := the split
-//    point just computed, exit := the previous exit) and checks dist <
-//    entry.t at the loop top (:853). The same happens here in registers, with
-//    no push and no pop: the near visit is counted, the entry becomes the
-//    split point, and the far child is returned; fin = dist < entry.t ends
-//    the ray (no occluder) without visiting it.
-//  * far child an empty leaf: pushed with the kEmptyFar node field, which
-//    trav_next pops through (its visit counted, after the same dist test)
-//    instead of starting a descent at it.
-// Node visits and the answer stay the reference's; only where the work
-// happens moves (no wave iteration ends at such a leaf).
-template <bool ELIDE = false>
+// (Round 5: empty-leaf elision here -- a near child that is an empty leaf
+// entered past in registers, a far one pushed flagged and popped through --
+// was parity-green and lost: DESIGN.md §5.)
 __device__ __forceinline__ uint32_t desc_decide(Trav& st, const LaneStack& stk, uint2 nd, uint32_t node,
-                                                uint32_t ax, unsigned rbits, unsigned& nnodes) {
+                                                uint32_t ax) {
   const float split = __uint_as_float(nd.x);
-  const uint32_t right = __builtin_amdgcn_ubfe(nd.y, 2u, rbits);
+  const uint32_t right = nd.y >> 2;
   const bool a0 = ax == 0u, a1 = ax == 1u;
   const float oa = sel3m(st.o, a0, a1), da = sel3m(st.d, a0, a1);
   const float enp = pt_coord(st.en_t, st.en_split, st.en_code, ax, oa, da);
@@ -606,32 +574,11 @@ __device__ __forceinline__ uint32_t desc_decide(Trav& st, const LaneStack& stk, 
   if (push) {
     const uint32_t far_ = left_first ? right : node + 1u;
     const float t = (split - oa) * sel3m(st.inv, a0, a1);
-    if (ELIDE) {
-      // bit 30: left child empty, bit 31: right child empty
-      const uint32_t nb = left_first ? 30u : 31u;  // the near child's bit; the far one's is 61 - nb
-      if ((YK_ELIDE & 1) && ((nd.y >> nb) & 1u)) {  // near child an empty leaf: visit it, enter the far child
-        nnodes++;
-        st.en_t = t;
-        st.en_split = split;
-        st.en_code = ax;
-        return far_;
-      }
-      stk.push(st.sp, make_uint2(__float_as_uint(st.ex_split), st.ex_w));
-      st.sp++;
-      st.ex_t = t;
-      st.ex_split = split;
-#if YK_ELIDE & 4  // flag in bit 29 of the node field (nodes < 2^28 whenever the packet bits exist)
-      st.ex_w = (far_ + 1u) | (((nd.y >> (61u - nb)) & 1u) << 29) | (ax << 30);
-#else
-      st.ex_w = (((YK_ELIDE & 2) && ((nd.y >> (61u - nb)) & 1u)) ? kEmptyFar : far_ + 1u) | (ax << 30);
-#endif
-    } else {
-      stk.push(st.sp, make_uint2(__float_as_uint(st.ex_split), st.ex_w));
-      st.sp++;
-      st.ex_t = t;
-      st.ex_split = split;
-      st.ex_w = (far_ + 1u) | (ax << 30);
-    }
+    stk.push(st.sp, make_uint2(__float_as_uint(st.ex_split), st.ex_w));
+    st.sp++;
+    st.ex_t = t;
+    st.ex_split = split;
+    st.ex_w = (far_ + 1u) | (ax << 30);
   }
   return left_first ? node + 1u : right;
 }
@@ -657,7 +604,7 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
 #define YK_DESC_FRAC 4  // measured 2 / 3 / 4 / 8: 2477 / 2524 / 2527 / 2450 Mrays/s (off: 2344)
 #endif
 #ifndef YK_DESC_FRAC_S
-#define YK_DESC_FRAC_S YK_DESC_FRAC  // any-hit kernel
+#define YK_DESC_FRAC_S 3  // any-hit kernel (round 4: 1/3 vs 1/4, +0.4-0.8 % with the combined defaults)
 #endif
   constexpr unsigned kFrac = CLOSEST ? YK_DESC_FRAC : YK_DESC_FRAC_S;
   // descent pause (YK_DESC_FRAC = f > 0): once fewer than 1/f of the lanes
@@ -675,9 +622,6 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
   // ended sit out the body under the exec mask. (A divergent loop exit makes
   // the compiler copy the descent's live-out registers every step, 13 of ~27
   // VALU ops; removing them measured equal: the loop waits on its loads.)
-  constexpr bool kElide = !CLOSEST && YK_ELIDE;
-  // an elision that moves the entry past dist ends the ray (no occluder):
-  // dist < en_t, which no descent otherwise produces (checked on entry)
   bool desc = ax != 3u;
   for (;;) {
     const unsigned long long m = __builtin_amdgcn_ballot_w64(desc);
@@ -685,28 +629,24 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
     if (kFrac && (unsigned)__popcll(m) * kFrac < started) break;
     if (++trips > kDescTrips) break;
     if (!desc) continue;
-    uint32_t nxt = desc_decide<kElide>(st, stk, nd, node, ax, S.rbits, nnodes);
-    // the near child's word is in the packet (so is the far child's, which an
-    // elision returns): decide there too (unless it is a leaf), then load the
-    // packet of the node that decision picks
+    uint32_t nxt = desc_decide(st, stk, nd, node, ax);
+    // the near child's word is in the packet: decide there too (unless it is
+    // a leaf), then load the packet of the node that decision picks
     const bool left = nxt == node + 1u;
     nd = left ? make_uint2(p0.z, p0.w) : p1;
     node = nxt;
-    bool go = !kElide || !(st.dist < st.en_t);
-    if (go) nnodes++;
+    nnodes++;
     ax = nd.y & 3u;
-    if (ax != 3u && go) {
-      nxt = desc_decide<kElide>(st, stk, nd, node, ax, S.rbits, nnodes);
+    if (ax != 3u) {
+      nxt = desc_decide(st, stk, nd, node, ax);
       ld_packet(nbase, nxt, p0, p1);
       nd = make_uint2(p0.x, p0.y);
       node = nxt;
-      go = !kElide || !(st.dist < st.en_t);
-      if (go) nnodes++;
+      nnodes++;
       ax = nd.y & 3u;
     }
-    desc = ax != 3u && go;
+    desc = ax != 3u;
   }
-  if (kElide && st.dist < st.en_t) return false;  // finished inside the descent: not occluded
   if (desc) {  // paused: resumes at this node in the next iteration
     if ((unsigned)st.sp > S.depth_cap) {  // watchdog: a stack no valid traversal reaches
       st.sp = kSpError;
@@ -725,66 +665,28 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
 // After the leaf: the closest-hit stop test, then pop (kdtree.cc:802-812).
 // True when the ray is finished.
 template <bool CLOSEST>
-__device__ __forceinline__ bool trav_next(const DScene& S, Trav& st, const LaneStack& stk, unsigned& nnodes) {
+__device__ __forceinline__ bool trav_next(const DScene& S, Trav& st, const LaneStack& stk) {
   if (CLOSEST && st.Z < st.dist && st.Z <= st.ex_t) return true;
-#if YK_ELIDE & 4
-  // flagged empty far leaf (bit 29 of the node field): at most one skipped
-  // per call (a second flagged entry is entered as an ordinary node)
-  constexpr int kSkips = CLOSEST ? 1 : 2;
-#pragma unroll
-  for (int k = 0; k < kSkips; ++k) {
-    st.en_t = st.ex_t;
-    st.en_split = st.ex_split;
-    st.en_code = st.ex_w >> 30;
-    const uint32_t field = st.ex_w & 0x3FFFFFFFu;
-    const bool flagged = !CLOSEST && S.rbits == 28u && (field & 0x20000000u);
-    st.node = (int)(field & (flagged ? 0x1FFFFFFFu : 0x3FFFFFFFu)) - 1;
-    if (st.node < 0) return true;
-    if ((unsigned)st.node >= S.nnodes || (unsigned)(st.sp - 1) >= S.depth_cap) {
-      st.sp = kSpError;
-      return true;
-    }
-    st.sp--;
-    const uint2 e = stk.pop(st.sp);
-    st.ex_split = __uint_as_float(e.x);
-    st.ex_w = e.y;
-    const uint32_t code = e.y >> 30;
-    st.ex_t = (code == 3u) ? st.ex_split : (st.ex_split - sel3(st.o, code)) * sel3(st.inv, code);
-    if (!flagged || k == kSkips - 1) return false;
-    if (st.dist < st.en_t) return true;
-    nnodes++;
+  st.en_t = st.ex_t;
+  st.en_split = st.ex_split;
+  st.en_code = st.ex_w >> 30;
+  st.node = (int)(st.ex_w & 0x3FFFFFFFu) - 1;
+  if (st.node < 0) return true;
+  // corrupt state (never index out of the tree or the stack area): a node
+  // outside the tree, or a stack outside [1, depth_cap] -- a valid traversal
+  // holds at most depth_cap entries, and the overflow area has room for one
+  // more descent's pushes than that
+  if ((unsigned)st.node >= S.nnodes || (unsigned)(st.sp - 1) >= S.depth_cap) {
+    st.sp = kSpError;
+    return true;
   }
+  st.sp--;
+  const uint2 e = stk.pop(st.sp);
+  st.ex_split = __uint_as_float(e.x);
+  st.ex_w = e.y;
+  const uint32_t code = e.y >> 30;
+  st.ex_t = (code == 3u) ? st.ex_split : (st.ex_split - sel3(st.o, code)) * sel3(st.inv, code);
   return false;
-#else
-  for (;;) {
-    st.en_t = st.ex_t;
-    st.en_split = st.ex_split;
-    st.en_code = st.ex_w >> 30;
-    const uint32_t field = st.ex_w & 0x3FFFFFFFu;
-    st.node = (int)field - 1;
-    if (st.node < 0) return true;
-    const bool empty_far = !CLOSEST && (YK_ELIDE & 2) && field == kEmptyFar;
-    // corrupt state (never index out of the tree or the stack area): a node
-    // outside the tree, or a stack outside [1, depth_cap] -- a valid traversal
-    // holds at most depth_cap entries, and the overflow area has room for one
-    // more descent's pushes than that
-    if (((unsigned)st.node >= S.nnodes && !empty_far) || (unsigned)(st.sp - 1) >= S.depth_cap) {
-      st.sp = kSpError;
-      return true;
-    }
-    st.sp--;
-    const uint2 e = stk.pop(st.sp);
-    st.ex_split = __uint_as_float(e.x);
-    st.ex_w = e.y;
-    const uint32_t code = e.y >> 30;
-    st.ex_t = (code == 3u) ? st.ex_split : (st.ex_split - sel3(st.o, code)) * sel3(st.inv, code);
-    if (!empty_far) return false;
-    // an empty far leaf (desc_decide): the reference's loop top tests dist
-    // against its entry (kdtree.cc:853), then visits it and pops again
-    if (st.dist < st.en_t) return true;
-    nnodes++;
-  }
-#endif
 }
 
 // total-order key of a float (for t >= 0 the raw bits; -0 is made +0 first so
@@ -1126,7 +1028,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       bool fin = false;  // any-hit: a result to stage
       int fin_rid = 0;
       if (act) {
-        bool done = !live || occ || (!paused && trav_next<CLOSEST>(S, st, stk, nnodes));
+        bool done = !live || occ || (!paused && trav_next<CLOSEST>(S, st, stk));
         if (runaway) {
           st.sp = kSpError;
           done = true;
@@ -1275,7 +1177,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 // same kernels with 64-ray hand-out chunks (DScene.chunk_max).
 // per-XCD ray segments of the any-hit kernel (A/B builds; 1 = one queue)
 #ifndef YK_SHADOW_SEGS
-#define YK_SHADOW_SEGS 1
+#define YK_SHADOW_SEGS 8
 #endif
 #ifndef YK_CLOSEST_WAVES
 #define YK_CLOSEST_WAVES 5
@@ -1673,16 +1575,15 @@ __device__ __forceinline__ bool dirac_illum(const DLight& L, v3 P, v3& ldir, flo
 #define YK_PRIMARY_APPEND_WAVE false
 #endif
 #ifndef YK_BOUNCE_BLOCK
-#define YK_BOUNCE_BLOCK 512  // k_path_start, k_shade_bounce
+#define YK_BOUNCE_BLOCK 640  // k_path_start, k_shade_bounce (10 waves: two blocks fill a CU at 5 waves / SIMD)
 #endif
 #ifndef YK_BOUNCE_APPEND_WAVE
 #define YK_BOUNCE_APPEND_WAVE true
 #endif
-#ifdef YK_BOUNCE_WAVES  // occupancy target of k_shade_bounce (A/B builds)
-#define YK_BOUNCE_ATTR __attribute__((amdgpu_waves_per_eu(YK_BOUNCE_WAVES)))
-#else
-#define YK_BOUNCE_ATTR
+#ifndef YK_BOUNCE_WAVES
+#define YK_BOUNCE_WAVES 5  // occupancy target of k_shade_bounce
 #endif
+#define YK_BOUNCE_ATTR __attribute__((amdgpu_waves_per_eu(YK_BOUNCE_WAVES)))
 #ifndef YK_APPEND_BLOCK
 #define YK_APPEND_BLOCK 512  // photon / final-gather kernels
 #endif
@@ -3619,13 +3520,10 @@ void set_handout(yk_device* d, size_t nn) {
   d->S.chunk_max = d->crowded_leaves ? 64u : (unsigned)YK_POOL_CHUNK_MAX;
 }
 
-// Node packets of the resident tree (k_pack_nodes); with fewer than 2^28
-// nodes every interior word carries its empty-child bits (rbits 28).
+// Node packets of the resident tree (k_pack_nodes).
 void pack_nodes(yk_device* d, size_t nn) {
-  const bool bits = nn < (1u << 28);
-  d->S.rbits = bits ? 28u : 30u;
   hipLaunchKernelGGL(k_pack_nodes, dim3(grid_for((long long)nn)), dim3(256), 0, d->stream, d->nodes.p, d->pk.p,
-                     (unsigned)nn, bits ? 1 : 0);
+                     (unsigned)nn);
   HIPCHK(hipGetLastError());
   d->S.pk = d->pk.p;
 }

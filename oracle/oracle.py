@@ -3,8 +3,11 @@
 TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
 cpu_baseline leg of bench.py, never by the product (core_amd/).
 
-Parity unpinned under this tier's rule (no reference golden vectors, no
-oracle/_ref build): the oracle equals every survey-build reference output in
+Parity partly pinned: the QMC / fast-math functions are checked bit for bit
+against the reference's own headers compiled here (oracle/ref.mk,
+tests/test_ref_pinning.py); the traversal / shading / film restatement is
+unpinned under this tier's rule (its reference headers need the generated
+yafray_config.h) and equals every survey-build reference output in
 tests/golden/ bit for bit, which DESIGN.md §6 records as evidence only.
 """
 import ctypes as C

@@ -18,12 +18,17 @@
  * Build: gcc -O2 -std=c99 -fno-fast-math -ffp-contract=off (see Makefile):
  * IEEE binary32/binary64, no contraction, so each line below is one rounding.
  *
- * PARITY UNPINNED under this tier's rule. The reference holds no golden
- * vectors, and it cannot be built here without its CMake system (generated
- * yafray_config.h), so no oracle/_ref exists. The fixtures in tests/golden/
- * were rendered by the survey stage's CMake build of the reference; the
- * oracle equals every one of them bit for bit, which is
- * evidence, not a pin under this tier's rule. The kd-tree this oracle walks
+ * PARITY PARTLY PINNED. The reference's header-only QMC / fast-math layer
+ * (mcqmc.h Halton / RI_vdC / RI_S / RI_LP / fnv_32a_buf, mathOptimizations.h
+ * fSin / fCos / fExp2, math_utils.h Round2Int / Floor2Int) is compiled here
+ * from /root/reference/include by oracle/ref.mk into oracle/_ref/ref_check,
+ * which checks the functions below bit for bit against it (exhaustively
+ * where the domain allows; the only differences are the reference process's
+ * FTZ+DAZ denormal flush). The rest (traversal, MT, shading,
+ * film) needs the generated yafray_config.h and stays UNPINNED under this
+ * tier's rule: the fixtures in tests/golden/ were rendered by the survey
+ * stage's CMake build of the reference; the oracle equals every one of them
+ * bit for bit, which is evidence, not a pin. The kd-tree this oracle walks
  * comes from the product's host builder (a scene input, like the geometry);
  * that builder reproduces the reference's recorded tree statistics exactly.
  */
