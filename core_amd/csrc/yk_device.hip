@@ -230,6 +230,9 @@ __device__ __forceinline__ int lane_fresh() {
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
   return l;
 }
+#ifdef YK_TRAV_STATS
+__device__ unsigned long long g_spill_stores[1];
+#endif
 struct LaneStack {
   uint2* lds;    // [kStackLds][64]
   uint2* ovf;    // overflow area of the launch: each lane's entries contiguous (one cache line holds 8)
@@ -240,7 +243,12 @@ struct LaneStack {
   }
   __device__ __forceinline__ void push(int sp, uint2 e) const {
     uint2* slot = lds + (sp & (kStackLds - 1)) * 64 + lane_fresh();
-    if (sp >= kStackLds) *ovf_at(sp - kStackLds) = *slot;
+    if (sp >= kStackLds) {
+      *ovf_at(sp - kStackLds) = *slot;
+#ifdef YK_TRAV_STATS
+      atomicAdd(g_spill_stores, 1ull);  // diagnostic build: overflow-area stores (8 B each)
+#endif
+    }
     *slot = e;
   }
   __device__ __forceinline__ uint2 pop(int sp) const {  // sp = index of the entry to pop
@@ -1067,7 +1075,9 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
             __syncthreads();
             const int l = lane_fresh();
             const unsigned e = res_slot[l];
+#ifndef YK_NO_SHADOW_RESULTS  // attribution experiment only (PMC WRITE_SIZE without the result stores)
             occl[e >> 1] = (uint8_t)(e & 1u);
+#endif
             if (l + 64u < npend) res_slot[l] = res_slot[l + 64];
             npend -= 64u;
             __syncthreads();
@@ -1138,7 +1148,9 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
     const int l = lane_fresh();
     if ((unsigned)l < npend) {
       const unsigned e = res_slot[l];
+#ifndef YK_NO_SHADOW_RESULTS
       occl[e >> 1] = (uint8_t)(e & 1u);
+#endif
     }
   }
   // wave-reduced work counters (nodes visited, triangle tests)
@@ -3443,6 +3455,12 @@ void launch_trace(yk_device* d, Pipe& P, const yk_ray* rays, long long n, yk_hit
   unsigned long long* work = P.counters.p;
   unsigned long long* acc = P.counters.p + 128;
   HIPCHK(hipMemsetAsync(work, 0, 144 * sizeof(unsigned long long), P.stream));
+#ifdef YK_TRAV_STATS
+  {
+    const unsigned long long z = 0;
+    HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_spill_stores), &z, sizeof z, 0, hipMemcpyHostToDevice, P.stream));
+  }
+#endif
   enqueue_trace<CLOSEST>(d, P, rays, nullptr, RayCount{nullptr, 0, n}, hits, occ, work, acc, P.ev0, P.ev1);
   unsigned long long h[13];
   HIPCHK(hipMemcpyAsync(h, acc, sizeof h, hipMemcpyDeviceToHost, P.stream));
@@ -3462,6 +3480,10 @@ void launch_trace(yk_device* d, Pipe& P, const yk_ray* rays, long long n, yk_hit
     std::fprintf(stderr, "[trav-stats] %s cycles: refill %.1f%% descent %.1f%% leaf %.1f%% pop %.1f%%; per wave iteration %.0f\n",
                  CLOSEST ? "closest" : "shadow", 100.0 * h[9] / tot, 100.0 * h[10] / tot, 100.0 * h[11] / tot,
                  100.0 * h[12] / tot, tot / (double)h[4]);
+    unsigned long long sp = 0;
+    HIPCHK(hipMemcpyFromSymbol(&sp, HIP_SYMBOL(g_spill_stores), sizeof sp));
+    std::fprintf(stderr, "[trav-stats] %s overflow-area stores %llu (%.3f per ray, %.1f MB at 8 B each)\n",
+                 CLOSEST ? "closest" : "shadow", sp, (double)sp / (double)n, 8e-6 * (double)sp);
   }
 #endif
   if (!st) return;

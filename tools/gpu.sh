@@ -20,6 +20,7 @@
 #   coh:VARIANT          primary-shadow ray-order experiment (tools/coherence_bench.py)
 #   pmctb:VARIANT        PMC counter passes over the traversal microbenchmark (tools/pmc_dump.py summary)
 #   multi                tests/test_multi_device.py + tests/test_0_multi_process.py
+#   pmcw:VARIANT         WRITE_SIZE passes (one-pipe headline frame, traversal microbenchmark)
 #   mallocs              hipMalloc count of 1 vs 3 yk_render_multi calls (rocprofv3 --hip-trace)
 set -e
 cd $GRAFT_REPO_ROOT
@@ -119,6 +120,13 @@ EOF
     done
     python3 tools/pmc_dump.py $P > $P/summary.txt
     echo "pmctb $v done" ;;
+  pmcw:*)
+    # WRITE_SIZE of the one-pipe headline frame and of the traversal
+    # microbenchmark with library VARIANT (write-traffic attribution)
+    v=${s#pmcw:}
+    YK_LIB=$(lib $v) timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmcw_${v}_frame -o w -- python3 bench.py $P1 > $O/pmcw_${v}_frame.log 2>&1
+    YK_LIB=$(lib $v) timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmcw_${v}_tb -o w -- python3 tools/trav_bench.py --reps 1 > $O/pmcw_${v}_tb.log 2>&1
+    echo "pmcw $v done" ;;
   mallocs)
     for k in 1 3; do
       timeout -k 10 300 rocprofv3 --hip-trace --output-format csv -d $O/mallocs_$k -o m -- python3 tools/multi_malloc_trace.py --calls $k > $O/mallocs_$k.log 2>&1
