@@ -521,11 +521,6 @@ __device__ __forceinline__ void ld_packet(const char* base, uint32_t i, uint4& p
   const char* a = base + (size_t)i * (4 * kPkWords);
   p0 = *reinterpret_cast<const uint4*>(a);
   r = *reinterpret_cast<const uint2*>(a + 16);
-#ifdef YK_XLOAD  // experiment: one more load instruction per packet (cost of a lane-load)
-  uint32_t x;
-  asm volatile("global_load_dword %0, %1, off offset:4\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(a) : "memory");
-  asm volatile("" ::"v"(x));
-#endif
 }
 __global__ void k_pack_nodes(const uint2* __restrict__ nodes, uint32_t* __restrict__ pk, unsigned n) {
   const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -591,6 +586,12 @@ __device__ __forceinline__ uint32_t desc_decide(Trav& st, const LaneStack& stk, 
   return left_first ? node + 1u : right;
 }
 
+#ifndef YK_DESC_FRAC
+#define YK_DESC_FRAC 4  // measured 2 / 3 / 4 / 8: 2477 / 2524 / 2527 / 2450 Mrays/s (off: 2344)
+#endif
+#ifndef YK_DESC_FRAC_S
+#define YK_DESC_FRAC_S 3  // any-hit kernel (round 4: 1/3 vs 1/4, +0.4-0.8 % with the combined defaults)
+#endif
 // Descends from st.node to a leaf (the descent of trav_step); false when the
 // ray is already finished (dist < entry t). Outputs the leaf's w0 and count.
 template <bool CLOSEST>
@@ -608,12 +609,6 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
   nd = make_uint2(p0.x, p0.y);
   nnodes++;
   uint32_t ax = nd.y & 3u;
-#ifndef YK_DESC_FRAC
-#define YK_DESC_FRAC 4  // measured 2 / 3 / 4 / 8: 2477 / 2524 / 2527 / 2450 Mrays/s (off: 2344)
-#endif
-#ifndef YK_DESC_FRAC_S
-#define YK_DESC_FRAC_S 3  // any-hit kernel (round 4: 1/3 vs 1/4, +0.4-0.8 % with the combined defaults)
-#endif
   constexpr unsigned kFrac = CLOSEST ? YK_DESC_FRAC : YK_DESC_FRAC_S;
   // descent pause (YK_DESC_FRAC = f > 0): once fewer than 1/f of the lanes
   // that started this descent are still descending, those pause at their
@@ -968,7 +963,10 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
             ray_n0[lane_fresh()] = nnodes;
             if (CLOSEST || UNI) s_tmin[lane_fresh()] = st.tmin;
           } else if (CLOSEST) {
-            hits[r] = yk_hit{-1, 0.f, 0.f, 0.f};
+            // the miss record from constants materialised here (hoisted out of
+            // the loop, the compiler kept the 16-B constant in 4 VGPRs)
+            const unsigned m1 = vconst<0xFFFFFFFFu>(), z = vconst<0u>();
+            hits[r] = yk_hit{(int)m1, __uint_as_float(z), __uint_as_float(z), __uint_as_float(z)};
           } else {
             occl[r] = 0;
             if (TS) {
@@ -3550,13 +3548,16 @@ void pack_nodes(yk_device* d, size_t nn) {
   d->S.pk = d->pk.p;
 }
 
-// Traversal copies of the resident tree: the leaf-ordered triangles
-// (k_gather_leaf_tris) and the node packets (k_pack_nodes).
-// Callers check the node count (kMaxNodes) before they touch any resident
-// buffer, so a refused tree leaves the previous one intact.
-void install_traversal(yk_device* d, size_t nn, size_t nleaf, uint32_t max_leaf_refs) {
+// Traversal copies of the resident tree: the leaf-ordered records and the
+// node packets. nodes_h / leaf_h: the same tree on the host (unused: both
+// copies are made on the device; round 5's 16-B packet layout was built on
+// the host from them).
+void install_traversal(yk_device* d, size_t nn, size_t nleaf, uint32_t max_leaf_refs, const uint32_t* nodes_h,
+                       const uint32_t* leaf_h) {
   d->big_leaves = max_leaf_refs >= kBigLeaf;
   HIPCHK(hipDeviceSynchronize());  // every copy into nodes / leaf / tris has landed
+  (void)nodes_h;
+  (void)leaf_h;
   if (nleaf) {
     d->ltris.ensure(kTriWords * nleaf);
     hipLaunchKernelGGL(k_gather_leaf_tris, dim3(grid_for((long long)nleaf)), dim3(256), 0, d->stream, d->tris.p,
@@ -3750,7 +3751,7 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
     uint32_t max_refs = 0;
     for (size_t i = 0; i < nn; ++i)
       if ((S.tree.nodes[2 * i + 1] & 3u) == 3u) max_refs = std::max(max_refs, S.tree.nodes[2 * i + 1] >> 2);
-    install_traversal(d, nn, S.tree.leaf_prims.size(), max_refs);
+    install_traversal(d, nn, S.tree.leaf_prims.size(), max_refs, S.tree.nodes.data(), S.tree.leaf_prims.data());
   }
   {
     const long long filled = (long long)S.tree.stats.leaves - S.tree.stats.empty_leaves;
