@@ -250,7 +250,9 @@ def roofline_line(args, w, ms_c, ms_s, rst, elapsed, pt):
         ms = (ms_c, ms_s)
         timing = "timed frames: HIP events around every launch, overlapped by the other pipes"
     kc = dict(name="k_trace_closest", launches=cnt[6], ms=ms[0], bytes=algorithmic_bytes(cnt[0], cnt[2], cnt[3], 16))
-    ks = dict(name="k_trace_shadow", launches=cnt[7], ms=ms[1], bytes=algorithmic_bytes(cnt[1], cnt[4], cnt[5], 1))
+    # H = 4 B for the shadow result, as SURVEY.md §8(d) prices it (the kernel
+    # stores 1 B)
+    ks = dict(name="k_trace_shadow", launches=cnt[7], ms=ms[1], bytes=algorithmic_bytes(cnt[1], cnt[4], cnt[5], 4))
     for k in (kc, ks):
         k["gbs"] = k["bytes"] / (k["ms"] * 1e-3) / 1e9 if k["ms"] > 0 else 0.0
         k["avg_ms"] = k["ms"] / max(k["launches"], 1)
