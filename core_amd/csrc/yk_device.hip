@@ -114,21 +114,17 @@ struct DScene {
 
 __device__ __forceinline__ v3 ld3(const float* p) { return V3(p[0], p[1], p[2]); }
 
-// Triangle record, 48 B: (a, prim id) (e1 = b - a, 0) (e2 = c - a, 0) -- the
-// Moller-Trumbore inputs with the reference's own subtractions, three aligned
-// 16-B loads. (A 40-B packing measured equal: 2752 / 2756 Mrays/s.)
-constexpr unsigned kTriWords = 12;
-__device__ __forceinline__ void ld_tri(const float* rec, float4& A, float4& E1, float4& E2) {
-  A = *reinterpret_cast<const float4*>(rec);
-  E1 = *reinterpret_cast<const float4*>(rec + 4);
-  E2 = *reinterpret_cast<const float4*>(rec + 8);
-}
-// the same without the prim id and the pad words: three 12-B loads (the
-// any-hit test needs only a, e1, e2)
+// Triangle record, 36 B: a, e1 = b - a, e2 = c - a -- the Moller-Trumbore
+// inputs with the reference's own subtractions, three 12-B loads. Round 5:
+// tight 36-B records (the prim id, which only a closest hit's winner needs,
+// comes from the leaf list) instead of 48-B ones (a, prim id | e1, 0 | e2, 0),
+// so the traversal's triangle arrays take 25 % fewer cache lines and bytes
+// (1M probe: 183 MB instead of 244 MB; hair: 15 GB instead of 20 GB).
+constexpr unsigned kTriWords = 9;
 typedef float f3l __attribute__((ext_vector_type(3)));
-__device__ __forceinline__ void ld_tri12(const float* rec, float4& A, float4& E1, float4& E2) {
-  const f3l a = *reinterpret_cast<const f3l*>(rec), e1 = *reinterpret_cast<const f3l*>(rec + 4),
-            e2 = *reinterpret_cast<const f3l*>(rec + 8);
+__device__ __forceinline__ void ld_tri(const float* rec, float4& A, float4& E1, float4& E2) {
+  const f3l a = *reinterpret_cast<const f3l*>(rec), e1 = *reinterpret_cast<const f3l*>(rec + 3),
+            e2 = *reinterpret_cast<const f3l*>(rec + 6);
   A = make_float4(a.x, a.y, a.z, 0.f);
   E1 = make_float4(e1.x, e1.y, e1.z, 0.f);
   E2 = make_float4(e2.x, e2.y, e2.z, 0.f);
@@ -537,11 +533,11 @@ __global__ void k_pack_nodes(const uint2* __restrict__ nodes, uint32_t* __restri
 }
 
 // Leaf-ordered triangles: a copy of every leaf-list entry's
-// triangle (a, e1, e2 as in S.tris) in leaf-list order, with the primitive id
-// in the first float4's w. A multi-primitive leaf's k-th test then loads
-// ltris[3 (w0 + k)] directly instead of leaf[w0 + k] and then tris[3 p]: one
-// dependent memory round trip less per test, for 48 B per leaf reference
-// (196 MB on the 1M probe, 20 GB on the 10M hair scene: HBM is 288 GB).
+// triangle (a, e1, e2 as in S.tris) in leaf-list order. A multi-primitive
+// leaf's k-th test then loads ltris[w0 + k] directly instead of leaf[w0 + k]
+// and then tris[p]: one dependent memory round trip less per test, for 36 B
+// per leaf reference (147 MB on the 1M probe, 15 GB on the 10M hair scene:
+// HBM is 288 GB).
 __global__ void k_gather_leaf_tris(const float* __restrict__ tris, const uint32_t* __restrict__ leaf,
                                    float* __restrict__ out, unsigned n) {
   const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -549,8 +545,7 @@ __global__ void k_gather_leaf_tris(const float* __restrict__ tris, const uint32_
   const float* src = tris + (size_t)leaf[i] * kTriWords;
   float* dst = out + (size_t)i * kTriWords;
 #pragma unroll
-  for (unsigned w = 0; w < kTriWords; w += 2)
-    *reinterpret_cast<float2*>(dst + w) = *reinterpret_cast<const float2*>(src + w);
+  for (unsigned w = 0; w < kTriWords; ++w) dst[w] = src[w];
 }
 
 // One descent decision at interior node `node` (word nd, axis ax): the near /
@@ -783,14 +778,11 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
     float th = 0.f, u = 0.f, v = 0.f;
     uint32_t p = 0;
     if (s < total) {
-      // one load: the leaf's own record (prim id in A.w)
+      // one record: the leaf's own, in leaf order (a single-reference leaf's
+      // from the prim array)
       const float* tp = (on == 1u) ? S.tris + (size_t)ow0 * kTriWords : S.ltris + (size_t)(ow0 + k) * kTriWords;
       float4 A, E1, E2;
-      // any-hit: 36 of the record's 48 B (round 3: headline 2907 -> 2920, C2
-      // 8191 -> 8274; the prim id is the closest-hit kernel's only)
-      if (CLOSEST) ld_tri(tp, A, E1, E2);
-      else ld_tri12(tp, A, E1, E2);
-      p = __float_as_uint(A.w);
+      ld_tri(tp, A, E1, E2);
       asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
                    "+v"(E2.y), "+v"(E2.z));
       if (mt_intersect(V3(A.x, A.y, A.z), V3(E1.x, E1.y, E1.z), V3(E2.x, E2.y, E2.z), ro, rd, th, u, v)) {
@@ -807,7 +799,10 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
     }
     if (CLOSEST) {
       __syncthreads();
-      if (valid && keys[own] == key) cand[own] = make_float4(th, u, v, __uint_as_float(p));
+      if (valid && keys[own] == key) {  // the winner reads its prim id (leaf list) once
+        p = (on == 1u) ? ow0 : S.leaf[ow0 + k];
+        cand[own] = make_float4(th, u, v, __uint_as_float(p));
+      }
     }
   }
   __syncthreads();
@@ -3687,11 +3682,9 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
     r[0] = t[0];
     r[1] = t[1];
     r[2] = t[2];
-    const uint32_t pid = (uint32_t)p;
-    std::memcpy(&r[3], &pid, 4);
-    for (int k = 0; k < 3; ++k) {  // e1 at words 4-6, e2 at 8-10
-      r[4 + k] = e[k];
-      r[8 + k] = e[3 + k];
+    for (int k = 0; k < 3; ++k) {  // e1 at words 3-5, e2 at 6-8
+      r[3 + k] = e[k];
+      r[6 + k] = e[3 + k];
     }
     float nw;
     int m = S.tri_material[p] | (S.tri_smooth[p] ? kSmoothBit : 0);

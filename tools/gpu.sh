@@ -16,6 +16,7 @@
 #   ab:V1,V2,...         A/B: trav bench + headline bench per variant, two interleaved reps
 #   abc2:V1,V2,...       A/B on the Cornell (C2) bench
 #   abpm:V1,V2,...       A/B on the photon-mapping bench
+#   abhair:V1,V2,...     A/B on the C5 hair bench
 #   tbab:V1,V2,...       A/B of the traversal microbenchmark only, three interleaved reps
 #   coh:VARIANT          primary-shadow ray-order experiment (tools/coherence_bench.py)
 #   pmctb:VARIANT        PMC counter passes over the traversal microbenchmark (tools/pmc_dump.py summary)
@@ -66,9 +67,10 @@ for s in "$@"; do
     v=${s#tb:}
     YK_LIB=$(lib $v) timeout -k 10 200 python -u tools/trav_bench.py --spp 4 > $O/tb_$v.json 2> $O/tb_$v.err
     cat $O/tb_$v.json ;;
-  ab:*|abc2:*|abpm:*)
+  ab:*|abc2:*|abpm:*|abhair:*)
     VS=$(echo ${s#*:} | tr , ' ')
     BA="--no-cpu --steps 2 --warmup 1 --no-roofline-frame"; [ ${s%%:*} = abc2 ] && BA="$BA $C2"; [ ${s%%:*} = abpm ] && BA="$BA $PM"
+    [ ${s%%:*} = abhair ] && BA="--no-cpu --steps 1 --warmup 1 --no-roofline-frame $HAIR"
     for rep in 1 2; do
       for v in $VS; do
         L=$(lib $v)
