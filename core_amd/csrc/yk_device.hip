@@ -138,14 +138,16 @@ struct SurfPt {
 // ============================================================ traversal
 
 // bound_t::cross (Smits), compiled form: ((a1-a0)-p)*inv evaluates as (a1-from)*inv
-__device__ __forceinline__ bool bound_cross(const float* bb, v3 from, v3 dir, float& enter, float& leave,
+// inv: 1/dir per axis, the traversal's own invDir (bound.h computes the same
+// float 1.0/dir on every axis it uses), so each ray divides three times, not six
+__device__ __forceinline__ bool bound_cross(const float* bb, v3 from, v3 dir, v3 inv, float& enter, float& leave,
                                             float dist) {
   float lmin = -1e38f, lmax = 1e38f;
-  const float o[3] = {from.x, from.y, from.z}, d[3] = {dir.x, dir.y, dir.z};
+  const float o[3] = {from.x, from.y, from.z}, d[3] = {dir.x, dir.y, dir.z}, iv[3] = {inv.x, inv.y, inv.z};
 #pragma unroll
   for (int ax = 0; ax < 3; ++ax) {
     if (d[ax] != 0.f) {
-      const float invr = 1.0f / d[ax];
+      const float invr = iv[ax];
       const float t0 = (bb[ax] - o[ax]) * invr, t1 = (bb[3 + ax] - o[ax]) * invr;
       const float ltmin = invr > 0.f ? t0 : t1, ltmax = invr > 0.f ? t1 : t0;
       if (ax == 0) {
@@ -324,8 +326,8 @@ __device__ __forceinline__ bool trav_begin(const DScene& S, Trav& st, const yk_r
   st.prim = -1;
   st.b1 = st.b2 = 0.f;
   float a, b;
-  if (!bound_cross(S.bound, st.o, st.d, a, b, st.dist)) return false;
   st.inv = V3(1.0f / st.d.x, 1.0f / st.d.y, 1.0f / st.d.z);
+  if (!bound_cross(S.bound, st.o, st.d, st.inv, a, b, st.dist)) return false;
   st.en_t = a;
   st.en_split = a;
   st.en_code = (a >= 0.0f) ? 3u : 4u;  // from + a*dir, or the origin itself
@@ -2313,7 +2315,12 @@ __global__ void __launch_bounds__(YK_BOUNCE_BLOCK) YK_BOUNCE_ATTR k_shade_bounce
         hal_start(h2, 2u, (unsigned)((int)offs - 1));
         int lnum = (int)(hal_next(h2) * (float)R.nlights);
         if (lnum > R.nlights - 1) lnum = R.nlights - 1;
-        nr = gen_light(B, c, 0, lnum, sp, pwo, s, B.soffs[c], (unsigned)lnum, traced);
+        // one light (C2, the headline): a literal light index, so the
+        // compiler reads its record with scalar loads instead of per-lane
+        // vector loads (which go through the texture path that limits this
+        // kernel, PMC TD busy 0.9)
+        if (R.nlights == 1) nr = gen_light(B, c, 0, 0, sp, pwo, s, B.soffs[c], 0u, traced);
+        else nr = gen_light(B, c, 0, lnum, sp, pwo, s, B.soffs[c], (unsigned)lnum, traced);
         kend = c_lights[lnum].nslots;
         B.lsel[c] = lnum;
         ps |= PS_EST;

@@ -22,6 +22,7 @@
 #   pmctb:VARIANT        PMC counter passes over the traversal microbenchmark (tools/pmc_dump.py summary)
 #   multi                tests/test_multi_device.py + tests/test_0_multi_process.py
 #   pmcw:VARIANT         WRITE_SIZE passes (one-pipe headline frame, traversal microbenchmark)
+#   pmcb:c2|head         the pmctb counter sets over a one-pipe frame, every kernel
 #   mallocs              hipMalloc count of 1 vs 3 yk_render_multi calls (rocprofv3 --hip-trace)
 set -e
 cd $GRAFT_REPO_ROOT
@@ -129,6 +130,22 @@ EOF
     YK_LIB=$(lib $v) timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmcw_${v}_frame -o w -- python3 bench.py $P1 > $O/pmcw_${v}_frame.log 2>&1
     YK_LIB=$(lib $v) timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmcw_${v}_tb -o w -- python3 tools/trav_bench.py --reps 1 > $O/pmcw_${v}_tb.log 2>&1
     echo "pmcw $v done" ;;
+  pmcb:*)
+    # the pmctb counter sets over a one-pipe frame (c2 | head), all kernels
+    sc=${s#pmcb:}
+    A=""; [ $sc = c2 ] && A="$C2"
+    P=$O/pmcb_$sc
+    mkdir -p $P
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/kt -o kt -- python3 bench.py $A $P1 > $P/kt.log 2>&1
+    i=0
+    for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM" \
+             "SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TD_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum" \
+             "SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_IDX_ACTIVE SQ_LEVEL_WAVES SQ_INSTS_SMEM SQ_INST_LEVEL_LDS SQ_WAVES TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum GRBM_GUI_ACTIVE GRBM_COUNT"; do
+      i=$((i+1))
+      timeout -s KILL 200 rocprofv3 --pmc $C --output-format csv -d $P/p$i -o p$i -- python3 bench.py $A $P1 > $P/p$i.log 2>&1
+    done
+    python3 tools/pmc_dump.py $P "shade|trace|resolve" > $P/summary.txt
+    echo "pmcb $sc done" ;;
   mallocs)
     for k in 1 3; do
       timeout -k 10 300 rocprofv3 --hip-trace --output-format csv -d $O/mallocs_$k -o m -- python3 tools/multi_malloc_trace.py --calls $k > $O/mallocs_$k.log 2>&1
