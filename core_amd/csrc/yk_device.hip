@@ -109,6 +109,7 @@ struct DScene {
   unsigned depth_cap;  // tree depth + 2: node visits of one valid descent and stack entries of a
                        // valid traversal (the watchdog's bounds)
   unsigned chunk_max;  // largest ray hand-out chunk (64 for crowded-leaf scenes, whose rays are costly)
+  int nmats;           // material records in c_mats (the shading kernels copy them to LDS)
   int uni;             // universal mode (vTriangle_t getSurface: b0 = 0; IntersectS t > tmin)
 };
 
@@ -1926,9 +1927,9 @@ __device__ __forceinline__ int emit_shadow(const Batch& B, long long slot, const
 // k of `traced` (k < 64) for each slot that holds a ray.
 __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, int li, const SurfPt& sp, v3 wo,
                                          unsigned pixelSample, unsigned soffs, unsigned loffs,
-                                         unsigned long long& traced) {
+                                         unsigned long long& traced, const DMat* mats = c_mats) {
   const DLight& L = c_lights[li];
-  const DMat& M = c_mats[sp.mat];
+  const DMat& M = mats[sp.mat];
   const c3 black = C3(0.f, 0.f, 0.f);
   if (L.type != YK_LIGHT_AREA) {  // Dirac branch, mcintegrator.cc:85-100: one shadow ray
     const long long slot = slot_of(B, c, k0);
@@ -2086,6 +2087,19 @@ __device__ __forceinline__ yk_ray path_first_segment(const Batch& B, const Rende
 // waves per SIMD); forcing 5 or 6 spilled 124-200 B per lane and lost 2-4 %.
 __global__ void __launch_bounds__(YK_PRIMARY_BLOCK) k_shade_primary(DScene S, Batch B, RenderConst R, long long nc,
                                                        unsigned long long* __restrict__ qword) {
+  // The material records in LDS: per-lane reads of constant memory (the
+  // lanes' materials differ) go through the vector-memory path, which limits
+  // the shading kernels (C2 PMC: TD busy 0.87-0.90 of the CU's cycles, waves
+  // waiting 51-62 %); LDS reads do not. C2 +1.8 %. (The same copy in
+  // k_shade_bounce, with this depth's two Faure permutations, cost it spills
+  // and measured -0.7 %.)
+  __shared__ DMat s_mats[kMaxMats];
+  {
+    const int nw = S.nmats * (int)(sizeof(DMat) / sizeof(int));
+    for (int i = threadIdx.x; i < nw; i += YK_PRIMARY_BLOCK)
+      reinterpret_cast<int*>(s_mats)[i] = reinterpret_cast<const int*>(c_mats)[i];
+    __syncthreads();
+  }
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = c < nc;
   int nr = 0, kend = 0;
@@ -2101,7 +2115,7 @@ __global__ void __launch_bounds__(YK_PRIMARY_BLOCK) k_shade_primary(DScene S, Ba
       const yk_ray r = B.p_rays[c];
       const v3 from = V3(r.from[0], r.from[1], r.from[2]), dir = V3(r.dir[0], r.dir[1], r.dir[2]);
       const SurfPt sp = make_surface(S, from, dir, h);
-      const DMat& M = c_mats[sp.mat];
+      const DMat& M = s_mats[sp.mat];
       const v3 wo = vneg(dir);
       ph = PH_HIT;
       if (M.flags & BSDF_EMIT) {
@@ -2126,7 +2140,7 @@ __global__ void __launch_bounds__(YK_PRIMARY_BLOCK) k_shade_primary(DScene S, Ba
         const unsigned s = R.ps ? B.psample[c] : (unsigned)c % (unsigned)R.spp;
         int k0 = 0;
         for (int l = 0; l < R.nlights; ++l) {
-          nr += gen_light(B, c, k0, l, sp, wo, s, B.soffs[c], (unsigned)l, traced);
+          nr += gen_light(B, c, k0, l, sp, wo, s, B.soffs[c], (unsigned)l, traced, s_mats);
           k0 += c_lights[l].nslots;
         }
         kend = k0;
@@ -3747,6 +3761,7 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   d->S.vn = S.any_smooth ? d->vn.p : nullptr;
   std::memcpy(d->S.bound, S.tree.bound, sizeof d->S.bound);
   d->S.nlights = (int)S.light_states.size();
+  d->S.nmats = (int)mats.size();
   d->S.nnodes = (unsigned)nn;
   d->S.uni = S.mode == YK_MODE_UNIVERSAL ? 1 : 0;
   {
