@@ -110,6 +110,8 @@ struct DScene {
                        // valid traversal (the watchdog's bounds)
   unsigned chunk_max;  // largest ray hand-out chunk (64 for crowded-leaf scenes, whose rays are costly)
   int nmats;           // material records in c_mats (the shading kernels copy them to LDS)
+  unsigned ntris;      // records in tris
+  unsigned nlref;      // leaf-list entries (records in ltris)
   int uni;             // universal mode (vTriangle_t getSurface: b0 = 0; IntersectS t > tmin)
 };
 
@@ -123,9 +125,11 @@ __device__ __forceinline__ v3 ld3(const float* p) { return V3(p[0], p[1], p[2]);
 // (1M probe: 183 MB instead of 244 MB; hair: 15 GB instead of 20 GB).
 constexpr unsigned kTriWords = 9;
 typedef float f3l __attribute__((ext_vector_type(3)));
+// TW = 12: the 48-B records of a small scene's LDS copy (16-B aligned vectors)
+template <unsigned TW = kTriWords>
 __device__ __forceinline__ void ld_tri(const float* rec, float4& A, float4& E1, float4& E2) {
-  const f3l a = *reinterpret_cast<const f3l*>(rec), e1 = *reinterpret_cast<const f3l*>(rec + 3),
-            e2 = *reinterpret_cast<const f3l*>(rec + 6);
+  const f3l a = *reinterpret_cast<const f3l*>(rec), e1 = *reinterpret_cast<const f3l*>(rec + TW / 3),
+            e2 = *reinterpret_cast<const f3l*>(rec + 2 * (TW / 3));
   A = make_float4(a.x, a.y, a.z, 0.f);
   E1 = make_float4(e1.x, e1.y, e1.z, 0.f);
   E2 = make_float4(e2.x, e2.y, e2.z, 0.f);
@@ -232,18 +236,21 @@ __device__ __forceinline__ int lane_fresh() {
 #ifdef YK_TRAV_STATS
 __device__ unsigned long long g_spill_stores[1];
 #endif
-struct LaneStack {
-  uint2* lds;    // [kStackLds][64]
+// R: LDS ring depth (a power of two)
+template <int R>
+struct LaneStackT {
+  uint2* lds;    // [R][64], this wave's
   uint2* ovf;    // overflow area of the launch: each lane's entries contiguous (one cache line holds 8)
   unsigned depth;  // overflow entries per lane
+  unsigned wave;   // the wave's index in the launch (wave-uniform)
   // the lane's overflow entry k, addressed on use (rare)
   __device__ __forceinline__ uint2* ovf_at(int k) const {
-    return ovf + ((size_t)(blockIdx.x * 64u + (unsigned)lane_fresh()) * depth + (unsigned)k);
+    return ovf + ((size_t)(wave * 64u + (unsigned)lane_fresh()) * depth + (unsigned)k);
   }
   __device__ __forceinline__ void push(int sp, uint2 e) const {
-    uint2* slot = lds + (sp & (kStackLds - 1)) * 64 + lane_fresh();
-    if (sp >= kStackLds) {
-      *ovf_at(sp - kStackLds) = *slot;
+    uint2* slot = lds + (sp & (R - 1)) * 64 + lane_fresh();
+    if (sp >= R) {
+      *ovf_at(sp - R) = *slot;
 #ifdef YK_TRAV_STATS
       atomicAdd(g_spill_stores, 1ull);  // diagnostic build: overflow-area stores (8 B each)
 #endif
@@ -251,12 +258,13 @@ struct LaneStack {
     *slot = e;
   }
   __device__ __forceinline__ uint2 pop(int sp) const {  // sp = index of the entry to pop
-    uint2* slot = lds + (sp & (kStackLds - 1)) * 64 + lane_fresh();
+    uint2* slot = lds + (sp & (R - 1)) * 64 + lane_fresh();
     const uint2 e = *slot;
-    if (sp >= kStackLds) *slot = *ovf_at(sp - kStackLds);
+    if (sp >= R) *slot = *ovf_at(sp - R);
     return e;
   }
 };
+using LaneStack = LaneStackT<kStackLds>;
 // Entry and exit points are kept implicitly (no 3-float points in
 // registers): the reference's pb of an entry / exit is from + t*dir on every
 // axis but the one of the split plane it lies on, which is the split itself
@@ -516,8 +524,11 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
 // against 2497 without: lanes that keep going stretch the wave's iteration.)
 constexpr unsigned kPkWords = 6;
 // packet of node i: p0 = (word of i, word of its left child), r = right child's word
+// (STRIDE: 24 B in HBM; 32 B in the LDS copy of a small scene, whose 16-B
+// reads need 16-B alignment)
+template <unsigned STRIDE = 4 * kPkWords>
 __device__ __forceinline__ void ld_packet(const char* base, uint32_t i, uint4& p0, uint2& r) {
-  const char* a = base + (size_t)i * (4 * kPkWords);
+  const char* a = base + (size_t)i * STRIDE;
   p0 = *reinterpret_cast<const uint4*>(a);
   r = *reinterpret_cast<const uint2*>(a + 16);
 }
@@ -557,8 +568,8 @@ __global__ void k_gather_leaf_tris(const float* __restrict__ tris, const uint32_
 // (Round 5: empty-leaf elision here -- a near child that is an empty leaf
 // entered past in registers, a far one pushed flagged and popped through --
 // was parity-green and lost: DESIGN.md §5.)
-__device__ __forceinline__ uint32_t desc_decide(Trav& st, const LaneStack& stk, uint2 nd, uint32_t node,
-                                                uint32_t ax) {
+template <class STK>
+__device__ __forceinline__ uint32_t desc_decide(Trav& st, const STK& stk, uint2 nd, uint32_t node, uint32_t ax) {
   const float split = __uint_as_float(nd.x);
   const uint32_t right = nd.y >> 2;
   const bool a0 = ax == 0u, a1 = ax == 1u;
@@ -592,18 +603,18 @@ __device__ __forceinline__ uint32_t desc_decide(Trav& st, const LaneStack& stk, 
 #endif
 // Descends from st.node to a leaf (the descent of trav_step); false when the
 // ray is already finished (dist < entry t). Outputs the leaf's w0 and count.
-template <bool CLOSEST>
-__device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const LaneStack& stk, unsigned& nnodes,
-                                             uint32_t& w0, uint32_t& nref, bool& paused) {
+// nbase: the packets (S.pk, or their LDS copy with PKS = 32).
+template <bool CLOSEST, unsigned PKS = 4 * kPkWords, class STK>
+__device__ __forceinline__ bool trav_descend(const DScene& S, const char* nbase, Trav& st, const STK& stk,
+                                             unsigned& nnodes, uint32_t& w0, uint32_t& nref, bool& paused) {
   paused = false;
   if (st.dist < st.en_t) return false;
   // node indices are unsigned 32-bit offsets from the uniform node pointer
   // (one address VALU per load: base in SGPRs, 32-bit lane offset)
-  const char* nbase = reinterpret_cast<const char*>(S.pk);
   uint32_t node = (uint32_t)st.node;
   uint4 p0;
   uint2 p1, nd;
-  ld_packet(nbase, node, p0, p1);
+  ld_packet<PKS>(nbase, node, p0, p1);
   nd = make_uint2(p0.x, p0.y);
   nnodes++;
   uint32_t ax = nd.y & 3u;
@@ -640,7 +651,7 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
     ax = nd.y & 3u;
     if (ax != 3u) {
       nxt = desc_decide(st, stk, nd, node, ax);
-      ld_packet(nbase, nxt, p0, p1);
+      ld_packet<PKS>(nbase, nxt, p0, p1);
       nd = make_uint2(p0.x, p0.y);
       node = nxt;
       nnodes++;
@@ -665,8 +676,8 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, Trav& st, const La
 
 // After the leaf: the closest-hit stop test, then pop (kdtree.cc:802-812).
 // True when the ray is finished.
-template <bool CLOSEST>
-__device__ __forceinline__ bool trav_next(const DScene& S, Trav& st, const LaneStack& stk) {
+template <bool CLOSEST, class STK>
+__device__ __forceinline__ bool trav_next(const DScene& S, Trav& st, const STK& stk) {
   if (CLOSEST && st.Z < st.dist && st.Z <= st.ex_t) return true;
   st.en_t = st.ex_t;
   st.en_split = st.ex_split;
@@ -722,11 +733,30 @@ __device__ __forceinline__ unsigned dpp_max_scan(unsigned x) {
 // 24-bit owner keys: the keys then hold the start relative to the round and
 // the owner's start is read from its lane (one cross-lane read more per
 // round; measured 0.7 % slower, so only such trees run it).
-template <bool CLOSEST, bool BIG = false, bool UNI = false>
-__device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t nref, uint32_t w0,
+// Orders a wave's LDS traffic between the phases of the leaf test. W waves
+// per workgroup: with one, a barrier (which is what it was written with);
+// with several (the small-scene kernels), fences only -- the waves run
+// independent rays and never wait for each other.
+template <int W>
+__device__ __forceinline__ void wave_lds_sync() {
+  if constexpr (W == 1) {
+    __syncthreads();
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+}
+
+// tb / lb: the triangle records by prim and in leaf order (S.tris / S.ltris,
+// or their LDS copies: W > 1, 48-B records)
+template <bool CLOSEST, bool BIG = false, bool UNI = false, int W = 1>
+__device__ __forceinline__ void coop_leaves(const DScene& S, const float* tb, const float* lb, Trav& st,
+                                            uint32_t nref, uint32_t w0,
                                             std::conditional_t<CLOSEST, unsigned long long, unsigned>* keys,
                                             float4* cand, unsigned* otab, const float* s_tmin,
                                             unsigned& ntris, bool& occluded) {
+  constexpr unsigned TW = W > 1 ? 12u : kTriWords;  // record stride (words)
   const int lane = lane_fresh();
   unsigned x = nref;  // inclusive prefix sum of the lanes' reference counts
   // DPP scan: row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15 / 31
@@ -745,7 +775,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
     if (CLOSEST) keys[lane] = ((unsigned long long)m1 << 32) | m1;
     else keys[lane] = m1;  // any-hit keys are reference indices: 32 bits
   }
-  __syncthreads();  // one wave per block: orders the LDS traffic of the phase
+  wave_lds_sync<W>();
   const float zlim = CLOSEST ? st.Z : st.dist;
   unsigned carry = 0u;  // ((start + 1) << 8 | lane) of the range covering the previous slot
   for (unsigned base = 0; base < total; base += 64u) {
@@ -757,7 +787,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
     otab[lane] = 0u;
     if (nref > 0u && pre >= base && pre - base < 64u)
       otab[pre - base] = ((BIG ? pre - base : pre) << 8) + (vconst<0x100u>() | (unsigned)lane);
-    __syncthreads();
+    wave_lds_sync<W>();
     const unsigned ov = dpp_max_scan(otab[lane]);
     // slots before the round's first range start continue the range that
     // covered the previous round's last slot
@@ -783,9 +813,9 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
     if (s < total) {
       // one record: the leaf's own, in leaf order (a single-reference leaf's
       // from the prim array)
-      const float* tp = (on == 1u) ? S.tris + (size_t)ow0 * kTriWords : S.ltris + (size_t)(ow0 + k) * kTriWords;
+      const float* tp = (on == 1u) ? tb + (size_t)ow0 * TW : lb + (size_t)(ow0 + k) * TW;
       float4 A, E1, E2;
-      ld_tri(tp, A, E1, E2);
+      ld_tri<TW>(tp, A, E1, E2);
       asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
                    "+v"(E2.y), "+v"(E2.z));
       if (mt_intersect(V3(A.x, A.y, A.z), V3(E1.x, E1.y, E1.z), V3(E2.x, E2.y, E2.z), ro, rd, th, u, v)) {
@@ -801,14 +831,14 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, Trav& st, uint32_t 
       }
     }
     if (CLOSEST) {
-      __syncthreads();
+      wave_lds_sync<W>();
       if (valid && keys[own] == key) {  // the winner reads its prim id (leaf list) once
         p = (on == 1u) ? ow0 : S.leaf[ow0 + k];
         cand[own] = make_float4(th, u, v, __uint_as_float(p));
       }
     }
   }
-  __syncthreads();
+  wave_lds_sync<W>();
   if (nref > 0u) {
     const unsigned long long kk = CLOSEST ? (unsigned long long)keys[lane] : (keys[lane] == ~0u ? ~0ull : keys[lane]);
     if (CLOSEST) {
@@ -846,29 +876,120 @@ struct RayCount {
   }
 };
 
-template <bool CLOSEST, int NSEG, bool TS = false, bool BIG = false, bool UNI = false>
+// Small-scene kernels (W > 1 waves per workgroup): the workgroup copies the
+// whole traversal data -- node packets (32-B stride) and both record arrays
+// (48-B records) -- into LDS once, and its waves then trace from there, off
+// the vector-memory path that bounds the traversal. The waves
+// share nothing else: each has its own block of the per-wave LDS below.
+#ifndef YK_SMALL_W
+#define YK_SMALL_W 4  // waves per workgroup of the small-scene kernels
+#endif
+#ifndef YK_SMALL_RING
+#define YK_SMALL_RING 4  // their LDS stack ring depth (entries per lane)
+#endif
+#ifndef YK_SMALL_MAX
+#define YK_SMALL_MAX 16384  // largest LDS copy (bytes) that takes the small-scene kernels
+#endif
+extern __shared__ uint4 yk_dyn_lds[];
+template <bool CLOSEST, bool UNI, int R>
+struct WaveLds {
+  unsigned otab[64];
+  std::conditional_t<CLOSEST, unsigned long long, unsigned> keys[64];
+  float s_tmin[(CLOSEST || UNI) ? 64 : 1];
+  unsigned ray_n0[64];
+  unsigned res_slot[CLOSEST ? 1 : 128];
+  float4 cand[CLOSEST ? 64 : 1];
+  uint2 stack[R * 64];
+};
+// LDS copy of the traversal data: packets (8 words per node), then the
+// records by prim and in leaf order (12 words each: a, e1, e2 padded to 16 B)
+__device__ __forceinline__ void small_scene_copy(const DScene& S, uint32_t* dst, int W) {
+  const unsigned nthr = 64u * (unsigned)W;
+  const unsigned npk = S.nnodes * 8u;
+  for (unsigned i = threadIdx.x; i < npk; i += nthr) {
+    const unsigned w = i & 7u;
+    dst[i] = w < kPkWords ? S.pk[(i >> 3) * kPkWords + w] : 0u;
+  }
+  float* t = reinterpret_cast<float*>(dst + npk);
+  const unsigned nt = S.ntris * 12u, nl = S.nlref * 12u;
+  for (unsigned i = threadIdx.x; i < nt + nl; i += nthr) {
+    const bool own = i < nt;
+    const unsigned j = own ? i : i - nt, rec = j / 12u, w = j - rec * 12u, c = w & 3u;
+    const float* src = own ? S.tris : S.ltris;
+    t[i] = c < 3u ? src[rec * kTriWords + (w >> 2) * 3u + c] : 0.f;
+  }
+}
+size_t small_scene_bytes(size_t nn, size_t ntris, size_t nlref) { return 4 * (8 * nn + 12 * (ntris + nlref)); }
+
+template <bool CLOSEST, int NSEG, bool TS = false, bool BIG = false, bool UNI = false, int W = 1>
 __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx,
                                            RayCount rc, yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
                                            unsigned long long* __restrict__ work, unsigned long long* __restrict__ ctr,
                                            uint2* __restrict__ ovf, int ovf_depth, int refill_min,
                                            float* __restrict__ tsf = nullptr, int ts_depth = 0) {
-  // LDS of the cooperative leaf test first: its owner table then sits at
-  // offset 0, and its addresses need no base register
-  __shared__ unsigned otab[64];
-  __shared__ uint2 lds[kStackLds * 64];
-  __shared__ float s_tmin[(CLOSEST || UNI) ? 64 : 1];  // the lanes' tmin, read by the cooperative leaf test
-  // any-hit results awaiting their store: (ray index << 1) | occluded
-  __shared__ unsigned res_slot[(!CLOSEST && !TS) ? 128 : 1];
+  using KeyT = std::conditional_t<CLOSEST, unsigned long long, unsigned>;
+  constexpr int R = W > 1 ? YK_SMALL_RING : kStackLds;
+  unsigned* otab;
+  uint2* lds;
+  float* s_tmin;    // the lanes' tmin, read by the cooperative leaf test
+  unsigned* res_slot;  // any-hit results awaiting their store: (ray index << 1) | occluded
+  unsigned* ray_n0;
+  KeyT* keys;
+  float4* cand;
+  const char* nbase;  // traversal data: HBM, or the workgroup's LDS copy
+  const float *tb, *lb;
+  unsigned wv = 0;  // wave of the workgroup
+  int lane;
+  if constexpr (W == 1) {
+    // LDS of the cooperative leaf test first: its owner table then sits at
+    // offset 0, and its addresses need no base register
+    __shared__ unsigned a_otab[64];
+    __shared__ uint2 a_lds[kStackLds * 64];
+    __shared__ float a_tmin[(CLOSEST || UNI) ? 64 : 1];
+    __shared__ unsigned a_res[(!CLOSEST && !TS) ? 128 : 1];
+    __shared__ unsigned a_n0[64];
+    __shared__ KeyT a_keys[64];
+    __shared__ float4 a_cand[CLOSEST ? 64 : 1];
+    otab = a_otab;
+    lds = a_lds;
+    s_tmin = a_tmin;
+    res_slot = a_res;
+    ray_n0 = a_n0;
+    keys = a_keys;
+    cand = a_cand;
+    nbase = reinterpret_cast<const char*>(S.pk);
+    tb = S.tris;
+    lb = S.ltris;
+    lane = threadIdx.x;
+  } else {
+    __shared__ WaveLds<CLOSEST, UNI, R> s_w[W];
+    wv = (unsigned)__builtin_amdgcn_readfirstlane((int)threadIdx.x) >> 6;
+    WaveLds<CLOSEST, UNI, R>& L = s_w[wv];
+    otab = L.otab;
+    lds = L.stack;
+    s_tmin = L.s_tmin;
+    res_slot = L.res_slot;
+    ray_n0 = L.ray_n0;
+    keys = L.keys;
+    cand = L.cand;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(yk_dyn_lds);
+    small_scene_copy(S, dst, W);
+    __syncthreads();  // the only workgroup barrier: the waves run independently from here
+    nbase = reinterpret_cast<const char*>(dst);
+    tb = reinterpret_cast<const float*>(dst + S.nnodes * 8u);
+    lb = tb + S.ntris * 12u;
+    lane = threadIdx.x & 63u;
+  }
+  const unsigned gw = blockIdx.x * (unsigned)W + wv;  // wave of the launch
   unsigned npend = 0;  // wave-uniform
-  const int lane = threadIdx.x;
   const long long n = __builtin_amdgcn_readfirstlane((int)rc.get());
-  if (blockIdx.x == 0 && lane == 0 && n > 0) atomicAdd(&ctr[3], (unsigned long long)n);  // rays traced
+  if (gw == 0 && lane == 0 && n > 0) atomicAdd(&ctr[3], (unsigned long long)n);  // rays traced
   // Small launches (the later bounces: 0.1-2.5M rays on a grid of ~6k waves)
   // engage only the waves they can fill with a 64-ray chunk each: the others
   // leave at once instead of contending on the queue and counter atomics
   // (each wave's end-of-launch adds; a tail of ~0.3 ms per small launch)
-  if ((long long)blockIdx.x * 64 >= n + 63) return;
-  const LaneStack stk{lds, ovf, (unsigned)ovf_depth};
+  if ((long long)gw * 64 >= n + 63) return;
+  const LaneStackT<R> stk{lds, ovf, (unsigned)ovf_depth, gw};
   int rid = -1;  // ray of this lane (host guarantees n < 2^31)
   bool exhausted = false;
   Trav st;
@@ -894,7 +1015,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 #endif
   const unsigned kPoolChunk = (unsigned)__builtin_amdgcn_readfirstlane((int)max(
       64u, min(min((unsigned)YK_POOL_CHUNK_MAX, S.chunk_max),
-               (unsigned)(n / ((long long)gridDim.x * YK_POOL_CHUNKS)) & ~63u)));
+               (unsigned)(n / ((long long)gridDim.x * W * YK_POOL_CHUNKS)) & ~63u)));
   unsigned xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
   constexpr unsigned kAll = (1u << NSEG) - 1u;
@@ -904,8 +1025,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   // per-ray watchdog: a valid traversal visits every node at most once, so a
   // ray whose node visits exceed the tree's node count is looping through a
   // corrupt tree; checked every 32nd wave iteration against the lane's node
-  // count at the ray's start (kept in LDS, off the register budget)
-  __shared__ unsigned ray_n0[64];
+  // count at the ray's start (kept in LDS, off the register budget: ray_n0)
   unsigned iters = 0;
 #ifdef YK_TRAV_STATS
   // diagnostic build (ctr holds kAccWords = 16 words per kernel kind there):
@@ -1004,13 +1124,11 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
     s_act += (unsigned long long)__popcll(__ballot(rid >= 0));
 #endif
     if constexpr (!TS) {
-      __shared__ std::conditional_t<CLOSEST, unsigned long long, unsigned> keys[64];
-      __shared__ float4 cand[CLOSEST ? 64 : 1];
       const bool act = rid >= 0;
       bool live = false;
       uint32_t w0 = 0, nref = 0;
       bool paused = false;
-      if (act) live = trav_descend<CLOSEST>(S, st, stk, nnodes, w0, nref, paused);
+      if (act) live = trav_descend<CLOSEST, (W > 1 ? 32u : 4u * kPkWords)>(S, nbase, st, stk, nnodes, w0, nref, paused);
 #ifdef YK_TRAV_STATS
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       {
@@ -1020,7 +1138,8 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       }
 #endif
       bool occ = false;
-      coop_leaves<CLOSEST, BIG, UNI>(S, st, (live && !paused) ? nref : 0u, w0, keys, cand, otab, s_tmin, ntris, occ);
+      coop_leaves<CLOSEST, BIG, UNI, W>(S, tb, lb, st, (live && !paused) ? nref : 0u, w0, keys, cand, otab, s_tmin,
+                                         ntris, occ);
 #ifdef YK_TRAV_STATS
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       {
@@ -1068,7 +1187,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
           }
           npend += (unsigned)__popcll(fm);
           if (npend >= 64u) {
-            __syncthreads();
+            wave_lds_sync<W>();
             const int l = lane_fresh();
             const unsigned e = res_slot[l];
 #ifndef YK_NO_SHADOW_RESULTS  // attribution experiment only (PMC WRITE_SIZE without the result stores)
@@ -1076,7 +1195,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 #endif
             if (l + 64u < npend) res_slot[l] = res_slot[l + 64];
             npend -= 64u;
-            __syncthreads();
+            wave_lds_sync<W>();
           }
         }
       }
@@ -1140,7 +1259,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   }
 #endif
   if (!CLOSEST && !TS && npend) {  // the staged results left
-    __syncthreads();
+    wave_lds_sync<W>();
     const int l = lane_fresh();
     if ((unsigned)l < npend) {
       const unsigned e = res_slot[l];
@@ -1240,6 +1359,22 @@ k_trace_shadow_ts(DScene S, const yk_ray* __restrict__ rays, const unsigned* __r
                   unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
   trace_body<false, 1, true>(S, rays, idx, n, nullptr, occl, work, ctr, ovf, ovf_depth, refill_min, tsf,
                                     ts_depth);
+}
+// small scenes (traversal data in LDS, YK_SMALL_W waves per workgroup;
+// dynamic LDS = small_scene_bytes)
+__global__ void __launch_bounds__(64 * YK_SMALL_W) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
+k_trace_closest_small(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+                      yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
+                      unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
+  trace_body<true, 8, false, false, false, YK_SMALL_W>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth,
+                                                       refill_min);
+}
+__global__ void __launch_bounds__(64 * YK_SMALL_W) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
+k_trace_shadow_small(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+                     yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
+                     unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
+  trace_body<false, YK_SHADOW_SEGS, false, false, false, YK_SMALL_W>(S, rays, idx, n, hits, occl, work, ctr, ovf,
+                                                                     ovf_depth, refill_min);
 }
 
 // ============================================================ shading
@@ -3027,6 +3162,10 @@ struct yk_device {
   int cus = 0;
   int per_cu[2] = {1, 1};  // resident trace waves per CU: [0] any-hit, [1] closest
   int per_cu_big[2] = {1, 1};  // the same for the BIG-leaf kernels
+  // small scenes: traversal data copied to LDS per workgroup (install_traversal)
+  bool small = false;
+  size_t small_bytes = 0;
+  int per_cu_small[2] = {1, 1};  // resident workgroups (YK_SMALL_W waves) per CU
   hipStream_t stream = nullptr;  // = pipe[0].stream (ray queries, film resolve)
   bool uploaded = false;
   const yk_scene* uploaded_scene = nullptr;  // the scene the resident arrays came from
@@ -3430,16 +3569,19 @@ int refill_env() {
 template <bool CLOSEST>
 void enqueue_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* idx, RayCount n, yk_hit* hits,
                    uint8_t* occ, unsigned long long* work, unsigned long long* acc, hipEvent_t ev0, hipEvent_t ev1) {
-  const long long per_cu = d->big_leaves ? d->per_cu_big[CLOSEST] : d->per_cu[CLOSEST];
+  const bool small = d->small && !d->big_leaves && !d->S.uni;
+  const int waves = small ? YK_SMALL_W : 1;  // per workgroup
+  const long long per_cu = small ? d->per_cu_small[CLOSEST] : d->big_leaves ? d->per_cu_big[CLOSEST] : d->per_cu[CLOSEST];
   const long long grid = (long long)d->cus * per_cu;
-  const int ovf_depth = std::max(1, stack_depth(d) - kStackLds);
-  P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64);
+  const int ovf_depth = std::max(1, stack_depth(d) - (small ? YK_SMALL_RING : kStackLds));
+  P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64 * waves);
   if (ev0) HIPCHK(hipEventRecord(ev0, P.stream));
-  auto kern = CLOSEST ? (d->big_leaves ? k_trace_closest_big : k_trace_closest)
-                      : (d->S.uni ? (d->big_leaves ? k_trace_shadow_big_uni : k_trace_shadow_uni)
-                                  : (d->big_leaves ? k_trace_shadow_big : k_trace_shadow));
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), 0, P.stream, d->S, rays, idx, n, hits, occ, work, acc,
-                     P.ovf.p, ovf_depth, CLOSEST ? d->refill : d->refill_shadow);
+  auto kern = small ? (CLOSEST ? k_trace_closest_small : k_trace_shadow_small)
+              : CLOSEST ? (d->big_leaves ? k_trace_closest_big : k_trace_closest)
+                        : (d->S.uni ? (d->big_leaves ? k_trace_shadow_big_uni : k_trace_shadow_uni)
+                                    : (d->big_leaves ? k_trace_shadow_big : k_trace_shadow));
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * waves), small ? d->small_bytes : 0, P.stream, d->S, rays,
+                     idx, n, hits, occ, work, acc, P.ovf.p, ovf_depth, CLOSEST ? d->refill : d->refill_shadow);
   HIPCHK(hipGetLastError());
   if (ev1) HIPCHK(hipEventRecord(ev1, P.stream));
 }
@@ -3583,9 +3725,28 @@ void install_traversal(yk_device* d, size_t nn, size_t nleaf, uint32_t max_leaf_
     HIPCHK(hipGetLastError());
   }
   d->S.ltris = nleaf ? d->ltris.p : nullptr;
+  d->S.nlref = (unsigned)nleaf;
   d->pk.ensure(kPkWords * nn);
   pack_nodes(d, nn);
   HIPCHK(hipStreamSynchronize(d->stream));
+  // small scenes trace from an LDS copy of the traversal data. YK_SMALL (read
+  // per upload: A/B runs, tests): 0 never, a byte count > 1 overrides the
+  // size limit YK_SMALL_MAX (at most 46 KB: with the
+  // per-wave blocks a workgroup stays within 64 KB of LDS)
+  const char* small_env = std::getenv("YK_SMALL");
+  const long long small_v = small_env ? std::atoll(small_env) : 1;
+  const size_t small_max = small_v > 1 ? (size_t)std::min(small_v, 47104ll) : (size_t)YK_SMALL_MAX;
+  d->small_bytes = small_scene_bytes(nn, d->S.ntris, nleaf);
+  d->small = small_v != 0 && d->small_bytes <= small_max;
+  if (d->small) {
+    int blocks = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow_small, 64 * YK_SMALL_W,
+                                                        d->small_bytes));
+    d->per_cu_small[0] = std::max(1, blocks);
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_closest_small, 64 * YK_SMALL_W,
+                                                        d->small_bytes));
+    d->per_cu_small[1] = std::max(1, blocks);
+  }
 }
 
 }  // namespace
@@ -3763,6 +3924,7 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
   d->S.nlights = (int)S.light_states.size();
   d->S.nmats = (int)mats.size();
   d->S.nnodes = (unsigned)nn;
+  d->S.ntris = (unsigned)nt;
   d->S.uni = S.mode == YK_MODE_UNIVERSAL ? 1 : 0;
   {
     uint32_t max_refs = 0;

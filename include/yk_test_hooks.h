@@ -41,6 +41,12 @@ enum {
 };
 int yk_debug_qmc_probe(yk_device* d, int32_t fn, const void* in, const uint32_t* in2, int64_t n, void* out);
 
+/* Which traversal kernels the resident scene takes: *bytes = the size of the
+ * LDS copy of its traversal data when ray queries and renders run the
+ * small-scene kernels (node packets and triangle records in LDS), 0 when
+ * they read them from HBM. YK_ERR_UNSUPPORTED unless YK_DEBUG_HOOKS=1. */
+int yk_debug_small_scene(yk_device* d, int64_t* bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -171,6 +171,48 @@ def test_render_bit_exact(gpu_device, name, case, crop, over):
     assert st.closest_nodes == cnt["closest_nodes"] and st.shadow_tris == cnt["shadow_tris"]
 
 
+SMALL_CASES = [  # (scene, YK_SMALL): "0" = HBM kernels, "1" = default size limit, else a forced limit
+    (("cornell_pt", 64, 64, 0, 0), "0"), (("cornell_pt", 64, 64, 0, 0), "1"),
+    (("bumpy", 64, 64, 10, 7), "47104"), (("bumpy", 64, 64, 10, 7), "0"),
+]
+
+
+@pytest.mark.parametrize("case,small", SMALL_CASES, ids=lambda v: v[0] + str(v[3]) if isinstance(v, tuple) else v)
+def test_small_scene_kernels(gpu_device, monkeypatch, case, small):
+    """The small-scene traversal kernels (traversal data copied to LDS, four
+    waves per workgroup, a 4-entry stack ring) against the oracle, and the HBM
+    kernels on the same scenes: hits, occlusion, work counters and a
+    path-traced crop bit-exact either way. The 625-node bumpy tree, forced
+    onto the small kernels, spills its stack past the ring."""
+    import ctypes as C
+    monkeypatch.setenv("YK_DEBUG_HOOKS", "1")
+    monkeypatch.setenv("YK_SMALL", small)
+    s, _, orc = scene(*case)
+    gpu_device.upload(s)
+    nb = C.c_int64(-1)
+    A.check(A.lib().yk_debug_small_scene(gpu_device._p, C.byref(nb)))
+    assert (nb.value > 0) == (small != "0"), nb.value
+    rays = _ray_batch(s, 31)
+    prim, t, b1, b2, cnt = orc.intersect(rays)
+    st = A.yk_stats()
+    gp, gt, gb1, gb2 = gpu_device.split_hits(gpu_device.trace_closest(gpu_device.rays_to_device(rays), st))
+    assert (gp == prim).all(), f"{(gp != prim).sum()} prim mismatches"
+    hit = prim >= 0
+    for a, b in ((gt, t), (gb1, b1), (gb2, b2)):
+        assert (a[hit].view(np.uint32) == b[hit].view(np.uint32)).all()
+    assert st.closest_nodes == cnt[0] and st.closest_tris == cnt[1]
+    rays[:, 6] = 0.0005
+    rays[::2, 7] = np.abs(rays[::2, 7]) + 0.3
+    occ, cnt = orc.shadow(rays)
+    st = A.yk_stats()
+    gocc = gpu_device.trace_shadow(gpu_device.rays_to_device(rays), st).cpu().numpy()
+    assert (gocc == occ).all(), f"{(gocc != occ).sum()} mismatches"
+    assert st.shadow_nodes == cnt[0] and st.shadow_tris == cnt[1]
+    sums_o, sums_g, _, _, cnt, st = _render_pair(gpu_device, case, (0, 0, 64, 64))
+    assert st.closest_rays == cnt["closest"] and st.shadow_rays == cnt["shadow"]
+    assert (sums_g.view(np.uint32) == sums_o.view(np.uint32)).all()
+
+
 def test_render_sharded_sum(gpu_device):
     """Tile sharding (tile t -> shard t % n): per-shard films summed equal the
     1-shard film within float reassociation, and rays split exactly."""

@@ -3,7 +3,8 @@
 #   tools/gpu.sh OUTDIR STEP [STEP ...]
 # Every step runs under its own time limit; set -e stops at the first failure,
 # so nothing else touches the GPU after a fault, abort or timeout.
-# Steps (VARIANT = base for core_amd/libyk.so, else tune/libyk_VARIANT.so):
+# Steps (VARIANT = base for core_amd/libyk.so, else tune/libyk_VARIANT.so; VARIANT@NAME=VALUE
+# adds one environment setting, e.g. base@YK_SMALL=0):
 #   test                 pytest -m gpu (one process, per-test timeout)
 #   smoke                __graft_entry__.smoke()
 #   bench                headline bench.py (1M tris, 1080p, 256 spp)
@@ -30,7 +31,9 @@ export TMPDIR=/tmp
 O=gpurun_out/$1
 shift
 mkdir -p $O
-lib() { if [ "$1" = base ]; then echo $PWD/core_amd/libyk.so; else echo $PWD/tune/libyk_$1.so; fi; }
+# VARIANT[@NAME=VALUE]: the library plus one environment setting (env A/B)
+lib() { local v=${1%%@*}; if [ "$v" = base ]; then echo $PWD/core_amd/libyk.so; else echo $PWD/tune/libyk_$v.so; fi; }
+envv() { case $1 in *@*) echo "${1#*@}" ;; *) echo "YK_AB=1" ;; esac; }
 C2="--scene cornell --width 1024 --height 1024 --spp 64"
 HAIR="--scene hair --spp 16"
 PM="--integrator photon --spp 16"
@@ -76,9 +79,9 @@ for s in "$@"; do
       for v in $VS; do
         L=$(lib $v)
         if [ ${s%%:*} = ab ]; then
-          YK_LIB=$L timeout -k 10 200 python -u tools/trav_bench.py --spp 4 > $O/ab_tb_${v}_$rep.json 2> $O/ab_tb_${v}_$rep.err
+          env $(envv $v) YK_LIB=$L timeout -k 10 200 python -u tools/trav_bench.py --spp 4 > $O/ab_tb_${v}_$rep.json 2> $O/ab_tb_${v}_$rep.err
         fi
-        YK_LIB=$L timeout -k 10 300 python -u bench.py $BA > $O/${s%%:*}_b_${v}_$rep.json 2> $O/${s%%:*}_b_${v}_$rep.err
+        env $(envv $v) YK_LIB=$L timeout -k 10 300 python -u bench.py $BA > $O/${s%%:*}_b_${v}_$rep.json 2> $O/${s%%:*}_b_${v}_$rep.err
         python3 - $O ${s%%:*} $v $rep <<'EOF'
 import json, os, sys
 o, kind, v, rep = sys.argv[1:]
@@ -96,7 +99,7 @@ EOF
     VS=$(echo ${s#*:} | tr , ' ')
     for rep in 1 2 3; do
       for v in $VS; do
-        YK_LIB=$(lib $v) timeout -k 10 200 python -u tools/trav_bench.py --spp 4 > $O/tbab_${v}_$rep.json 2> $O/tbab_${v}_$rep.err
+        env $(envv $v) YK_LIB=$(lib $v) timeout -k 10 200 python -u tools/trav_bench.py --spp 4 > $O/tbab_${v}_$rep.json 2> $O/tbab_${v}_$rep.err
         python3 -c "import json;d=json.load(open('$O/tbab_${v}_$rep.json'));print('$v rep$rep', d['total_Mrays_s'], [d[k]['Mrays_s'] for k in ('camera','bounce','shadow1','shadow2')])"
       done
     done ;;
