@@ -126,8 +126,16 @@ __device__ __forceinline__ v3 ld3(const float* p) { return V3(p[0], p[1], p[2]);
 constexpr unsigned kTriWords = 9;
 typedef float f3l __attribute__((ext_vector_type(3)));
 // TW = 12: the 48-B records of a small scene's LDS copy (16-B aligned vectors)
+// (read as three 16-B vectors: ds_read_b128 serves 16 lanes per LDS cycle,
+// ds_read_b96 only 8)
 template <unsigned TW = kTriWords>
 __device__ __forceinline__ void ld_tri(const float* rec, float4& A, float4& E1, float4& E2) {
+  if constexpr (TW == 12u) {
+    A = *reinterpret_cast<const float4*>(rec);
+    E1 = *reinterpret_cast<const float4*>(rec + 4);
+    E2 = *reinterpret_cast<const float4*>(rec + 8);
+    return;
+  }
   const f3l a = *reinterpret_cast<const f3l*>(rec), e1 = *reinterpret_cast<const f3l*>(rec + TW / 3),
             e2 = *reinterpret_cast<const f3l*>(rec + 2 * (TW / 3));
   A = make_float4(a.x, a.y, a.z, 0.f);
@@ -523,14 +531,21 @@ __device__ __forceinline__ bool trav_step(const DScene& S, Trav& st, const LaneS
 // or popped through without loads -- measured 2185 / 2072 / 2394 Mrays/s
 // against 2497 without: lanes that keep going stretch the wave's iteration.)
 constexpr unsigned kPkWords = 6;
-// packet of node i: p0 = (word of i, word of its left child), r = right child's word
-// (STRIDE: 24 B in HBM; 32 B in the LDS copy of a small scene, whose 16-B
-// reads need 16-B alignment)
-template <unsigned STRIDE = 4 * kPkWords>
-__device__ __forceinline__ void ld_packet(const char* base, uint32_t i, uint4& p0, uint2& r) {
-  const char* a = base + (size_t)i * STRIDE;
-  p0 = *reinterpret_cast<const uint4*>(a);
-  r = *reinterpret_cast<const uint2*>(a + 16);
+// packet of node i: p0 = (word of i, word of its left child), r = right child's word.
+// LDSL: the LDS copy of a small scene, split in two arrays -- p0 at base +
+// 16 i, r at base2 + 8 i: a ds_read_b128 serves 16 lanes per LDS cycle when
+// their 16-B slots lie in distinct bank quads, and a 32-B packet stride
+// would leave half of the quads unused (MI355X_MICROARCH.md §LDS)
+template <bool LDSL = false>
+__device__ __forceinline__ void ld_packet(const char* base, const char* base2, uint32_t i, uint4& p0, uint2& r) {
+  if constexpr (LDSL) {
+    p0 = reinterpret_cast<const uint4*>(base)[i];
+    r = reinterpret_cast<const uint2*>(base2)[i];
+  } else {
+    const char* a = base + (size_t)i * (4 * kPkWords);
+    p0 = *reinterpret_cast<const uint4*>(a);
+    r = *reinterpret_cast<const uint2*>(a + 16);
+  }
 }
 __global__ void k_pack_nodes(const uint2* __restrict__ nodes, uint32_t* __restrict__ pk, unsigned n) {
   const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -603,9 +618,10 @@ __device__ __forceinline__ uint32_t desc_decide(Trav& st, const STK& stk, uint2 
 #endif
 // Descends from st.node to a leaf (the descent of trav_step); false when the
 // ray is already finished (dist < entry t). Outputs the leaf's w0 and count.
-// nbase: the packets (S.pk, or their LDS copy with PKS = 32).
-template <bool CLOSEST, unsigned PKS = 4 * kPkWords, class STK>
-__device__ __forceinline__ bool trav_descend(const DScene& S, const char* nbase, Trav& st, const STK& stk,
+// nbase: the packets (S.pk, or with LDSL their LDS copy, right words at nbase2).
+template <bool CLOSEST, bool LDSL = false, class STK>
+__device__ __forceinline__ bool trav_descend(const DScene& S, const char* nbase, const char* nbase2, Trav& st,
+                                             const STK& stk,
                                              unsigned& nnodes, uint32_t& w0, uint32_t& nref, bool& paused) {
   paused = false;
   if (st.dist < st.en_t) return false;
@@ -614,7 +630,7 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, const char* nbase,
   uint32_t node = (uint32_t)st.node;
   uint4 p0;
   uint2 p1, nd;
-  ld_packet<PKS>(nbase, node, p0, p1);
+  ld_packet<LDSL>(nbase, nbase2, node, p0, p1);
   nd = make_uint2(p0.x, p0.y);
   nnodes++;
   uint32_t ax = nd.y & 3u;
@@ -651,7 +667,7 @@ __device__ __forceinline__ bool trav_descend(const DScene& S, const char* nbase,
     ax = nd.y & 3u;
     if (ax != 3u) {
       nxt = desc_decide(st, stk, nd, node, ax);
-      ld_packet<PKS>(nbase, nxt, p0, p1);
+      ld_packet<LDSL>(nbase, nbase2, nxt, p0, p1);
       nd = make_uint2(p0.x, p0.y);
       node = nxt;
       nnodes++;
@@ -901,16 +917,18 @@ struct WaveLds {
   float4 cand[CLOSEST ? 64 : 1];
   uint2 stack[R * 64];
 };
-// LDS copy of the traversal data: packets (8 words per node), then the
+// LDS copy of the traversal data: the packets' 16-B halves (4 words per
+// node), their right words (2 per node), then -- from a 16-B boundary -- the
 // records by prim and in leaf order (12 words each: a, e1, e2 padded to 16 B)
+__host__ __device__ __forceinline__ unsigned small_rec_word(unsigned nn) { return (nn * 6u + 3u) & ~3u; }
 __device__ __forceinline__ void small_scene_copy(const DScene& S, uint32_t* dst, int W) {
   const unsigned nthr = 64u * (unsigned)W;
-  const unsigned npk = S.nnodes * 8u;
-  for (unsigned i = threadIdx.x; i < npk; i += nthr) {
-    const unsigned w = i & 7u;
-    dst[i] = w < kPkWords ? S.pk[(i >> 3) * kPkWords + w] : 0u;
+  const unsigned n4 = S.nnodes * 4u, n6 = S.nnodes * 6u;
+  for (unsigned i = threadIdx.x; i < n6; i += nthr) {
+    const unsigned node = i < n4 ? i >> 2 : (i - n4) >> 1, w = i < n4 ? i & 3u : 4u + ((i - n4) & 1u);
+    dst[i] = S.pk[node * kPkWords + w];
   }
-  float* t = reinterpret_cast<float*>(dst + npk);
+  float* t = reinterpret_cast<float*>(dst + small_rec_word(S.nnodes));
   const unsigned nt = S.ntris * 12u, nl = S.nlref * 12u;
   for (unsigned i = threadIdx.x; i < nt + nl; i += nthr) {
     const bool own = i < nt;
@@ -919,7 +937,9 @@ __device__ __forceinline__ void small_scene_copy(const DScene& S, uint32_t* dst,
     t[i] = c < 3u ? src[rec * kTriWords + (w >> 2) * 3u + c] : 0.f;
   }
 }
-size_t small_scene_bytes(size_t nn, size_t ntris, size_t nlref) { return 4 * (8 * nn + 12 * (ntris + nlref)); }
+size_t small_scene_bytes(size_t nn, size_t ntris, size_t nlref) {
+  return 4 * (((6 * nn + 3) & ~(size_t)3) + 12 * (ntris + nlref));  // small_rec_word in 64 bits
+}
 
 template <bool CLOSEST, int NSEG, bool TS = false, bool BIG = false, bool UNI = false, int W = 1>
 __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx,
@@ -937,6 +957,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   KeyT* keys;
   float4* cand;
   const char* nbase;  // traversal data: HBM, or the workgroup's LDS copy
+  const char* nbase2 = nullptr;
   const float *tb, *lb;
   unsigned wv = 0;  // wave of the workgroup
   int lane;
@@ -976,7 +997,8 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
     small_scene_copy(S, dst, W);
     __syncthreads();  // the only workgroup barrier: the waves run independently from here
     nbase = reinterpret_cast<const char*>(dst);
-    tb = reinterpret_cast<const float*>(dst + S.nnodes * 8u);
+    nbase2 = reinterpret_cast<const char*>(dst + S.nnodes * 4u);
+    tb = reinterpret_cast<const float*>(dst + small_rec_word(S.nnodes));
     lb = tb + S.ntris * 12u;
     lane = threadIdx.x & 63u;
   }
@@ -1128,7 +1150,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       bool live = false;
       uint32_t w0 = 0, nref = 0;
       bool paused = false;
-      if (act) live = trav_descend<CLOSEST, (W > 1 ? 32u : 4u * kPkWords)>(S, nbase, st, stk, nnodes, w0, nref, paused);
+      if (act) live = trav_descend<CLOSEST, (W > 1)>(S, nbase, nbase2, st, stk, nnodes, w0, nref, paused);
 #ifdef YK_TRAV_STATS
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       {
