@@ -28,6 +28,7 @@ from core_amd.scene import probe_scene  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 L2_PEAK_GBS = 34500.0  # aggregate L2 bandwidth, 8 XCDs (MI355X_MICROARCH.md, "L2 (per XCD)")
+LDS_PEAK_GBS = 150000.0  # aggregate LDS read bandwidth, ds_read_b64/b128 on every CU (MI355X_MICROARCH.md §LDS)
 
 
 def algorithmic_bytes(rays, nodes, tris, out_bytes):
@@ -101,6 +102,7 @@ def main():
     dev = Device(local)
     dev.upload(scene)
     tree_info = dev.build_tree(scene) if args.gpu_tree else None
+    small = small_scene_bytes(dev)
     pm_info = None
     if args.integrator == "photon":  # photonIntegrator_t::preprocess, once per scene (not timed)
         p.integrator = A.YK_INTEGRATOR_PHOTON
@@ -182,7 +184,7 @@ def main():
         dist.destroy_process_group()
         return
 
-    roofline = roofline_line(args, w, ms_c, ms_s, rst, elapsed, pm_info is None)
+    roofline = roofline_line(args, w, ms_c, ms_s, rst, elapsed, pm_info is None, small)
 
     cpu = None
     if not args.no_cpu:
@@ -236,10 +238,30 @@ def main():
         dist.destroy_process_group()
 
 
-def roofline_line(args, w, ms_c, ms_s, rst, elapsed, pt):
+def small_scene_bytes(dev):
+    """Bytes of the LDS copy of the traversal data when the resident scene runs
+    the small-scene kernels (k_trace_*_small), else 0 (read-only query of the
+    test-hooks header, enabled for this call)."""
+    old = os.environ.get("YK_DEBUG_HOOKS")
+    os.environ["YK_DEBUG_HOOKS"] = "1"
+    try:
+        b = C.c_int64(0)
+        A.check(A.lib().yk_debug_small_scene(dev._p, C.byref(b)))
+        return int(b.value)
+    finally:
+        if old is None:
+            del os.environ["YK_DEBUG_HOOKS"]
+        else:
+            os.environ["YK_DEBUG_HOOKS"] = old
+
+
+def roofline_line(args, w, ms_c, ms_s, rst, elapsed, pt, small=0):
     """Roofline of the dominant traversal kernel. Durations come from the
     serialised roofline frame (rst) when it ran, else from the timed frames'
-    HIP events (overlapped by the other pipes: a lower bound on the rate)."""
+    HIP events (overlapped by the other pipes: a lower bound on the rate).
+    small > 0: the scene's traversal data sits in LDS (small-scene kernels),
+    so its node / record bytes are LDS reads; the line then also prices them
+    against the LDS peak."""
     if rst is not None:
         cnt = [rst.closest_rays, rst.shadow_rays, rst.closest_nodes, rst.closest_tris, rst.shadow_nodes,
                rst.shadow_tris, rst.closest_launches, rst.shadow_launches]
@@ -249,10 +271,11 @@ def roofline_line(args, w, ms_c, ms_s, rst, elapsed, pt):
         cnt = list(w[:8])
         ms = (ms_c, ms_s)
         timing = "timed frames: HIP events around every launch, overlapped by the other pipes"
-    kc = dict(name="k_trace_closest", launches=cnt[6], ms=ms[0], bytes=algorithmic_bytes(cnt[0], cnt[2], cnt[3], 16))
+    sfx = "_small" if small else ""
+    kc = dict(name="k_trace_closest" + sfx, launches=cnt[6], ms=ms[0], bytes=algorithmic_bytes(cnt[0], cnt[2], cnt[3], 16))
     # H = 4 B for the shadow result, as SURVEY.md §8(d) prices it (the kernel
     # stores 1 B)
-    ks = dict(name="k_trace_shadow", launches=cnt[7], ms=ms[1], bytes=algorithmic_bytes(cnt[1], cnt[4], cnt[5], 4))
+    ks = dict(name="k_trace_shadow" + sfx, launches=cnt[7], ms=ms[1], bytes=algorithmic_bytes(cnt[1], cnt[4], cnt[5], 4))
     for k in (kc, ks):
         k["gbs"] = k["bytes"] / (k["ms"] * 1e-3) / 1e9 if k["ms"] > 0 else 0.0
         k["avg_ms"] = k["ms"] / max(k["launches"], 1)
@@ -294,6 +317,11 @@ def roofline_line(args, w, ms_c, ms_s, rst, elapsed, pt):
         out["traffic_source"] = traffic_note
     out["hbm"] = {"peak": HBM_PEAK_GBS, "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4)}
     out["l2"] = {"peak": L2_PEAK_GBS, "frac": round(dom["gbs"] / L2_PEAK_GBS, 4)}
+    if small:
+        out["lds"] = {"peak": LDS_PEAK_GBS, "frac": round(dom["gbs"] / LDS_PEAK_GBS, 4), "scene_copy_bytes": small,
+                      "note": "traversal data (node packets, triangle records) copied to LDS once per 4-wave "
+                              "workgroup: the per-node / per-test bytes are LDS reads, only rays and results "
+                              "cross HBM"}
     # all traversal bytes of the timed frames over their wall time
     out["traversal_achieved_wall"] = round((algorithmic_bytes(w[0], w[2], w[3], 16) +
                                             algorithmic_bytes(w[1], w[4], w[5], 1)) / elapsed / 1e9, 2)

@@ -8,7 +8,9 @@ Populations (synthetic, in the renderer's tile / pixel / sample order):
   shadow1 : from the camera hits to a uniform point of the 1x1 area light
   bounce  : cosine-hemisphere rays from the camera hits
   shadow2 : from the bounce hits to the light
-  python tools/trav_bench.py [--reps 3] [--spp 2]
+  python tools/trav_bench.py [--reps 3] [--spp 2] [--scene cornell]
+(--scene cornell: the C2 Cornell box, camera at (0, 1, -3.4) toward the box's
+centre, shadow rays to a 0.5 x 0.5 square under the ceiling)
 """
 import argparse
 import json
@@ -27,10 +29,10 @@ from core_amd.device import Device  # noqa: E402
 from core_amd.scene import probe_scene  # noqa: E402
 
 
-def camera_rays(w, h, spp, dev, gen):
+def camera_rays(w, h, spp, dev, gen, cornell=False):
     # pinhole from (0,1.5,-4) toward (0,1.2,0), vertical fov ~ 2*atan(0.5/1.4)
-    eye = torch.tensor([0.0, 1.5, -4.0], device=dev)
-    fwd = torch.tensor([0.0, -0.3, 4.0], device=dev)
+    eye = torch.tensor([0.0, 1.0, -3.4] if cornell else [0.0, 1.5, -4.0], device=dev)
+    fwd = torch.tensor([0.0, 0.0, 1.0] if cornell else [0.0, -0.3, 4.0], device=dev)
     fwd = fwd / fwd.norm()
     right = torch.linalg.cross(torch.tensor([0.0, 1.0, 0.0], device=dev), fwd)
     right = right / right.norm()
@@ -65,9 +67,11 @@ def hit_points(rays, hits, ng):
     return P, N
 
 
-def shadow_rays(P, gen):
+def shadow_rays(P, gen, cornell=False):
     q = torch.rand((len(P), 2), device=P.device, generator=gen) - 0.5
-    L = torch.stack([q[:, 0], torch.full_like(q[:, 0], 3.0), q[:, 1]], 1)
+    if cornell:
+        q = q * 0.5
+    L = torch.stack([q[:, 0], torch.full_like(q[:, 0], 1.98 if cornell else 3.0), q[:, 1]], 1)
     d = L - P
     dist = d.norm(dim=1)
     r = torch.zeros((len(P), 8), device=P.device)
@@ -103,21 +107,23 @@ def main():
     ap.add_argument("--spp", type=int, default=2)
     ap.add_argument("--nu", type=int, default=1000)
     ap.add_argument("--nv", type=int, default=501)
+    ap.add_argument("--scene", default="bumpy", choices=["bumpy", "cornell"])
     args = ap.parse_args()
-    scene, _ = probe_scene("bumpy", 64, 64, args.nu, args.nv)
+    cb = args.scene == "cornell"
+    scene, _ = probe_scene("cornell_pt", 64, 64) if cb else probe_scene("bumpy", 64, 64, args.nu, args.nv)
     ng = torch.from_numpy(scene.export()["tri_normal"]).cuda()
     dev = Device(0)
     dev.upload(scene)
     gen = torch.Generator(device="cuda")
     gen.manual_seed(7)
-    cam = camera_rays(1920, 1080, args.spp, "cuda", gen)
+    cam = camera_rays(1920, 1080, args.spp, "cuda", gen, cb)
     h0 = dev.trace_closest(cam)
     P, N = hit_points(cam, h0, ng)
-    sh1 = shadow_rays(P, gen)
+    sh1 = shadow_rays(P, gen, cb)
     bo = bounce_rays(P, N, gen)
     h1 = dev.trace_closest(bo)
     P2, _ = hit_points(bo, h1, ng)
-    sh2 = shadow_rays(P2, gen)
+    sh2 = shadow_rays(P2, gen, cb)
     out = {"lib": os.path.basename(A.LIB_PATH)}
     tot_rays = tot_ms = 0.0
     for name, rays, closest in (("camera", cam, True), ("bounce", bo, True), ("shadow1", sh1, False),
