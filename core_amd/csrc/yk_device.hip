@@ -1398,6 +1398,13 @@ k_trace_shadow_small(DScene S, const yk_ray* __restrict__ rays, const unsigned* 
   trace_body<false, YK_SHADOW_SEGS, false, false, false, YK_SMALL_W>(S, rays, idx, n, hits, occl, work, ctr, ovf,
                                                                      ovf_depth, refill_min);
 }
+__global__ void __launch_bounds__(64 * YK_SMALL_W) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
+k_trace_shadow_uni_small(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+                         yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
+                         unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
+  trace_body<false, 1, false, false, true, YK_SMALL_W>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth,
+                                                       refill_min);
+}
 
 // ============================================================ shading
 
@@ -3187,7 +3194,7 @@ struct yk_device {
   // small scenes: traversal data copied to LDS per workgroup (install_traversal)
   bool small = false;
   size_t small_bytes = 0;
-  int per_cu_small[2] = {1, 1};  // resident workgroups (YK_SMALL_W waves) per CU
+  int per_cu_small[3] = {1, 1, 1};  // resident workgroups (YK_SMALL_W waves) per CU: any-hit, closest, universal any-hit
   hipStream_t stream = nullptr;  // = pipe[0].stream (ray queries, film resolve)
   bool uploaded = false;
   const yk_scene* uploaded_scene = nullptr;  // the scene the resident arrays came from
@@ -3591,14 +3598,14 @@ int refill_env() {
 template <bool CLOSEST>
 void enqueue_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* idx, RayCount n, yk_hit* hits,
                    uint8_t* occ, unsigned long long* work, unsigned long long* acc, hipEvent_t ev0, hipEvent_t ev1) {
-  const bool small = d->small && !d->big_leaves && !d->S.uni;
+  const bool small = d->small && !d->big_leaves;
   const int waves = small ? YK_SMALL_W : 1;  // per workgroup
-  const long long per_cu = small ? d->per_cu_small[CLOSEST] : d->big_leaves ? d->per_cu_big[CLOSEST] : d->per_cu[CLOSEST];
+  const long long per_cu = small ? d->per_cu_small[(!CLOSEST && d->S.uni) ? 2 : (int)CLOSEST] : d->big_leaves ? d->per_cu_big[CLOSEST] : d->per_cu[CLOSEST];
   const long long grid = (long long)d->cus * per_cu;
   const int ovf_depth = std::max(1, stack_depth(d) - (small ? YK_SMALL_RING : kStackLds));
   P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64 * waves);
   if (ev0) HIPCHK(hipEventRecord(ev0, P.stream));
-  auto kern = small ? (CLOSEST ? k_trace_closest_small : k_trace_shadow_small)
+  auto kern = small ? (CLOSEST ? k_trace_closest_small : d->S.uni ? k_trace_shadow_uni_small : k_trace_shadow_small)
               : CLOSEST ? (d->big_leaves ? k_trace_closest_big : k_trace_closest)
                         : (d->S.uni ? (d->big_leaves ? k_trace_shadow_big_uni : k_trace_shadow_uni)
                                     : (d->big_leaves ? k_trace_shadow_big : k_trace_shadow));
@@ -3768,6 +3775,9 @@ void install_traversal(yk_device* d, size_t nn, size_t nleaf, uint32_t max_leaf_
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_closest_small, 64 * YK_SMALL_W,
                                                         d->small_bytes));
     d->per_cu_small[1] = std::max(1, blocks);
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow_uni_small, 64 * YK_SMALL_W,
+                                                        d->small_bytes));
+    d->per_cu_small[2] = std::max(1, blocks);
   }
 }
 

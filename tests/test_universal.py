@@ -162,3 +162,36 @@ def test_universal_render_bit_exact(gpu_device, kind, over):
     st = gpu_device.render_shard(p, film)
     assert st.closest_rays == cnt["closest"] and st.shadow_rays == cnt["shadow"]
     assert (film.cpu().numpy().view(np.uint32) == sums_o.view(np.uint32)).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("small", ["0", "1"])
+def test_universal_small_scene_kernels(gpu_device, monkeypatch, small):
+    """Universal mode on a scene small enough for the LDS-resident traversal
+    kernels (the Cornell box as VTRIM meshes): k_trace_shadow_uni_small and
+    the HBM kernels both equal the oracle (t > tmin any-hit rule, counters)."""
+    import ctypes as C
+    from oracle.oracle import Oracle
+    monkeypatch.setenv("YK_DEBUG_HOOKS", "1")
+    monkeypatch.setenv("YK_SMALL", small)
+    s = Scene()
+    s.generate("cornell_pt", 16, 16)
+    s.set_mode(A.YK_MODE_UNIVERSAL)
+    for oid in range(1, s.info().nmeshes + 1):
+        s.set_mesh_type(oid, A.YK_MESH_VTRIM)
+    s.build()
+    orc = Oracle(s)
+    gpu_device.upload(s)
+    nb = C.c_int64(-1)
+    A.check(A.lib().yk_debug_small_scene(gpu_device._p, C.byref(nb)))
+    assert (nb.value > 0) == (small != "0")
+    e = s.export()
+    rays = np.concatenate([random_rays(e["bound"], 20000, 5), edge_rays(e["bound"], e["nodes"], 6)])
+    rays[:, 6] = 0.05
+    rays[::2, 7] = np.abs(rays[::2, 7]) + 0.4
+    occ, cnt = orc.shadow(rays)
+    st = A.yk_stats()
+    gocc = gpu_device.trace_shadow(gpu_device.rays_to_device(rays), st).cpu().numpy()
+    assert (gocc == occ).all(), f"{(gocc != occ).sum()} mismatches"
+    assert 0 < occ.sum() < len(occ)
+    assert st.shadow_nodes == cnt[0] and st.shadow_tris == cnt[1]
