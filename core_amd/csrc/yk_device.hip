@@ -869,6 +869,41 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, const float* tb, co
   }
 }
 
+// Per-lane leaf test of the small-scene kernels (YK_SMALL_LANE_LEAF): each
+// lane runs its own leaf's references in the reference's order
+// (kdtree.cc:760-800 closest, 905-940 any-hit) from the LDS records. With
+// the 1-2 references per leaf of such trees this costs a wave max(nref)
+// tests instead of the cooperative round's scans and ray shuffles. Closest
+// hits keep (t, b1, b2, code) in cand[lane]: code = prim | 1 << 31 for a
+// single-reference leaf, else the leaf-list position (the prim id is read
+// from the leaf list once, when the ray finishes).
+template <bool CLOSEST, bool UNI>
+__device__ __forceinline__ void lane_leaves(const float* tb, const float* lb, Trav& st, uint32_t nref, uint32_t w0,
+                                            float4* cand, const float* s_tmin, unsigned& ntris, bool& occluded) {
+  if (nref == 0u) return;
+  const int lane = lane_fresh();
+  const float tmin = (CLOSEST || UNI) ? s_tmin[lane] : 0.f;
+  uint32_t i = 0;
+  for (; i < nref; ++i) {
+    const float* tp = (nref == 1u) ? tb + (size_t)w0 * 12u : lb + (size_t)(w0 + i) * 12u;
+    float4 A, E1, E2;
+    ld_tri<12u>(tp, A, E1, E2);
+    float th, u, v;
+    if (mt_intersect(V3(A.x, A.y, A.z), V3(E1.x, E1.y, E1.z), V3(E2.x, E2.y, E2.z), st.o, st.d, th, u, v)) {
+      if (CLOSEST) {
+        if (th < st.Z && th >= tmin) {
+          st.Z = th;
+          cand[lane] = make_float4(th, u, v, __uint_as_float(nref == 1u ? (w0 | 0x80000000u) : w0 + i));
+        }
+      } else if (th < st.dist && th >= tmin) {
+        occluded = true;
+        break;
+      }
+    }
+  }
+  ntris += (!CLOSEST && occluded) ? i + 1u : nref;
+}
+
 __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int src) {
   const unsigned lo = bperm((unsigned)v, src), hi = bperm((unsigned)(v >> 32), src);
   return ((unsigned long long)hi << 32) | lo;
@@ -903,14 +938,18 @@ struct RayCount {
 #ifndef YK_SMALL_RING
 #define YK_SMALL_RING 4  // their LDS stack ring depth (entries per lane)
 #endif
+#ifndef YK_SMALL_LANE_LEAF
+#define YK_SMALL_LANE_LEAF 1  // small-scene kernels test leaves per lane (lane_leaves), not cooperatively
+#endif
 #ifndef YK_SMALL_MAX
 #define YK_SMALL_MAX 16384  // largest LDS copy (bytes) that takes the small-scene kernels
 #endif
 extern __shared__ uint4 yk_dyn_lds[];
 template <bool CLOSEST, bool UNI, int R>
 struct WaveLds {
-  unsigned otab[64];
-  std::conditional_t<CLOSEST, unsigned long long, unsigned> keys[64];
+  // owner table and keys of the cooperative leaf test (unused by lane_leaves)
+  unsigned otab[YK_SMALL_LANE_LEAF ? 1 : 64];
+  std::conditional_t<CLOSEST, unsigned long long, unsigned> keys[YK_SMALL_LANE_LEAF ? 1 : 64];
   float s_tmin[(CLOSEST || UNI) ? 64 : 1];
   unsigned ray_n0[64];
   unsigned res_slot[CLOSEST ? 1 : 128];
@@ -1160,8 +1199,11 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       }
 #endif
       bool occ = false;
-      coop_leaves<CLOSEST, BIG, UNI, W>(S, tb, lb, st, (live && !paused) ? nref : 0u, w0, keys, cand, otab, s_tmin,
-                                         ntris, occ);
+      if constexpr (W > 1 && YK_SMALL_LANE_LEAF)
+        lane_leaves<CLOSEST, UNI>(tb, lb, st, (live && !paused) ? nref : 0u, w0, cand, s_tmin, ntris, occ);
+      else
+        coop_leaves<CLOSEST, BIG, UNI, W>(S, tb, lb, st, (live && !paused) ? nref : 0u, w0, keys, cand, otab, s_tmin,
+                                           ntris, occ);
 #ifdef YK_TRAV_STATS
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       {
@@ -1185,7 +1227,9 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
             yk_hit h{-1, 0.f, 0.f, 0.f};
             if (st.Z < st.dist && !err) {
               const float4 c = cand[lane_fresh()];
-              h = yk_hit{(int)__float_as_uint(c.w), c.x, c.y, c.z};
+              unsigned p = __float_as_uint(c.w);
+              if (W > 1 && YK_SMALL_LANE_LEAF) p = (p & 0x80000000u) ? p & 0x7FFFFFFFu : S.leaf[p];
+              h = yk_hit{(int)p, c.x, c.y, c.z};
             }
             hits[rid] = h;
           } else {
