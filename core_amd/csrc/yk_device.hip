@@ -743,6 +743,9 @@ __device__ __forceinline__ unsigned dpp_max_scan(unsigned x) {
   return x;
 }
 
+#ifndef YK_ANYHIT_SKIP
+#define YK_ANYHIT_SKIP 1
+#endif
 // Wave-uniform: every lane calls it; nref = 0 for lanes without a leaf to test.
 // BIG: trees with a leaf of 2^17 references or more (degenerate or heavily
 // overlapping geometry at maxDepth), whose absolute range starts overflow the
@@ -826,7 +829,11 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, const float* tb, co
     unsigned long long key = 0;
     float th = 0.f, u = 0.f, v = 0.f;
     uint32_t p = 0;
-    if (s < total) {
+    // any-hit, from the second round on: a pair whose owner already has a hit
+    // at a lower reference (an earlier round's atomic) is not tested -- the
+    // reference's leaf loop stopped there, and the owner's key is final
+    // (crowded leaves span many rounds: hair)
+    if (s < total && (CLOSEST || !YK_ANYHIT_SKIP || base == 0u || keys[own] > k)) {
       // one record: the leaf's own, in leaf order (a single-reference leaf's
       // from the prim array)
       const float* tp = (on == 1u) ? tb + (size_t)ow0 * TW : lb + (size_t)(ow0 + k) * TW;
