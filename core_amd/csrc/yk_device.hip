@@ -746,6 +746,9 @@ __device__ __forceinline__ unsigned dpp_max_scan(unsigned x) {
 #ifndef YK_ANYHIT_SKIP
 #define YK_ANYHIT_SKIP 1
 #endif
+#ifndef YK_ANYHIT_DYN
+#define YK_ANYHIT_DYN 1  // any-hit leaves of several rounds: rounds scheduled over the lanes not yet occluded
+#endif
 // Wave-uniform: every lane calls it; nref = 0 for lanes without a leaf to test.
 // BIG: trees with a leaf of 2^17 references or more (degenerate or heavily
 // overlapping geometry at maxDepth), whose absolute range starts overflow the
@@ -796,6 +799,67 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, const float* tb, co
   }
   wave_lds_sync<W>();
   const float zlim = CLOSEST ? st.Z : st.dist;
+  if constexpr (!CLOSEST && YK_ANYHIT_DYN) {
+    // Any-hit leaves of more than one round (crowded leaves: hair): the
+    // rounds are scheduled as they go -- each round hands its 64 slots to the
+    // next untested references of the lanes not yet occluded (a prefix scan
+    // of what they have left), so an occluded lane's remaining references
+    // take no slots at all. A lane's references are still tested in index
+    // order, and its key is the lowest hitting index: the reference's first
+    // hit and test count.
+    if (total > 64u) {
+      unsigned cons = 0u;  // references of this lane already tested
+      for (;;) {
+        const unsigned rem = (keys[lane] == ~0u) ? nref - cons : 0u;
+        unsigned y = rem;
+        y += (unsigned)__builtin_amdgcn_update_dpp(0, (int)y, 0x111, 0xf, 0xf, false);
+        y += (unsigned)__builtin_amdgcn_update_dpp(0, (int)y, 0x112, 0xf, 0xf, false);
+        y += (unsigned)__builtin_amdgcn_update_dpp(0, (int)y, 0x114, 0xf, 0xf, false);
+        y += (unsigned)__builtin_amdgcn_update_dpp(0, (int)y, 0x118, 0xf, 0xf, false);
+        y += (unsigned)__builtin_amdgcn_update_dpp(0, (int)y, 0x142, 0xa, 0xf, false);
+        y += (unsigned)__builtin_amdgcn_update_dpp(0, (int)y, 0x143, 0xc, 0xf, false);
+        const unsigned rpre = y - rem;
+        const unsigned rtot = (unsigned)__builtin_amdgcn_readlane((int)y, 63);
+        if (rtot == 0u) break;
+        otab[lane] = 0u;
+        if (rem > 0u && rpre < 64u) otab[rpre] = (rpre << 8) + (vconst<0x100u>() | (unsigned)lane);
+        wave_lds_sync<W>();
+        // slot 0 always starts a range (the first lane with references left)
+        const unsigned ov = dpp_max_scan(otab[lane]);
+        int own;
+        asm volatile("v_and_b32 %0, 0xff, %1" : "=v"(own) : "v"(ov));
+        const unsigned k = bperm(cons, own) + ((unsigned)lane - ((ov >> 8) - 1u));
+        const uint32_t ow0 = bperm(w0, own), on = bperm(nref, own);
+        const v3 ro = V3(bperm(st.o.x, own), bperm(st.o.y, own), bperm(st.o.z, own));
+        const v3 rd = V3(bperm(st.d.x, own), bperm(st.d.y, own), bperm(st.d.z, own));
+        const float rz = bperm(zlim, own);
+        const float rtmin = UNI ? s_tmin[own] : 0.f;
+        if ((unsigned)lane < rtot) {
+          const float* tp = (on == 1u) ? tb + (size_t)ow0 * TW : lb + (size_t)(ow0 + k) * TW;
+          float4 A, E1, E2;
+          ld_tri<TW>(tp, A, E1, E2);
+          asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
+                       "+v"(E2.y), "+v"(E2.z));
+          float th, u, v;
+          if (mt_intersect(V3(A.x, A.y, A.z), V3(E1.x, E1.y, E1.z), V3(E2.x, E2.y, E2.z), ro, rd, th, u, v) &&
+              th < rz && th >= rtmin)
+            atomicMin(&keys[own], k);
+        }
+        if (rem > 0u && rpre < 64u) cons += min(rem, 64u - rpre);
+        wave_lds_sync<W>();
+      }
+      if (nref > 0u) {
+        const unsigned kk = keys[lane];
+        if (kk != ~0u) {
+          occluded = true;
+          ntris += kk + 1u;
+        } else {
+          ntris += nref;
+        }
+      }
+      return;
+    }
+  }
   unsigned carry = 0u;  // ((start + 1) << 8 | lane) of the range covering the previous slot
   for (unsigned base = 0; base < total; base += 64u) {
     const unsigned s = base + (unsigned)lane;
