@@ -9,7 +9,9 @@ hook (in-range words, as a memory fault would leave them):
   so rays re-enter a subtree they already left (the per-ray bound, at most
   the tree's node count of visits, or the stack bound fires).
 
-A fresh upload restores the device."""
+A fresh upload restores the device. Every case runs on the HBM traversal
+kernels (a 40k-tri tree) and on the small-scene kernels, which trace from an
+LDS copy of the tree (a 625-node tree, forced onto them with YK_SMALL)."""
 import ctypes as C
 import time
 
@@ -22,16 +24,27 @@ from core_amd.scene import probe_scene
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True)
-def _hooks_on(monkeypatch):
+@pytest.fixture(autouse=True, params=["hbm", "small"])
+def kernels(request, monkeypatch):
     """the damage hook is test-only and off unless YK_DEBUG_HOOKS=1
-    (include/yk_test_hooks.h)"""
+    (include/yk_test_hooks.h); params: which traversal kernel family runs"""
     monkeypatch.setenv("YK_DEBUG_HOOKS", "1")
+    monkeypatch.setenv("YK_SMALL", "0" if request.param == "hbm" else "47104")
+    return request.param
 
 
-def _setup(gpu_device):
-    s, p = probe_scene("bumpy", 64, 48, 200, 101)
+_SCN = {}
+
+
+def _setup(gpu_device, kernels):
+    key = (200, 101) if kernels == "hbm" else (10, 7)
+    if key not in _SCN:
+        _SCN[key] = probe_scene("bumpy", 64, 48, *key)
+    s, p = _SCN[key]
     gpu_device.upload(s)
+    nb = C.c_int64(-1)
+    A.check(A.lib().yk_debug_small_scene(gpu_device._p, C.byref(nb)))
+    assert (nb.value > 0) == (kernels == "small")
     nodes, _ = gpu_device.export_tree()
     return s, p, nodes
 
@@ -83,8 +96,8 @@ def _restored(gpu_device, s):
 
 
 @pytest.mark.parametrize("target", ["root", "self"])
-def test_descent_cycle_errors(gpu_device, target):
-    s, p, nodes = _setup(gpu_device)
+def test_descent_cycle_errors(gpu_device, kernels, target):
+    s, p, nodes = _setup(gpu_device, kernels)
     assert _interior(nodes, 0) and _interior(nodes, 1)
     # node 1 (root's left child) and, for "self", also its right sibling chain
     for i in (0, 1):
@@ -95,12 +108,12 @@ def test_descent_cycle_errors(gpu_device, target):
     _restored(gpu_device, s)
 
 
-def test_pop_cycle_errors(gpu_device):
+def test_pop_cycle_errors(gpu_device, kernels):
     """Interior nodes whose right child is their grandparent: a ray that goes
     left there pushes the grandparent, reaches a leaf, pops back up and comes
     round again (a cycle through leaves and pops, caught by the per-ray
     node-visit bound); one that goes right loops inside a descent."""
-    s, p, nodes = _setup(gpu_device)
+    s, p, nodes = _setup(gpu_device, kernels)
     n = len(nodes)
     parent = np.full(n, -1, np.int64)
     for i in range(n):
@@ -118,11 +131,11 @@ def test_pop_cycle_errors(gpu_device):
     _restored(gpu_device, s)
 
 
-def test_shared_subtree_terminates(gpu_device):
+def test_shared_subtree_terminates(gpu_device, kernels):
     """A node's right child pointed at its sibling (a DAG, no cycle): the
     traversal is finite, so queries finish -- with an error or a result --
     and never hang."""
-    s, p, nodes = _setup(gpu_device)
+    s, p, nodes = _setup(gpu_device, kernels)
     n = len(nodes)
     for i in range(1, min(n, 4000)):
         if _interior(nodes, i) and _interior(nodes, i + 1):
@@ -138,8 +151,8 @@ def test_shared_subtree_terminates(gpu_device):
     _restored(gpu_device, s)
 
 
-def test_hook_refuses_out_of_range(gpu_device):
-    s, p, nodes = _setup(gpu_device)
+def test_hook_refuses_out_of_range(gpu_device, kernels):
+    s, p, nodes = _setup(gpu_device, kernels)
     n = len(nodes)
     for i, w0, w1 in ((n, 0, 0), (0, nodes[0, 0], (nodes[0, 1] & 3) | (n << 2))):
         rc = A.lib().yk_device_debug_set_node(gpu_device._p, i, int(w0), int(w1))
