@@ -1947,7 +1947,9 @@ __device__ __forceinline__ long long slot_of(const Batch& B, long long c, int k)
 // prim_hit flags
 enum : int { PH_HIT = 1, PH_DIFFUSE = 2, PH_LIGHT = 4 };
 // path state bits
-enum : int { PS_ALIVE = 1, PS_RESOLVE = 2, PS_CONT = 4, PS_EST = 8 };
+// (PS_EMIT: emit_b holds this bounce's emission; otherwise it is zero and
+// not stored. 256: clear of the final-gather bits, yk_photon.inc)
+enum : int { PS_ALIVE = 1, PS_RESOLVE = 2, PS_CONT = 4, PS_EST = 8, PS_EMIT = 256 };
 
 // Per-batch device state. Camera sample c owns K shadow slots k = 0..K-1:
 // doLightEstimation's i-th light sample is slot k0+i, its i-th BSDF (MIS)
@@ -2615,17 +2617,29 @@ __global__ void __launch_bounds__(YK_BOUNCE_BLOCK) YK_BOUNCE_ATTR k_shade_bounce
         if (R.nlights == 1) nr = gen_light(B, c, 0, 0, sp, pwo, s, B.soffs[c], 0u, traced);
         else nr = gen_light(B, c, 0, lnum, sp, pwo, s, B.soffs[c], (unsigned)lnum, traced);
         kend = c_lights[lnum].nslots;
-        B.lsel[c] = lnum;
+        if (R.nlights > 1) B.lsel[c] = lnum;  // one light: the resolve knows it is light 0
         ps |= PS_EST;
       }
+      // emission, stored only where the resolve adds it (a zero emission is
+      // not stored: adding +0 to the resolve's non-negative light sum is exact)
       c3 em = C3(0.f, 0.f, 0.f);
-      if (depth == 1 && (M.flags & BSDF_EMIT)) em = mat_emit(M, sp, pwo, false);
+      bool emits = false;
+      if (depth == 1 && (M.flags & BSDF_EMIT)) {
+        em = mat_emit(M, sp, pwo, false);
+        emits = true;
+      }
       // "matBSDFs & (BSDF_EMIT && caustic)" is matBSDFs & BSDF_SPECULAR when
       // the segment was caustic (pathtracer.cc:295); includeLights = caustic
-      if (R.spec && depth >= 2 && B.caus[c] && (M.flags & BSDF_SPECULAR)) em = mat_emit(M, sp, pwo, true);
-      B.emit_b[3 * c] = em.r;
-      B.emit_b[3 * c + 1] = em.g;
-      B.emit_b[3 * c + 2] = em.b;
+      if (R.spec && depth >= 2 && B.caus[c] && (M.flags & BSDF_SPECULAR)) {
+        em = mat_emit(M, sp, pwo, true);
+        emits = true;
+      }
+      if (emits) {
+        B.emit_b[3 * c] = em.r;
+        B.emit_b[3 * c + 1] = em.g;
+        B.emit_b[3 * c + 2] = em.b;
+        ps |= PS_EMIT;
+      }
       if (depth < R.bounces) {
         const float s1 = (float)scr_halton(4 * depth + 3, offs);
         const float s2 = (float)scr_halton(4 * depth + 4, offs);
@@ -2676,10 +2690,11 @@ __global__ void __launch_bounds__(256) k_resolve_bounce(Batch B, RenderConst R,
   if (!(ps & PS_RESOLVE)) return;
   c3 lcol = C3(0.f, 0.f, 0.f);
   if (ps & PS_EST) {
-    const int lnum = B.lsel[c];
+    const int lnum = R.nlights > 1 ? B.lsel[c] : 0;
     lcol = cscale((float)R.nlights, resolve_light(B, c, 0, lnum));
   }
-  if (depth == 1 || R.spec) lcol = cadd(lcol, C3(B.emit_b[3 * c], B.emit_b[3 * c + 1], B.emit_b[3 * c + 2]));
+  if ((depth == 1 || R.spec) && (ps & PS_EMIT))
+    lcol = cadd(lcol, C3(B.emit_b[3 * c], B.emit_b[3 * c + 1], B.emit_b[3 * c + 2]));
   const c3 thr = C3(B.thr[3 * c], B.thr[3 * c + 1], B.thr[3 * c + 2]);
   B.pathcol[3 * c] = B.pathcol[3 * c] + lcol.r * thr.r;
   B.pathcol[3 * c + 1] = B.pathcol[3 * c + 1] + lcol.g * thr.g;
