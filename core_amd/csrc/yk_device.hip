@@ -1594,6 +1594,14 @@ __device__ __forceinline__ c3 mat_eval(const DMat& M, const SurfPt& sp, v3 wo, v
 // shinyDiffuseMat_t::sample, shinydiffuse.cc:259-336; lightMat_t::sample
 // (simple.cc:55-60). ok=false: early return with W and wi untouched.
 // sflags = s.sampledFlags.
+// DIFF: every material of the scene is a light or a shinydiffuse with the one
+// component DIFFUSE|REFLECT (host check, diffuse_only()): the general
+// component loop below then matches that component alone, whatever the
+// caller's flags (every caller's mask holds DIFFUSE|REFLECT), so the
+// specialisation performs the same float operations on the same values --
+// sum = 0 + w, the normalisation by 1/sum, s1 / wp -- without the loop's
+// per-lane arrays (the shading kernels' registers).
+template <bool DIFF = false>
 __device__ __forceinline__ c3 mat_sample(const DMat& M, const SurfPt& sp, v3 wo, v3& wi, float s1in, float s2in,
                                          unsigned flags, float& pdf, float& W, bool& ok, unsigned& sflags) {
   ok = true;
@@ -1608,6 +1616,28 @@ __device__ __forceinline__ c3 mat_sample(const DMat& M, const SurfPt& sp, v3 wo,
   const float Kr = mat_fresnel(M, wo, N);
   float a[4];
   mat_accum(M, Kr, a);
+  if constexpr (DIFF) {
+    const int ci = M.cindex[0];
+    const float w0 = ci == 0 ? a[0] : (ci == 1 ? a[1] : (ci == 2 ? a[2] : a[3]));
+    float sum = 0.f;
+    sum += w0;
+    if ((double)sum < 0.00001) {
+      pdf = 0.f;
+      ok = false;
+      return C3(1.f, 1.f, 1.f);
+    }
+    const float inv_sum = 1.f / sum;
+    const float wp = w0 * inv_sum;
+    const float s1 = s1in / wp;
+    const v3 w = sample_cos_hemisphere(N, sp.NU, sp.NV, s1, s2in);
+    c3 sc = C3(0.f, 0.f, 0.f);
+    if (cos_Ng_wo * vdot(sp.Ng, w) > 0.f) sc = cscale(a[3], C3(M.col[0], M.col[1], M.col[2]));
+    pdf = fabsf(vdot(N, w)) * wp;
+    wi = w;
+    sflags = BSDF_DIFFUSE | BSDF_REFLECT;
+    W = fabsf(vdot(w, sp.N)) / (pdf * 0.99f + 0.01f);
+    return sc;
+  }
   float sum = 0.f, val[4], width[4];
   unsigned choice[4];
   int nMatch = 0;
@@ -1674,10 +1704,11 @@ __device__ __forceinline__ c3 mat_sample(const DMat& M, const SurfPt& sp, v3 wo,
   W = fabsf(vdot(w, sp.N)) / (pdf * 0.99f + 0.01f);
   return sc;
 }
+template <bool DIFF = false>
 __device__ __forceinline__ c3 mat_sample(const DMat& M, const SurfPt& sp, v3 wo, v3& wi, float s1in, float s2in,
                                          unsigned flags, float& pdf, float& W, bool& ok) {
   unsigned sf;
-  return mat_sample(M, sp, wo, wi, s1in, s2in, flags, pdf, W, ok, sf);
+  return mat_sample<DIFF>(M, sp, wo, wi, s1in, s2in, flags, pdf, W, ok, sf);
 }
 
 // shinyDiffuseMat_t::pdf, shinydiffuse.cc:338-377: every component sharing a
@@ -1870,7 +1901,14 @@ __device__ __forceinline__ bool dirac_illum(const DLight& L, v3 P, v3& ldir, flo
 #ifndef YK_BOUNCE_WAVES
 #define YK_BOUNCE_WAVES 5  // occupancy target of k_shade_bounce
 #endif
-#define YK_BOUNCE_ATTR __attribute__((amdgpu_waves_per_eu(YK_BOUNCE_WAVES)))
+// the diffuse-only instantiation (mat_sample<true>, fewer registers)
+#ifndef YK_BOUNCE_BLOCK_D
+#define YK_BOUNCE_BLOCK_D YK_BOUNCE_BLOCK
+#endif
+#ifndef YK_BOUNCE_WAVES_D
+#define YK_BOUNCE_WAVES_D YK_BOUNCE_WAVES
+#endif
+constexpr int bounce_block(bool diff) { return diff ? YK_BOUNCE_BLOCK_D : YK_BOUNCE_BLOCK; }
 #ifndef YK_APPEND_BLOCK
 #define YK_APPEND_BLOCK 512  // photon / final-gather kernels
 #endif
@@ -2206,6 +2244,7 @@ __device__ __forceinline__ int emit_shadow(const Batch& B, long long slot, const
 // at its isShadowed calls: every shadow ray it would trace is written to its
 // slot with the contribution it adds when unoccluded. Returns #rays; sets bit
 // k of `traced` (k < 64) for each slot that holds a ray.
+template <bool DIFF = false>
 __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, int li, const SurfPt& sp, v3 wo,
                                          unsigned pixelSample, unsigned soffs, unsigned loffs,
                                          unsigned long long& traced, const DMat* mats = c_mats) {
@@ -2294,9 +2333,9 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
     float W = 0.f, spdf = 0.f;
     bool ok;
     v3 bdir = V3(0.f, 0.f, 0.f);
-    const c3 surf = mat_sample(M, sp, wo, bdir, s1, s2,
-                               BSDF_GLOSSY | BSDF_DIFFUSE | BSDF_DISPERSIVE | BSDF_REFLECT | BSDF_TRANSMIT, spdf, W,
-                               ok);
+    const c3 surf = mat_sample<DIFF>(M, sp, wo, bdir, s1, s2,
+                                     BSDF_GLOSSY | BSDF_DIFFUSE | BSDF_DISPERSIVE | BSDF_REFLECT | BSDF_TRANSMIT, spdf,
+                                     W, ok);
     float bt, lightPdf;
     if (!(spdf > 1e-6f && light_hit(L, sp.P, bdir, bt, lightPdf))) {
       put_slot(B, slot, 0, black);
@@ -2341,6 +2380,7 @@ __device__ __forceinline__ void flush_shadow(const Batch& B, long long c, int ke
 
 // First segment of sub-path isub from a diffuse camera-ray hit: sample the
 // primary BSDF (pathtracer.cc:169-187). Returns the segment's ray.
+template <bool DIFF = false>
 __device__ __forceinline__ yk_ray path_first_segment(const Batch& B, const RenderConst& R, long long c,
                                                      const SurfPt& sp, const DMat& M, v3 dir, int isub) {
   const unsigned s = R.ps ? B.psample[c] : (unsigned)c % (unsigned)R.spp;
@@ -2350,7 +2390,7 @@ __device__ __forceinline__ yk_ray path_first_segment(const Batch& B, const Rende
   float pdf, W = B.wlast[c];
   bool ok;
   v3 pdir = V3(0.f, 0.f, 0.f);
-  c3 scol = mat_sample(M, sp, vneg(dir), pdir, s1, s2, BSDF_DIFFUSE | BSDF_REFLECT | BSDF_TRANSMIT, pdf, W, ok);
+  c3 scol = mat_sample<DIFF>(M, sp, vneg(dir), pdir, s1, s2, BSDF_DIFFUSE | BSDF_REFLECT | BSDF_TRANSMIT, pdf, W, ok);
   B.wlast[c] = W;
   scol = cscale(W, scol);
   B.thr[3 * c] = scol.r;
@@ -2366,6 +2406,7 @@ __device__ __forceinline__ yk_ray path_first_segment(const Batch& B, const Rende
 // first segment of sub-path 0 (appended to bounce queue 1).
 // Shading kernels run at the compiler's register choice (128 / 122 VGPRs, 4
 // waves per SIMD); forcing 5 or 6 spilled 124-200 B per lane and lost 2-4 %.
+template <bool DIFF>
 __global__ void __launch_bounds__(YK_PRIMARY_BLOCK) k_shade_primary(DScene S, Batch B, RenderConst R, long long nc,
                                                        unsigned long long* __restrict__ qword) {
   // The material records in LDS: per-lane reads of constant memory (the
@@ -2421,13 +2462,13 @@ __global__ void __launch_bounds__(YK_PRIMARY_BLOCK) k_shade_primary(DScene S, Ba
         const unsigned s = R.ps ? B.psample[c] : (unsigned)c % (unsigned)R.spp;
         int k0 = 0;
         for (int l = 0; l < R.nlights; ++l) {
-          nr += gen_light(B, c, k0, l, sp, wo, s, B.soffs[c], (unsigned)l, traced, s_mats);
+          nr += gen_light<DIFF>(B, c, k0, l, sp, wo, s, B.soffs[c], (unsigned)l, traced, s_mats);
           k0 += c_lights[l].nslots;
         }
         kend = k0;
         if (R.integrator == YK_INTEGRATOR_PATH) {
           B.wlast[c] = 0.f;
-          seg = path_first_segment(B, R, c, sp, M, dir, 0);
+          seg = path_first_segment<DIFF>(B, R, c, sp, M, dir, 0);
           emit = true;
           if (R.spec) {  // state.includeLights = false before the first segment's intersect
             B.incl[c] = 0;
@@ -2529,6 +2570,7 @@ __global__ void __launch_bounds__(256) k_resolve_primary(Batch B, RenderConst R,
 
 // First segment of sub-paths isub >= 1 (sub-path 0 is fused into
 // k_shade_primary).
+template <bool DIFF>
 __global__ void __launch_bounds__(YK_BOUNCE_BLOCK) k_path_start(DScene S, Batch B, RenderConst R, long long nc, int isub,
                                                     unsigned long long* __restrict__ qword) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2540,7 +2582,7 @@ __global__ void __launch_bounds__(YK_BOUNCE_BLOCK) k_path_start(DScene S, Batch 
     const yk_ray pr = B.p_rays[c];
     const v3 from = V3(pr.from[0], pr.from[1], pr.from[2]), dir = V3(pr.dir[0], pr.dir[1], pr.dir[2]);
     const SurfPt sp = make_surface(S, from, dir, h);
-    r = path_first_segment(B, R, c, sp, c_mats[sp.mat], dir, isub);
+    r = path_first_segment<DIFF>(B, R, c, sp, c_mats[sp.mat], dir, isub);
     emit = true;
     if (R.spec) {
       B.incl[c] = 0;
@@ -2559,7 +2601,9 @@ __global__ void __launch_bounds__(YK_BOUNCE_BLOCK) k_path_start(DScene S, Batch 
 // (pathtracer.cc:189-298): estimateOneDirectLight shadow rays, emission,
 // and the BSDF sample of the next segment. One thread per live path (entry
 // qi of the input bounce queue, owned by camera sample c).
-__global__ void __launch_bounds__(YK_BOUNCE_BLOCK) YK_BOUNCE_ATTR k_shade_bounce(DScene S, Batch B, RenderConst R,
+template <bool DIFF>
+__global__ void __launch_bounds__(bounce_block(DIFF))
+__attribute__((amdgpu_waves_per_eu(DIFF ? YK_BOUNCE_WAVES_D : YK_BOUNCE_WAVES))) k_shade_bounce(DScene S, Batch B, RenderConst R,
                                                       const unsigned long long* __restrict__ qin_word, int depth,
                                                       int isub, int qin, unsigned long long* __restrict__ qword) {
   const long long nq = (long long)(*qin_word >> 32);  // live paths (device-side count)
@@ -2584,7 +2628,7 @@ __global__ void __launch_bounds__(YK_BOUNCE_BLOCK) YK_BOUNCE_ATTR k_shade_bounce
       B.pstate[c] = 0;
     }
     int src;
-    valid = pack_block<YK_BOUNCE_BLOCK>(valid && prim >= 0, src);
+    valid = pack_block<bounce_block(DIFF)>(valid && prim >= 0, src);
     qi = qb + src;
   }
   const long long c = valid ? B.q_owner[qin][qi] : 0;
@@ -2614,8 +2658,8 @@ __global__ void __launch_bounds__(YK_BOUNCE_BLOCK) YK_BOUNCE_ATTR k_shade_bounce
         // compiler reads its record with scalar loads instead of per-lane
         // vector loads (which go through the texture path that limits this
         // kernel, PMC TD busy 0.9)
-        if (R.nlights == 1) nr = gen_light(B, c, 0, 0, sp, pwo, s, B.soffs[c], 0u, traced);
-        else nr = gen_light(B, c, 0, lnum, sp, pwo, s, B.soffs[c], (unsigned)lnum, traced);
+        if (R.nlights == 1) nr = gen_light<DIFF>(B, c, 0, 0, sp, pwo, s, B.soffs[c], 0u, traced);
+        else nr = gen_light<DIFF>(B, c, 0, lnum, sp, pwo, s, B.soffs[c], (unsigned)lnum, traced);
         kend = c_lights[lnum].nslots;
         if (R.nlights > 1) B.lsel[c] = lnum;  // one light: the resolve knows it is light 0
         ps |= PS_EST;
@@ -2647,7 +2691,7 @@ __global__ void __launch_bounds__(YK_BOUNCE_BLOCK) YK_BOUNCE_ATTR k_shade_bounce
         bool ok;
         v3 ndir = dir;  // pRay.dir keeps the previous direction if sample() returns early
         unsigned sfl;
-        c3 sc = mat_sample(M, sp, pwo, ndir, s1, s2, BSDF_ALL, pdf, W, ok, sfl);
+        c3 sc = mat_sample<DIFF>(M, sp, pwo, ndir, s1, s2, BSDF_ALL, pdf, W, ok, sfl);
         B.wlast[c] = W;
         sc = cscale(W, sc);
         if (!cblack(sc)) {
@@ -3342,6 +3386,7 @@ struct yk_device {
   DScene S{};
   int ntris = 0, max_depth = 0, nlights = 0, sum_light_slots = 0;
   bool spec = false;  // some material has SPECULAR|FILTER components: recursion pipeline
+  bool diff_only = false;  // every material a light or a one-component DIFFUSE|REFLECT shinydiffuse (mat_sample<true>)
   yk_abort_fn abort_fn = nullptr;  // yk_device_set_abort: polled between batches
   void* abort_user = nullptr;
   bool big_leaves = false;  // the resident tree has a leaf of 2^17 references or more: *_big kernels
@@ -4059,6 +4104,13 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
     d->mat_flags.push_back(m.bsdf_flags);
     if (m.bsdf_flags & (BSDF_SPECULAR | BSDF_FILTER)) d->spec = true;
   }
+  {  // the shading kernels' diffuse-only instantiation (mat_sample<true>); YK_DIFF=0 never
+    const char* e = std::getenv("YK_DIFF");
+    d->diff_only = !(e && std::atoi(e) == 0);
+    for (const DMat& m : mats)
+      if (!(m.type == YK_MAT_LIGHT || (m.ncomp == 1 && m.cflags[0] == (BSDF_DIFFUSE | BSDF_REFLECT))))
+        d->diff_only = false;
+  }
   std::vector<DLight> lights;
   int sum_slots = 0;
   for (size_t i = 0; i < S.light_states.size(); ++i) {
@@ -4602,14 +4654,14 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
         HIPCHK(hipMemsetAsync(d->spec_words.p, 0, d->spec_words.n * sizeof(unsigned long long), P.stream));
         launch = 0;
         trace(true, Bc.p_rays, nullptr, RayCount{nullptr, 0, n}, Bc.p_hits, nullptr);
-        hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(n, YK_PRIMARY_BLOCK)), dim3(YK_PRIMARY_BLOCK), 0, P.stream, d->S, Bc, Rc, n, qw(0, 0));
+        hipLaunchKernelGGL(d->diff_only ? k_shade_primary<true> : k_shade_primary<false>, dim3(grid_for(n, YK_PRIMARY_BLOCK)), dim3(YK_PRIMARY_BLOCK), 0, P.stream, d->S, Bc, Rc, n, qw(0, 0));
         HIPCHK(hipGetLastError());
         trace(false, Bc.s_rays, Bc.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, Bc.s_occl);
         hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(n)), dim3(256), 0, P.stream, Bc, Rc, n);
         HIPCHK(hipGetLastError());
         for (int isub = 0; isub < (path ? nsub : 0); ++isub) {
           if (isub > 0) {
-            hipLaunchKernelGGL(k_path_start, dim3(grid_for(n, YK_BOUNCE_BLOCK)), dim3(YK_BOUNCE_BLOCK), 0, P.stream, d->S, Bc, Rc, n, isub,
+            hipLaunchKernelGGL(d->diff_only ? k_path_start<true> : k_path_start<false>, dim3(grid_for(n, YK_BOUNCE_BLOCK)), dim3(YK_BOUNCE_BLOCK), 0, P.stream, d->S, Bc, Rc, n, isub,
                                qw(isub, 0));
             HIPCHK(hipGetLastError());
           }
@@ -4618,7 +4670,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
             const unsigned long long* in_w = qw(isub, depth - 1);
             unsigned long long* out_w = qw(isub, depth);
             trace(true, Bc.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, Bc.q_hits[qin], nullptr);
-            hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(n, YK_BOUNCE_BLOCK)), dim3(YK_BOUNCE_BLOCK), 0, P.stream, d->S, Bc, Rc, in_w, depth,
+            hipLaunchKernelGGL(d->diff_only ? k_shade_bounce<true> : k_shade_bounce<false>, dim3(grid_for(n, bounce_block(d->diff_only))), dim3(bounce_block(d->diff_only)), 0, P.stream, d->S, Bc, Rc, in_w, depth,
                                isub, qin, out_w);
             HIPCHK(hipGetLastError());
             trace(false, Bc.s_rays, Bc.s_idx, RayCount{out_w, 0, 0}, nullptr, Bc.s_occl);
@@ -4663,7 +4715,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     }
     if (!d->spec) {
     trace(true, B.p_rays, nullptr, RayCount{nullptr, 0, nc}, B.p_hits, nullptr);
-    hipLaunchKernelGGL(k_shade_primary, dim3(grid_for(nc, YK_PRIMARY_BLOCK)), dim3(YK_PRIMARY_BLOCK), 0, P.stream, d->S, B, R, nc, qw(0, 0));
+    hipLaunchKernelGGL(d->diff_only ? k_shade_primary<true> : k_shade_primary<false>, dim3(grid_for(nc, YK_PRIMARY_BLOCK)), dim3(YK_PRIMARY_BLOCK), 0, P.stream, d->S, B, R, nc, qw(0, 0));
     HIPCHK(hipGetLastError());
     trace(false, B.s_rays, B.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, B.s_occl);
     hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
@@ -4674,7 +4726,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     // accumulated in the reference's order (pathtracer.cc:164-298)
     for (int isub = 0; isub < (path ? nsub : 0); ++isub) {
       if (isub > 0) {  // sub-path 0's first segment came out of k_shade_primary
-        hipLaunchKernelGGL(k_path_start, dim3(grid_for(nc, YK_BOUNCE_BLOCK)), dim3(YK_BOUNCE_BLOCK), 0, P.stream, d->S, B, R, nc, isub,
+        hipLaunchKernelGGL(d->diff_only ? k_path_start<true> : k_path_start<false>, dim3(grid_for(nc, YK_BOUNCE_BLOCK)), dim3(YK_BOUNCE_BLOCK), 0, P.stream, d->S, B, R, nc, isub,
                            qw(isub, 0));
         HIPCHK(hipGetLastError());
       }
@@ -4683,7 +4735,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
         const unsigned long long* in_w = qw(isub, depth - 1);
         unsigned long long* out_w = qw(isub, depth);
         trace(true, B.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, B.q_hits[qin], nullptr);
-        hipLaunchKernelGGL(k_shade_bounce, dim3(grid_for(nc, YK_BOUNCE_BLOCK)), dim3(YK_BOUNCE_BLOCK), 0, P.stream, d->S, B, R, in_w, depth, isub,
+        hipLaunchKernelGGL(d->diff_only ? k_shade_bounce<true> : k_shade_bounce<false>, dim3(grid_for(nc, bounce_block(d->diff_only))), dim3(bounce_block(d->diff_only)), 0, P.stream, d->S, B, R, in_w, depth, isub,
                            qin, out_w);
         HIPCHK(hipGetLastError());
         trace(false, B.s_rays, B.s_idx, RayCount{out_w, 0, 0}, nullptr, B.s_occl);
