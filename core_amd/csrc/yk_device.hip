@@ -1595,12 +1595,12 @@ __device__ __forceinline__ c3 mat_eval(const DMat& M, const SurfPt& sp, v3 wo, v
 // (simple.cc:55-60). ok=false: early return with W and wi untouched.
 // sflags = s.sampledFlags.
 // DIFF: every material of the scene is a light or a shinydiffuse with the one
-// component DIFFUSE|REFLECT (host check, diffuse_only()): the general
-// component loop below then matches that component alone, whatever the
-// caller's flags (every caller's mask holds DIFFUSE|REFLECT), so the
-// specialisation performs the same float operations on the same values --
-// sum = 0 + w, the normalisation by 1/sum, s1 / wp -- without the loop's
-// per-lane arrays (the shading kernels' registers).
+// component DIFFUSE|REFLECT (host check at upload, yk_device::diffuse_only):
+// the general component loop below then matches that component alone, or
+// nothing when the caller's mask lacks it, so the specialisation performs the
+// same float operations on the same values -- sum = 0 + w, the normalisation
+// by 1/sum, s1 / wp -- without the loop's per-lane arrays (the shading
+// kernels' registers).
 template <bool DIFF = false>
 __device__ __forceinline__ c3 mat_sample(const DMat& M, const SurfPt& sp, v3 wo, v3& wi, float s1in, float s2in,
                                          unsigned flags, float& pdf, float& W, bool& ok, unsigned& sflags) {
@@ -1617,6 +1617,11 @@ __device__ __forceinline__ c3 mat_sample(const DMat& M, const SurfPt& sp, v3 wo,
   float a[4];
   mat_accum(M, Kr, a);
   if constexpr (DIFF) {
+    if ((flags & (BSDF_DIFFUSE | BSDF_REFLECT)) != (BSDF_DIFFUSE | BSDF_REFLECT)) {  // no component matches
+      pdf = 0.f;
+      ok = false;
+      return C3(1.f, 1.f, 1.f);
+    }
     const int ci = M.cindex[0];
     const float w0 = ci == 0 ? a[0] : (ci == 1 ? a[1] : (ci == 2 ? a[2] : a[3]));
     float sum = 0.f;
@@ -4602,7 +4607,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
       // final gathering (photonintegr.cc:637-790): gather path index outermost,
       // pathCol accumulated across paths in the reference's order
       for (int isub = 0; isub < (R.pm_fg ? nsub : 0); ++isub) {
-        hipLaunchKernelGGL(k_fg_start, dim3(grid_for(n, YK_APPEND_BLOCK)), dim3(YK_APPEND_BLOCK), 0, P.stream, d->S, Bc, Rc, n, isub, P.fgl.p,
+        hipLaunchKernelGGL(d->diff_only ? k_fg_start<true> : k_fg_start<false>, dim3(grid_for(n, YK_APPEND_BLOCK)), dim3(YK_APPEND_BLOCK), 0, P.stream, d->S, Bc, Rc, n, isub, P.fgl.p,
                            qw(isub, 0));
         HIPCHK(hipGetLastError());
         int qin = 1;
@@ -4611,7 +4616,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
           unsigned long long* out_w = qw(isub, it + 1);
           trace(true, Bc.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, Bc.q_hits[qin], nullptr);
           unsigned long long* lk_w = qw(isub, it) + qwords_per_batch;  // lookup-queue count
-          hipLaunchKernelGGL(k_fg_hit, dim3(grid_for(n, YK_APPEND_BLOCK)), dim3(YK_APPEND_BLOCK), 0,
+          hipLaunchKernelGGL(d->diff_only ? k_fg_hit<true> : k_fg_hit<false>, dim3(grid_for(n, YK_APPEND_BLOCK)), dim3(YK_APPEND_BLOCK), 0,
                              P.stream, d->S, Bc, Rc, PMC, in_w, it, isub, qin,
                              P.fgl.p, P.fglen.p, out_w, P.lkq.p, lk_w);
           HIPCHK(hipGetLastError());
