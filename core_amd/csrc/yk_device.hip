@@ -919,8 +919,12 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, const float* tb, co
     }
     if (CLOSEST) {
       wave_lds_sync<W>();
-      if (valid && keys[own] == key) {  // the winner reads its prim id (leaf list) once
-        p = (on == 1u) ? ow0 : S.leaf[ow0 + k];
+      // the winner keeps its prim as a code: prim | 1 << 31 for a
+      // single-reference leaf, else its leaf-list position, read when the
+      // ray finishes (a leaf-list load here put a dependent global load on
+      // every round that has a winner)
+      if (valid && keys[own] == key) {
+        p = (on == 1u) ? (ow0 | 0x80000000u) : ow0 + k;
         cand[own] = make_float4(th, u, v, __uint_as_float(p));
       }
     }
@@ -1299,7 +1303,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
             if (st.Z < st.dist && !err) {
               const float4 c = cand[lane_fresh()];
               unsigned p = __float_as_uint(c.w);
-              if (W > 1 && YK_SMALL_LANE_LEAF) p = (p & 0x80000000u) ? p & 0x7FFFFFFFu : S.leaf[p];
+              p = (p & 0x80000000u) ? p & 0x7FFFFFFFu : S.leaf[p];  // the prim code of coop_leaves / lane_leaves
               h = yk_hit{(int)p, c.x, c.y, c.z};
             }
             hits[rid] = h;
