@@ -195,6 +195,10 @@ __device__ __forceinline__ bool bound_cross(const float* bb, v3 from, v3 dir, v3
 #define YK_STACK_LDS 8
 #endif
 constexpr int kStackLds = YK_STACK_LDS;  // LDS ring depth per lane (16 measured slower: 1807 vs 2054, round 1)
+#ifndef YK_STACK_LDS_C
+#define YK_STACK_LDS_C YK_STACK_LDS
+#endif
+constexpr int kStackLdsC = YK_STACK_LDS_C;  // the closest-hit kernels' ring (any depth: not a power of two -> mod)
 // accumulator words per traversal kernel kind ({nodes, triangle tests, errors,
 // rays}; the YK_TRAV_STATS diagnostic build adds its cycle counters, ctr[4..12])
 #ifdef YK_TRAV_STATS
@@ -255,8 +259,10 @@ struct LaneStackT {
   __device__ __forceinline__ uint2* ovf_at(int k) const {
     return ovf + ((size_t)(wave * 64u + (unsigned)lane_fresh()) * depth + (unsigned)k);
   }
+  // ring slot of entry sp (R a power of two: a mask; else sp mod R)
+  static __device__ __forceinline__ int ring(int sp) { return (R & (R - 1)) == 0 ? (sp & (R - 1)) : (int)((unsigned)sp % (unsigned)R); }
   __device__ __forceinline__ void push(int sp, uint2 e) const {
-    uint2* slot = lds + (sp & (R - 1)) * 64 + lane_fresh();
+    uint2* slot = lds + ring(sp) * 64 + lane_fresh();
     if (sp >= R) {
       *ovf_at(sp - R) = *slot;
 #ifdef YK_TRAV_STATS
@@ -266,7 +272,7 @@ struct LaneStackT {
     *slot = e;
   }
   __device__ __forceinline__ uint2 pop(int sp) const {  // sp = index of the entry to pop
-    uint2* slot = lds + (sp & (R - 1)) * 64 + lane_fresh();
+    uint2* slot = lds + ring(sp) * 64 + lane_fresh();
     const uint2 e = *slot;
     if (sp >= R) *slot = *ovf_at(sp - R);
     return e;
@@ -1062,7 +1068,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
                                            uint2* __restrict__ ovf, int ovf_depth, int refill_min,
                                            float* __restrict__ tsf = nullptr, int ts_depth = 0) {
   using KeyT = std::conditional_t<CLOSEST, unsigned long long, unsigned>;
-  constexpr int R = W > 1 ? YK_SMALL_RING : kStackLds;
+  constexpr int R = W > 1 ? YK_SMALL_RING : (CLOSEST ? kStackLdsC : kStackLds);
   unsigned* otab;
   uint2* lds;
   float* s_tmin;    // the lanes' tmin, read by the cooperative leaf test
@@ -1079,7 +1085,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
     // LDS of the cooperative leaf test first: its owner table then sits at
     // offset 0, and its addresses need no base register
     __shared__ unsigned a_otab[64];
-    __shared__ uint2 a_lds[kStackLds * 64];
+    __shared__ uint2 a_lds[R * 64];
     __shared__ float a_tmin[(CLOSEST || UNI) ? 64 : 1];
     __shared__ unsigned a_res[(!CLOSEST && !TS) ? 128 : 1];
     __shared__ unsigned a_n0[64];
@@ -1432,10 +1438,10 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 // rays 2479 (5 waves, round 3) -> 2614 (6 waves) -> 2661 (7 waves) Mrays/s,
 // the centre crop at 64 spp (112 nodes per ray) 2086 -> 2455, headline
 // 2976 -> 3076 (6) -> 3114 (7); 8 waves (18 spills) fell to 1715 on the
-// microbenchmark. Closest-hit: the attribute asks for at least 5 waves; its
-// diet (80 VGPRs, 6.4 KB LDS per wave) lets it run 6 (round 3 measured a
-// forced 6 with spills at 2657 against 2835), with per-XCD ray segments (+12 %
-// from L2 locality). Any-hit per-XCD segments: 2700 / 2719 (round 2),
+// microbenchmark. Closest-hit: its diet (80 VGPRs, 6.4 KB LDS per wave) let
+// it run 6 (round 3 measured a forced 6 with spills at 2657 against 2835);
+// round 5 asks for 7 (72 VGPRs, one cold spill), which the LDS caps at 25
+// waves per CU (+1.4 % headline); per-XCD ray segments (+12 % from L2 locality). Any-hit per-XCD segments: 2700 / 2719 (round 2),
 // 2806 / 2800 (round 3), +0.3 % at 7 waves (round 4, YK_SHADOW_SEGS=8: under
 // the 2 % bar); non-temporal ray / result accesses 2775 against
 // 2824; resident grids below the occupancy limit lost 2-4 %. PMC (round 3):
@@ -1448,7 +1454,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 #define YK_SHADOW_SEGS 8
 #endif
 #ifndef YK_CLOSEST_WAVES
-#define YK_CLOSEST_WAVES 5
+#define YK_CLOSEST_WAVES 7  // round 5: 72 VGPRs (1 spilled on a cold path); its 6.4 KB of LDS per wave then allow 25 waves per CU (24 at 76 VGPRs)
 #endif
 #ifndef YK_SHADOW_WAVES
 #define YK_SHADOW_WAVES 7
@@ -3786,7 +3792,7 @@ void enqueue_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* id
   const int waves = small ? YK_SMALL_W : 1;  // per workgroup
   const long long per_cu = small ? d->per_cu_small[(!CLOSEST && d->S.uni) ? 2 : (int)CLOSEST] : d->big_leaves ? d->per_cu_big[CLOSEST] : d->per_cu[CLOSEST];
   const long long grid = (long long)d->cus * per_cu;
-  const int ovf_depth = std::max(1, stack_depth(d) - (small ? YK_SMALL_RING : kStackLds));
+  const int ovf_depth = std::max(1, stack_depth(d) - (small ? YK_SMALL_RING : (CLOSEST ? kStackLdsC : kStackLds)));
   P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64 * waves);
   if (ev0) HIPCHK(hipEventRecord(ev0, P.stream));
   auto kern = small ? (CLOSEST ? k_trace_closest_small : d->S.uni ? k_trace_shadow_uni_small : k_trace_shadow_small)
