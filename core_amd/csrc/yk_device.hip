@@ -2248,9 +2248,7 @@ __device__ __forceinline__ void put_aux(const Batch& B, long long slot, float a,
 // `traced`, one queued ray
 __device__ __forceinline__ int emit_shadow(const Batch& B, long long slot, const yk_ray& sr, int kbit,
                                            unsigned long long& traced) {
-#ifndef YK_EXP_NO_SRAY  // experiment only: how much of the shading time the shadow-ray stores take
   st_ray(&B.s_rays[slot], sr);
-#endif
   if (kbit < 64) traced |= 1ull << kbit;
   return 1;
 }
