@@ -213,6 +213,20 @@ def test_small_scene_kernels(gpu_device, monkeypatch, case, small):
     assert (sums_g.view(np.uint32) == sums_o.view(np.uint32)).all()
 
 
+@pytest.mark.parametrize("diff", ["0", "1"])
+@pytest.mark.parametrize("case", [("cornell_pt", 64, 64, 0, 0), ("cornell_dl", 64, 64, 0, 0)], ids=["pt", "dl"])
+def test_shading_instantiations(gpu_device, monkeypatch, case, diff):
+    """The diffuse-only shading instantiation (mat_sample<true>, chosen at
+    upload when every material is a light or a one-component diffuse
+    shinydiffuse) and the general one (YK_DIFF=0) on the same scene: both
+    equal the oracle bit for bit, ray counts included."""
+    monkeypatch.setenv("YK_DIFF", diff)
+    sums_o, sums_g, rgba_o, rgba_g, cnt, st = _render_pair(gpu_device, case, (0, 0, 64, 64))
+    assert st.closest_rays == cnt["closest"] and st.shadow_rays == cnt["shadow"]
+    assert (sums_g.view(np.uint32) == sums_o.view(np.uint32)).all()
+    assert (rgba_g.view(np.uint32) == rgba_o.view(np.uint32)).all()
+
+
 def test_render_sharded_sum(gpu_device):
     """Tile sharding (tile t -> shard t % n): per-shard films summed equal the
     1-shard film within float reassociation, and rays split exactly."""
