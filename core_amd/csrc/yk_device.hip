@@ -990,7 +990,8 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
   return ((unsigned long long)hi << 32) | lo;
 }
 
-// Persistent ray-query kernel. One 64-lane wave per workgroup; each lane owns
+// Persistent ray-query kernel. One 64-lane wave per workgroup (W waves for
+// the small-scene kernels, which share an LDS copy of the scene); each lane owns
 // one ray at a time and advances it one leaf visit per loop iteration. Lanes
 // whose ray finished are refilled from a global work counter in bulk
 // (__ballot + one atomicAdd per wave + mbcnt-style ranks), so the wave stays
