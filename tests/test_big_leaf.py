@@ -102,3 +102,46 @@ def test_big_leaf_render_bit_exact(gpu_device):
     st = gpu_device.render_shard(p, film)
     assert st.closest_rays == cnt_o["closest"] and st.shadow_rays == cnt_o["shadow"]
     assert (film.cpu().numpy().view(np.uint32) == sums_o.view(np.uint32)).all()
+
+
+N_CROWD = 200  # 600 references in one leaf: many cooperative rounds, below the BIG limit
+
+
+def crowded_scene(mode):
+    s = Scene()
+    p = s.generate("cornell_pt", 24, 24)
+    tri = np.array([[-0.3, 0.5, 0.1], [0.3, 0.5, 0.1], [0.0, 1.1, 0.1],
+                    [-0.3, 0.6, 0.0], [0.3, 0.6, 0.2], [0.0, 1.0, 0.15],
+                    [-0.25, 0.55, 0.3], [0.32, 0.7, -0.1], [0.05, 1.05, 0.05]], np.float32)
+    faces = np.tile(np.array([[0, 1, 2], [3, 4, 5], [6, 7, 8]], np.int32), (N_CROWD, 1))
+    mid = s.add_mesh(tri, faces, 0)
+    if mode == A.YK_MODE_UNIVERSAL:
+        s.set_mode(mode)
+        for oid in range(1, mid + 1):
+            s.set_mesh_type(oid, A.YK_MESH_VTRIM)
+    s.build()
+    return s
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [A.YK_MODE_TRIANGLE, A.YK_MODE_UNIVERSAL], ids=["triangle", "universal"])
+def test_crowded_leaf_any_hit_rounds(gpu_device, mode):
+    """A 600-reference leaf: the any-hit test schedules its rounds over the
+    lanes not yet occluded and skips the pairs of decided owners
+    (coop_leaves, YK_ANYHIT_DYN / YK_ANYHIT_SKIP); occlusion and the
+    reference's test counts (first hit index + 1) stay exact, in both tree
+    modes (universal: t > tmin)."""
+    from oracle.oracle import Oracle
+    s = crowded_scene(mode)
+    assert _largest_leaf(s) >= 3 * N_CROWD
+    orc = Oracle(s)
+    sh = _rays(s, seed=9)
+    sh[:, 6] = 0.0005
+    sh[::2, 7] = np.abs(sh[::2, 7]) + 0.5
+    occ, cnt = orc.shadow(sh)
+    gpu_device.upload(s)
+    st = A.yk_stats()
+    gocc = gpu_device.trace_shadow(gpu_device.rays_to_device(sh), st).cpu().numpy()
+    assert (gocc == occ).all(), f"{(gocc != occ).sum()} mismatches"
+    assert 0 < occ.sum() < len(occ)
+    assert st.shadow_nodes == cnt[0] and st.shadow_tris == cnt[1]
