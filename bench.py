@@ -8,6 +8,10 @@ RCCL (torch.distributed "nccl") and rank 0 normalises the frame
 (yk_film_resolve). Total work is fixed as N grows ("scaling": "strong").
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
+
+Under torch.distributed.run every process is one rank. Started directly with
+--gpus N > 1, bench.py starts the N rank processes itself (launch_ranks)
+before it touches a GPU, and exits non-zero if any of them fails.
 """
 import argparse
 import ctypes as C
@@ -71,21 +75,36 @@ def main():
                     help="batch pipelines of the timed frames (default: libyk's 4; 1 serialises the kernels)")
     ap.add_argument("--no-roofline-frame", action="store_true",
                     help="skip the extra serialised frame the roofline line is measured on")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="film-reduce backend for N > 1: nccl (RCCL over xGMI, one GPU per rank) or gloo (host "
+                         "copies; lets N ranks share one GPU, for tests)")
     args = ap.parse_args()
     if args.pipes:
         os.environ["YK_PIPES"] = str(args.pipes)
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start the N rank processes here, before this process
+        # touches the GPU (torch is imported, no device call made yet)
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    fail = os.environ.get("YK_BENCH_FAIL_RANK")  # test hook: this rank exits at once (launcher failure path)
+    if fail is not None and int(fail) == rank:
+        raise SystemExit(3)
     dist = None
+    gloo = args.backend == "gloo"
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # ranks beyond the visible GPUs share them (gloo test runs on one GPU)
+        local = local % max(1, torch.cuda.device_count())
 
     t_build = time.perf_counter()
     if rank == 0:
@@ -125,7 +144,13 @@ def main():
             if ev is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-            dist.reduce(film, dst=0)
+            if gloo:  # gloo reduces host tensors: device -> host, reduce, host -> device
+                h = film.cpu()
+                dist.reduce(h, dst=0)
+                if rank == 0:
+                    film.copy_(h)
+            else:
+                dist.reduce(film, dst=0)
             if ev is not None:
                 e1.record()
                 ev.append((e0, e1))
@@ -153,6 +178,8 @@ def main():
     kern = torch.tensor([st.ms_closest, st.ms_shadow], dtype=torch.float64, device="cuda")
     tmax = torch.tensor([elapsed, ms_reduce], dtype=torch.float64, device="cuda")
     if dist is not None:
+        if gloo:
+            work, kern, tmax = work.cpu(), kern.cpu(), tmax.cpu()
         dist.all_reduce(work)
         dist.all_reduce(kern)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -318,14 +345,65 @@ def roofline_line(args, w, ms_c, ms_s, rst, elapsed, pt, small=0):
     out["hbm"] = {"peak": HBM_PEAK_GBS, "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4)}
     out["l2"] = {"peak": L2_PEAK_GBS, "frac": round(dom["gbs"] / L2_PEAK_GBS, 4)}
     if small:
+        note = "algorithmic bytes: the node / record bytes among them are LDS reads here, not HBM or L2 traffic"
+        out["hbm"]["note"] = note
+        out["l2"]["note"] = note
         out["lds"] = {"peak": LDS_PEAK_GBS, "frac": round(dom["gbs"] / LDS_PEAK_GBS, 4), "scene_copy_bytes": small,
                       "note": "traversal data (node packets, triangle records) copied to LDS once per 4-wave "
                               "workgroup: the per-node / per-test bytes are LDS reads, only rays and results "
                               "cross HBM"}
     # all traversal bytes of the timed frames over their wall time
     out["traversal_achieved_wall"] = round((algorithmic_bytes(w[0], w[2], w[3], 16) +
-                                            algorithmic_bytes(w[1], w[4], w[5], 1)) / elapsed / 1e9, 2)
+                                            algorithmic_bytes(w[1], w[4], w[5], 4)) / elapsed / 1e9, 2)
     return out
+
+
+def launch_ranks(n):
+    """Start N rank processes of this same command line (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR / MASTER_PORT set, as torch.distributed.run sets
+    them) and wait for them. Rank 0 prints the JSON line to the inherited
+    stdout. Returns 0 when every rank exits 0; when one fails, the others are
+    terminated and its exit code is returned. The multi-GPU split this drives
+    replaces the reference's render thread pool (integrator.cc:177-211)."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+
+    def stop(*_):
+        for q in procs:
+            if q.poll() is None:
+                q.terminate()
+        for q in procs:
+            try:
+                q.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                q.kill()
+                q.wait()
+
+    signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+    rc = 0
+    live = list(procs)
+    while live:
+        for q in list(live):
+            code = q.poll()
+            if code is None:
+                continue
+            live.remove(q)
+            if code != 0:
+                print(f"[bench] rank {procs.index(q)} exited with {code}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                stop()
+                return code if code > 0 else 128 - code
+        time.sleep(0.2)
+    return rc
 
 
 def host_threads():

@@ -204,6 +204,7 @@ SIGNATURES = {
     "yk_device_debug_set_node": (C.c_int, [P, i64, C.c_uint32, C.c_uint32]),
     "yk_debug_qmc_probe": (C.c_int, [P, C.c_int32, P, P, i64, P]),
     "yk_debug_small_scene": (C.c_int, [P, C.POINTER(i64)]),
+    "yk_debug_shading_kind": (C.c_int, [P, C.POINTER(C.c_int32)]),
 }
 
 _lib = None

@@ -47,6 +47,13 @@ int yk_debug_qmc_probe(yk_device* d, int32_t fn, const void* in, const uint32_t*
  * they read them from HBM. YK_ERR_UNSUPPORTED unless YK_DEBUG_HOOKS=1. */
 int yk_debug_small_scene(yk_device* d, int64_t* bytes);
 
+/* Which shading instantiation the resident scene takes: *diff_only = 1 when
+ * the shading and final-gather kernels run the diffuse-only specialisation
+ * (mat_sample<true>: every material a light or a one-component diffuse
+ * shinydiffuse, and YK_DIFF != 0 at upload), 0 for the general component
+ * loop. YK_ERR_UNSUPPORTED unless YK_DEBUG_HOOKS=1. */
+int yk_debug_shading_kind(yk_device* d, int32_t* diff_only);
+
 #ifdef __cplusplus
 }
 #endif

@@ -222,9 +222,41 @@ def test_shading_instantiations(gpu_device, monkeypatch, case, diff):
     equal the oracle bit for bit, ray counts included."""
     monkeypatch.setenv("YK_DIFF", diff)
     sums_o, sums_g, rgba_o, rgba_g, cnt, st = _render_pair(gpu_device, case, (0, 0, 64, 64))
+    assert _diff_only(gpu_device, monkeypatch) == int(diff)  # the instantiation under test ran
     assert st.closest_rays == cnt["closest"] and st.shadow_rays == cnt["shadow"]
     assert (sums_g.view(np.uint32) == sums_o.view(np.uint32)).all()
     assert (rgba_g.view(np.uint32) == rgba_o.view(np.uint32)).all()
+
+
+def _diff_only(gpu_device, monkeypatch):
+    import ctypes as C
+    monkeypatch.setenv("YK_DEBUG_HOOKS", "1")
+    k = C.c_int32(-1)
+    A.check(A.lib().yk_debug_shading_kind(gpu_device._p, C.byref(k)))
+    return k.value
+
+
+@pytest.mark.parametrize("diff", ["0", "1"])
+def test_shading_instantiations_photon(gpu_device, monkeypatch, diff):
+    """The same for photon mapping's final gather (k_fg_start / k_fg_hit take
+    the diffuse-only specialisation too): maps and film bit-exact."""
+    monkeypatch.setenv("YK_DIFF", diff)
+    s, p, orc = scene("cornell_pt", 48, 48)
+    q = A.yk_render_params.from_buffer_copy(p)
+    q.integrator = A.YK_INTEGRATOR_PHOTON
+    q.photon.photons = 4000
+    q.photon.fg_samples = 3
+    q.aa_samples = 2
+    gpu_device.upload(s)
+    assert _diff_only(gpu_device, monkeypatch) == int(diff)
+    info_o = orc.photon_build(q)
+    info = gpu_device.photon_build(q)
+    assert info.diffuse_photons == info_o["diffuse_photons"]
+    film = gpu_device.new_film(q)
+    st = gpu_device.render_shard(q, film)
+    _, sums_o, cnt = orc.render(q)
+    assert st.closest_rays == cnt["closest"] and st.shadow_rays == cnt["shadow"]
+    assert (film.cpu().numpy().view(np.uint32) == sums_o.view(np.uint32)).all()
 
 
 def test_render_sharded_sum(gpu_device):
