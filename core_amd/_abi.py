@@ -30,12 +30,15 @@ YK_MESH_TRIM, YK_MESH_VTRIM = 0, 1
 f3 = C.c_float * 3
 
 
+YK_BRDF_LAMBERT, YK_BRDF_OREN_NAYAR = 0, 1
+
+
 class yk_material(C.Structure):
     _fields_ = [("type", C.c_int32), ("color", f3), ("diffuse_reflect", C.c_float),
                 ("emit", C.c_float), ("power", C.c_float), ("double_sided", C.c_int32),
                 ("mirror_color", f3), ("specular_reflect", C.c_float), ("transparency", C.c_float),
                 ("translucency", C.c_float), ("transmit_filter", C.c_float), ("fresnel_effect", C.c_int32),
-                ("ior", C.c_double)]
+                ("ior", C.c_double), ("diffuse_brdf", C.c_int32), ("sigma", C.c_double)]
 
 
 class yk_light(C.Structure):
@@ -56,7 +59,8 @@ class yk_material_state(C.Structure):
                 ("diffuse_strength", C.c_float), ("emit_color", f3), ("double_sided", C.c_int32),
                 ("mirror_color", f3), ("component", C.c_float * 4), ("ncomp", C.c_int32),
                 ("comp_flags", C.c_uint32 * 4), ("comp_index", C.c_int32 * 4), ("transmit_filter", C.c_float),
-                ("has_fresnel", C.c_int32), ("ior_squared", C.c_float)]
+                ("has_fresnel", C.c_int32), ("ior_squared", C.c_float), ("oren_nayar", C.c_int32),
+                ("oren_nayar_a", C.c_float), ("oren_nayar_b", C.c_float)]
 
 
 class yk_area_light_state(C.Structure):

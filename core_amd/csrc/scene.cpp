@@ -83,6 +83,12 @@ yk_material_state material_state(const yk_material& m) {
     }
     if (m.diffuse_reflect * acc > 0.00001f) add(kDiffuse | kReflect, 3, m.diffuse_reflect);
     o.ncomp = n;
+    if (m.diffuse_brdf == YK_BRDF_OREN_NAYAR) {  // factory -> initOrenNayar(sigma), shinydiffuse.cc:170-176,505-514
+      const double s2 = m.sigma * m.sigma;
+      o.oren_nayar = 1;
+      o.oren_nayar_a = (float)(1.0 - 0.5 * (s2 / (s2 + 0.33)));
+      o.oren_nayar_b = (float)(0.45 * s2 / (s2 + 0.09));
+    }
   }
   return o;
 }

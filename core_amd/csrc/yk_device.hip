@@ -63,6 +63,8 @@ struct DMat {
   int fresnel;        // mHasFresnelEffect
   float ior2;         // mIOR_Squared
   int translucent;    // mIsTranslucent
+  int on;             // mUseOrenNayar (shinydiffuse.cc:170-176)
+  float on_a, on_b;   // mOrenNayar_A / mOrenNayar_B
 };
 
 struct DLight {  // areaLight_t members after its constructor (arealight.cc:30-49)
@@ -1591,8 +1593,37 @@ __device__ __forceinline__ void mat_accum(const DMat& M, float Kr, float* a) {
   a[3] = ((1.f - M.comp[2]) * M.comp[3]) * acc2;
 }
 
+// shinyDiffuseMat_t::OrenNayar, shinydiffuse.cc:185-220, in source order
+// (parity unpinned: no reference output has an Oren-Nayar material).
+// std::min(1.f, x) / std::max(1e-8f, x) as the ternaries <algorithm> defines
+// (a NaN dot product gives 1 then), fSqrt = sqrtf, normalize() as vector3d.h.
+__device__ __forceinline__ float oren_nayar(const DMat& M, v3 wi, v3 wo, v3 N) {
+  const float di = vdot(N, wi), dO = vdot(N, wo);
+  const float mi = (di < 1.f) ? di : 1.f, mo = (dO < 1.f) ? dO : 1.f;
+  const float cos_ti = (1e-8f < mi) ? mi : 1e-8f, cos_to = (1e-8f < mo) ? mo : 1e-8f;
+  float maxcos_f = 0.f;
+  if (cos_ti < 0.9999f && cos_to < 0.9999f) {
+    const v3 v1 = vnormalize(vsub(wi, vmul(cos_ti, N)));
+    const v3 v2 = vnormalize(vsub(wo, vmul(cos_to, N)));
+    const float d = vdot(v1, v2);
+    maxcos_f = (0.f < d) ? d : 0.f;
+  }
+  float sin_alpha, tan_beta;
+  if (cos_to >= cos_ti) {
+    sin_alpha = sqrtf(1.f - cos_ti * cos_ti);
+    tan_beta = sqrtf(1.f - cos_to * cos_to) / cos_to;
+  } else {
+    sin_alpha = sqrtf(1.f - cos_to * cos_to);
+    tan_beta = sqrtf(1.f - cos_ti * cos_ti) / cos_ti;
+  }
+  return M.on_a + ((M.on_b * maxcos_f) * sin_alpha) * tan_beta;
+}
+
 // shinyDiffuseMat_t::eval, shinydiffuse.cc:223-249 (compiled: cos_Ng_wl as
-// (y + z) + x; mD = ((1-c2)*c3)*mT)
+// (y + z) + x; mD = ((1-c2)*c3)*mT), then mD *= OrenNayar(wo, wl, N) (:247).
+// ON = false: the scene has no Oren-Nayar material (the diffuse-only
+// instantiation's scenes), so the factor's code is not compiled in.
+template <bool ON = true>
 __device__ __forceinline__ c3 mat_eval(const DMat& M, const SurfPt& sp, v3 wo, v3 wl) {
   if (M.type == YK_MAT_LIGHT) return C3(0.f, 0.f, 0.f);
   const float cos_Ng_wo = vdot(sp.Ng, wo);
@@ -1603,7 +1634,10 @@ __device__ __forceinline__ c3 mat_eval(const DMat& M, const SurfPt& sp, v3 wo, v
   const float mT = (1.f - Kr * M.comp[0]) * (1.f - M.comp[1]);
   if (cos_Ng_wo * cos_Ng_wl < 0.f && M.translucent) return cscale(mT * M.comp[2], C3(M.col[0], M.col[1], M.col[2]));
   if (vdot(wl, N) < 0.0f) return C3(0.f, 0.f, 0.f);
-  const float mD = ((1.f - M.comp[2]) * M.comp[3]) * mT;
+  float mD = ((1.f - M.comp[2]) * M.comp[3]) * mT;
+  if constexpr (ON) {
+    if (M.on) mD *= oren_nayar(M, wo, wl, N);
+  }
   return cscale(mD, C3(M.col[0], M.col[1], M.col[2]));
 }
 
@@ -1718,6 +1752,7 @@ __device__ __forceinline__ c3 mat_sample(const DMat& M, const SurfPt& sp, v3 wo,
   } else {
     w = sample_cos_hemisphere(N, sp.NU, sp.NV, s1, s2in);
     if (cos_Ng_wo * vdot(sp.Ng, w) > 0.f) sc = cscale(a[3], dcol);
+    if (M.on) sc = cscale(oren_nayar(M, wo, w, N), sc);  // scolor *= OrenNayar(wo, wi, N), :330
     pdf = fabsf(vdot(N, w)) * wp;
   }
   wi = w;
@@ -2295,7 +2330,7 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
       put_ray(sr, sp.P, ldir, YK_SHADOW_BIAS, ltmax);
       nq = emit_shadow(B, slot, sr, k0, traced);
     }
-    const c3 surf = mat_eval(M, sp, wo, ldir);
+    const c3 surf = mat_eval<!DIFF>(M, sp, wo, ldir);
     const float f = fabsf(vdot(sp.N, ldir));
     if (B.ts) {  // lcol *= scol first (mcintegrator.cc:94): keep the parts
       put_slot(B, slot, SL_TRACED | SL_ADDS, surf);
@@ -2334,7 +2369,7 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
       put_slot(B, slot, SL_TRACED, black);
       continue;
     }
-    const c3 surf = mat_eval(M, sp, wo, ldir);
+    const c3 surf = mat_eval<!DIFF>(M, sp, wo, ldir);
     const float mPdf = mat_pdf(M, sp, wo, ldir);
     // compiled form: ((surf*lcol) * (|N.l| * (1/pdf))) [* w]
     const float k = fabsf(vdot(sp.N, ldir)) * (1.0f / lpdf);
@@ -3696,6 +3731,9 @@ DMat make_mat(const yk_material_state& m) {
   M.tfilter = m.transmit_filter;
   M.fresnel = m.has_fresnel;
   M.ior2 = m.ior_squared;
+  M.on = m.oren_nayar ? 1 : 0;
+  M.on_a = m.oren_nayar_a;
+  M.on_b = m.oren_nayar_b;
   return M;
 }
 
@@ -4161,7 +4199,7 @@ int yk_device_upload(yk_device* d, const yk_scene* s) {
     const char* e = std::getenv("YK_DIFF");
     d->diff_only = !(e && std::atoi(e) == 0);
     for (const DMat& m : mats)
-      if (!(m.type == YK_MAT_LIGHT || (m.ncomp == 1 && m.cflags[0] == (BSDF_DIFFUSE | BSDF_REFLECT))))
+      if (!(m.type == YK_MAT_LIGHT || (m.ncomp == 1 && m.cflags[0] == (BSDF_DIFFUSE | BSDF_REFLECT) && !m.on)))
         d->diff_only = false;
   }
   std::vector<DLight> lights;

@@ -52,6 +52,8 @@ int yk_scene_add_material(yk_scene* s, const yk_material* m, int32_t* id_out) {
   if (!s || !m) return set_error(YK_ERR_ARG, "yk_scene_add_material: NULL argument");
   if (m->type != YK_MAT_SHINYDIFFUSE && m->type != YK_MAT_LIGHT)
     return set_error(YK_ERR_UNSUPPORTED, "material type not supported by the GPU path");
+  if (m->diffuse_brdf != YK_BRDF_LAMBERT && m->diffuse_brdf != YK_BRDF_OREN_NAYAR)
+    return set_error(YK_ERR_ARG, "yk_scene_add_material: diffuse_brdf must be YK_BRDF_LAMBERT or YK_BRDF_OREN_NAYAR");
   YK_GUARD_BEGIN
   const int id = s->s.add_material(*m);
   if (id_out) *id_out = id;
@@ -63,6 +65,8 @@ int yk_scene_add_material_state(yk_scene* s, const yk_material_state* m, int32_t
   if (!s || !m) return set_error(YK_ERR_ARG, "yk_scene_add_material_state: NULL argument");
   if (m->type != YK_MAT_SHINYDIFFUSE && m->type != YK_MAT_LIGHT)
     return set_error(YK_ERR_UNSUPPORTED, "material type not supported by the GPU path");
+  if (m->oren_nayar != 0 && m->oren_nayar != 1)
+    return set_error(YK_ERR_ARG, "yk_scene_add_material_state: oren_nayar must be 0 or 1");
   YK_GUARD_BEGIN
   const int id = s->s.add_material_state(*m);
   if (id_out) *id_out = id;

@@ -33,12 +33,15 @@ class Scene:
     # -- assembly ------------------------------------------------------
     def add_material(self, type_=A.YK_MAT_SHINYDIFFUSE, color=(1, 1, 1), diffuse_reflect=1.0, emit=0.0,
                      power=1.0, double_sided=False, mirror_color=(1, 1, 1), specular_reflect=0.0,
-                     transparency=0.0, translucency=0.0, transmit_filter=1.0, fresnel_effect=False, ior=1.33):
+                     transparency=0.0, translucency=0.0, transmit_filter=1.0, fresnel_effect=False, ior=1.33,
+                     diffuse_brdf="lambert", sigma=0.1):
         """shinydiffusemat / light_mat parameters with the reference factory defaults
-        (shinydiffuse.cc:474-503, simple.cc:80-90)."""
+        (shinydiffuse.cc:474-514, simple.cc:80-90); diffuse_brdf "oren_nayar"
+        with roughness sigma (shinydiffuse.cc:505-514)."""
+        brdf = {"lambert": A.YK_BRDF_LAMBERT, "oren_nayar": A.YK_BRDF_OREN_NAYAR}[diffuse_brdf]
         m = A.yk_material(type_, A.f3(*color), diffuse_reflect, emit, power, int(double_sided),
                           A.f3(*mirror_color), specular_reflect, transparency, translucency, transmit_filter,
-                          int(fresnel_effect), ior)
+                          int(fresnel_effect), ior, brdf, sigma)
         mid = C.c_int32()
         A.check(A.lib().yk_scene_add_material(self._p, C.byref(m), C.byref(mid)))
         return mid.value

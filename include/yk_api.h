@@ -58,7 +58,14 @@ typedef struct yk_material {
   float transmit_filter;  /* "transmit_filter" [1]                                  */
   int32_t fresnel_effect; /* "fresnel_effect" [0]                                   */
   double ior;             /* "IOR" [1.33] (parsed as double; mIOR_Squared = IOR*IOR) */
+  /* "diffuse_brdf" (shinydiffuse.cc:505-514): YK_BRDF_LAMBERT [default] or
+   * YK_BRDF_OREN_NAYAR ("oren_nayar"), whose roughness is "sigma" [0.1,
+   * parsed as double; a zero-initialised struct must set it]:
+   * initOrenNayar(sigma), shinydiffuse.cc:170-176 */
+  int32_t diffuse_brdf;
+  double sigma;
 } yk_material;
+enum { YK_BRDF_LAMBERT = 0, YK_BRDF_OREN_NAYAR = 1 };
 
 enum { YK_LIGHT_AREA = 0, YK_LIGHT_POINT = 1, YK_LIGHT_DIRECTIONAL = 2 };
 typedef struct yk_light {
@@ -284,6 +291,9 @@ typedef struct yk_material_state {
   float transmit_filter;    /* mTransmitFilterStrength                                   */
   int32_t has_fresnel;      /* mHasFresnelEffect                                         */
   float ior_squared;        /* mIOR_Squared                                              */
+  int32_t oren_nayar;       /* mUseOrenNayar                                             */
+  float oren_nayar_a;       /* mOrenNayar_A = 1 - 0.5 s^2/(s^2 + 0.33), in double        */
+  float oren_nayar_b;       /* mOrenNayar_B = 0.45 s^2/(s^2 + 0.09), in double           */
 } yk_material_state;
 
 typedef struct yk_area_light_state { /* areaLight_t members (arealight.h:45-53) */

@@ -748,6 +748,8 @@ typedef struct {
   int fresnel;
   float ior2;
   int double_sided;
+  int on;             /* mUseOrenNayar */
+  float on_a, on_b;   /* mOrenNayar_A / mOrenNayar_B (float members, computed in double) */
 } sdmat;
 static sdmat* g_sd;
 
@@ -806,7 +808,39 @@ static void mats_setup(void) {
       D->comp[3] = M->diffuse_reflect;
     }
     D->ncomp = n;
+    /* factory: diffuse_brdf "oren_nayar" -> initOrenNayar(sigma) (shinydiffuse.cc:505-514, 170-176) */
+    if (M->diffuse_brdf == YK_BRDF_OREN_NAYAR) {
+      double sigma_squared = M->sigma * M->sigma;
+      D->on = 1;
+      D->on_a = (float)(1.0 - 0.5 * (sigma_squared / (sigma_squared + 0.33)));
+      D->on_b = (float)(0.45 * sigma_squared / (sigma_squared + 0.09));
+    }
   }
+}
+
+/* shinyDiffuseMat_t::OrenNayar, shinydiffuse.cc:185-220, source order
+ * (parity unpinned: no reference output uses it). std::min(1.f, x) is
+ * (x < 1) ? x : 1 and std::max(1e-8f, x) is (1e-8 < x) ? x : 1e-8
+ * (<algorithm>); fSqrt is sqrtf; normalize() as vector3d.h:249-260. */
+static float sd_oren_nayar(const sdmat* M, v3 wi, v3 wo, v3 N) {
+  float di = vdot(N, wi), dO = vdot(N, wo);
+  float mi = (di < 1.f) ? di : 1.f, mo = (dO < 1.f) ? dO : 1.f;
+  float cos_ti = (1e-8f < mi) ? mi : 1e-8f, cos_to = (1e-8f < mo) ? mo : 1e-8f;
+  float maxcos_f = 0.f, sin_alpha, tan_beta;
+  if (cos_ti < 0.9999f && cos_to < 0.9999f) {
+    v3 v1 = vnormalize(vsub(wi, vmul(cos_ti, N)));
+    v3 v2 = vnormalize(vsub(wo, vmul(cos_to, N)));
+    float d = vdot(v1, v2);
+    maxcos_f = (0.f < d) ? d : 0.f;
+  }
+  if (cos_to >= cos_ti) {
+    sin_alpha = sqrtf(1.f - cos_ti * cos_ti);
+    tan_beta = sqrtf(1.f - cos_to * cos_to) / cos_to;
+  } else {
+    sin_alpha = sqrtf(1.f - cos_to * cos_to);
+    tan_beta = sqrtf(1.f - cos_ti * cos_ti) / cos_ti;
+  }
+  return M->on_a + M->on_b * maxcos_f * sin_alpha * tan_beta;
 }
 
 static const sdmat* mat_of(int m) { return &g_sd[m]; }
@@ -850,6 +884,7 @@ static col3 sd_eval(const sdmat* M, const surfpt* sp, v3 wo, v3 wl, unsigned bsd
   DBG_CMP(3, vdot(wl, N));
   if (vdot(wl, N) < 0.0f) return C(0, 0, 0);
   float mD = ((1.f - M->comp[2]) * M->comp[3]) * mT;
+  if (M->on) mD *= sd_oren_nayar(M, wo, wl, N); /* shinydiffuse.cc:247 */
   return cscale(mD, M->diff);
 }
 
@@ -939,6 +974,7 @@ static col3 sd_sample(const sdmat* M, const surfpt* sp, v3 wo, v3* wi, float s1i
       w = sample_cos_hemisphere(N, sp->NU, sp->NV, s1, s2in);
       DBG_CMP(4, cos_Ng_wo * vdot(sp->Ng, w));
       if (cos_Ng_wo * vdot(sp->Ng, w) > 0) sc = cscale(a[3], M->diff);
+      if (M->on) sc = cscale(sd_oren_nayar(M, wo, w, N), sc); /* scolor *= OrenNayar(wo, wi, N), :330 */
       *pdf = fabsf(vdot(N, w)) * width[pick];
       break;
   }

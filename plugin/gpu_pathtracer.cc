@@ -18,7 +18,7 @@
 //                 the reference's own flush() normalises them exactly as
 //                 k_film_resolve does
 // What the GPU path cannot reproduce is refused with an error, never rendered
-// differently: textured / Oren-Nayar materials, other lights / backgrounds /
+// differently: textured (shader-node) materials, other lights / backgrounds /
 // cameras / volume integrators, film filters libyk does not build, premultiplied
 // alpha (compounded per pixel, imagefilm.cc:502), depth passes.
 #include <core_api/environment.h>
@@ -105,6 +105,8 @@ YK_MEMBER(SdIsDiffuse, shinyDiffuseMat_t, bool, mIsDiffuse)
 YK_MEMBER(SdFresnel, shinyDiffuseMat_t, bool, mHasFresnelEffect)
 YK_MEMBER(SdIor2, shinyDiffuseMat_t, float, mIOR_Squared)
 YK_MEMBER(SdOrenNayar, shinyDiffuseMat_t, bool, mUseOrenNayar)
+YK_MEMBER(SdOrenNayarA, shinyDiffuseMat_t, float, mOrenNayar_A)
+YK_MEMBER(SdOrenNayarB, shinyDiffuseMat_t, float, mOrenNayar_B)
 YK_MEMBER(SdNBSDF, shinyDiffuseMat_t, int, nBSDF)
 YK_MEMBER(SdCFlags, shinyDiffuseMat_t, BSDF_t[4], cFlags)
 YK_MEMBER(SdCIndex, shinyDiffuseMat_t, int[4], cIndex)
@@ -588,7 +590,6 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
       if (GET(*sd, SdDiffuseShader) || GET(*sd, SdBumpShader) || GET(*sd, SdMirrorShader) ||
           GET(*sd, SdMirrorColorShader) || GET(*sd, SdTranspShader) || GET(*sd, SdTranslShader))
         return unsupported("textured (shader-node) shinydiffuse is not on the GPU path");
-      if (GET(*sd, SdOrenNayar)) return unsupported("Oren-Nayar shinydiffuse is not on the GPU path");
       const color_t &c = GET(*sd, SdColor), &e = GET(*sd, SdEmit), &mc = GET(*sd, SdMirrorColor);
       put3(s.color, c.R, c.G, c.B);
       put3(s.emit_color, e.R, e.G, e.B);
@@ -608,6 +609,11 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
       s.transmit_filter = GET(*sd, SdFilter);
       s.has_fresnel = GET(*sd, SdFresnel) ? 1 : 0;
       s.ior_squared = GET(*sd, SdIor2);
+      // diffuse_brdf "oren_nayar": initOrenNayar's A / B as the object holds
+      // them (shinydiffuse.cc:170-176)
+      s.oren_nayar = GET(*sd, SdOrenNayar) ? 1 : 0;
+      s.oren_nayar_a = GET(*sd, SdOrenNayarA);
+      s.oren_nayar_b = GET(*sd, SdOrenNayarB);
     } else if (s.bsdf_flags == BSDF_EMIT) {
       // lightMat_t is defined in a .cc (simple.cc:36-70): read lightCol and
       // doubleSided back through its virtual emit()

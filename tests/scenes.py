@@ -197,3 +197,27 @@ def dof_cornell(resx, resy, integrator="cornell_pt", bokeh_type=0, bokeh_bias=0,
                  dof_distance=4.2, bokeh_type=bokeh_type, bokeh_bias=bokeh_bias, bokeh_rotation=rotation)
     s.build()
     return s, p
+
+
+def oren_nayar(resx, resy, integrator="cornell_pt", sigma=0.1, brdf="oren_nayar"):
+    """Cornell box + two smooth spheres and a flat box of shinydiffuse
+    materials with diffuse_brdf "oren_nayar" (shinydiffuse.cc:170-220,
+    505-514): a diffuse-only one, one with a translucent component (the
+    general component loop) and, on the box, sigma doubled. The factor
+    applies in eval (:247, direct light) and sample (:330, path bounces)."""
+    s = Scene()
+    p = s.generate(integrator, resx, resy)
+    on1 = s.add_material(color=(0.8, 0.75, 0.6), diffuse_brdf=brdf, sigma=sigma)
+    on2 = s.add_material(color=(0.5, 0.8, 0.9), diffuse_reflect=0.7, translucency=0.35, diffuse_brdf=brdf,
+                         sigma=sigma)
+    on3 = s.add_material(color=(0.9, 0.4, 0.4), diffuse_brdf=brdf, sigma=2 * sigma)
+    for (cx, cy, cz, r), m in (((-0.35, 0.45, 0.2, 0.3), on1), ((0.4, 0.3, -0.35, 0.28), on2)):
+        pts, faces, nrm = uv_sphere(18, 11, r, (cx, cy, cz))
+        oid = s.add_mesh(pts, faces, m)
+        s.set_mesh_normals(oid, nrm, faces, smooth=True)
+    b = np.array([[x, y, z] for x in (-0.1, 0.2) for y in (1.0, 1.4) for z in (-0.2, 0.1)], np.float32)
+    box = np.array([[0, 1, 3], [0, 3, 2], [4, 6, 7], [4, 7, 5], [0, 4, 5], [0, 5, 1],
+                    [2, 3, 7], [2, 7, 6], [0, 2, 6], [0, 6, 4], [1, 5, 7], [1, 7, 3]], np.int32)
+    s.add_mesh(b, box, on3)
+    s.build()
+    return s, p
