@@ -6,6 +6,7 @@
 # Steps (VARIANT = base for core_amd/libyk.so, else tune/libyk_VARIANT.so; VARIANT@NAME=VALUE
 # adds one environment setting, e.g. base@YK_SMALL=0):
 #   test                 pytest -m gpu (one process, per-test timeout)
+#   testv:VARIANT        the traversal / render parity files with a tuning variant's library
 #   smoke                __graft_entry__.smoke()
 #   bench                headline bench.py (1M tris, 1080p, 256 spp)
 #   c2 | pm | hair       BASELINE configs[1] Cornell / photon mapping / C5 hair benches
@@ -14,6 +15,7 @@
 #   pmc                  FETCH_SIZE and WRITE_SIZE passes of the one-pipe headline frame
 #   pmc_c2 | pmc_hair    the same for Cornell / hair
 #   tb:VARIANT           traversal microbenchmark (tools/trav_bench.py)
+#   tbs:VARIANT          the same with launch time against ray count (prefixes; intercept = per-launch cost)
 #   ab:V1,V2,...         A/B: trav bench + headline bench per variant, two interleaved reps
 #   abc2:V1,V2,...       A/B on the Cornell (C2) bench
 #   abpm:V1,V2,...       A/B on the photon-mapping bench
@@ -43,6 +45,11 @@ for s in "$@"; do
   test)
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gputest.txt 2>&1
     tail -3 $O/gputest.txt ;;
+  testv:*)
+    # the parity files against a tuning variant's library (bit-exactness of an A/B build)
+    v=${s#testv:}
+    YK_LIB=$(lib $v) timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_big_leaf.py tests/test_universal.py tests/test_transparent_shadows.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/testv_$v.txt 2>&1
+    tail -2 $O/testv_$v.txt ;;
   smoke)
     timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1
     tail -1 $O/smoke.txt ;;
@@ -67,6 +74,11 @@ for s in "$@"; do
     timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/${s}_fetch -o f -- python3 bench.py $A $P1 > $O/${s}_fetch.log 2>&1
     timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/${s}_write -o w -- python3 bench.py $A $P1 > $O/${s}_write.log 2>&1
     echo "$s done" ;;
+  tbs:*)
+    # launch time against ray count (prefixes of each population)
+    v=${s#tbs:}
+    YK_LIB=$(lib $v) timeout -k 10 300 python -u tools/trav_bench.py --spp 4 --sizes > $O/tbs_$v.json 2> $O/tbs_$v.err
+    cat $O/tbs_$v.json ;;
   tb:*)
     v=${s#tb:}
     YK_LIB=$(lib $v) timeout -k 10 200 python -u tools/trav_bench.py --spp 4 > $O/tb_$v.json 2> $O/tb_$v.err

@@ -108,6 +108,9 @@ def main():
     ap.add_argument("--nu", type=int, default=1000)
     ap.add_argument("--nv", type=int, default=501)
     ap.add_argument("--scene", default="bumpy", choices=["bumpy", "cornell"])
+    ap.add_argument("--sizes", action="store_true",
+                    help="also trace prefixes (1/16 .. 1) of each population: launch time against ray count, "
+                         "whose intercept is the per-launch cost (start + drain tail)")
     args = ap.parse_args()
     cb = args.scene == "cornell"
     scene, _ = probe_scene("cornell_pt", 64, 64) if cb else probe_scene("bumpy", 64, 64, args.nu, args.nv)
@@ -141,6 +144,23 @@ def main():
         tris = (st.closest_tris if closest else st.shadow_tris) / n
         out[name] = {"rays": n, "ms": round(ms, 3), "Mrays_s": round(n / ms / 1e3, 1), "nodes": round(nodes, 2),
                      "tris": round(tris, 2)}
+        if args.sizes:
+            pts = []
+            for f in (16, 8, 4, 2, 1):
+                m = n // f
+                sub = rays[:m].contiguous()
+                t = []
+                for _ in range(args.reps):
+                    st = A.yk_stats()
+                    (dev.trace_closest if closest else dev.trace_shadow)(sub, st)
+                    t.append(st.ms_closest if closest else st.ms_shadow)
+                pts.append((m, min(t)))
+            x = np.array([p[0] for p in pts], float)
+            y = np.array([p[1] for p in pts], float)
+            b, a = np.polyfit(x, y, 1)
+            out[name]["sizes"] = [[int(m), round(t, 4)] for m, t in pts]
+            out[name]["fit_ms_intercept"] = round(float(a), 4)
+            out[name]["fit_ns_per_ray"] = round(float(b) * 1e6, 4)
         tot_rays += n
         tot_ms += ms
     out["total_Mrays_s"] = round(tot_rays / tot_ms / 1e3, 1)
