@@ -2165,6 +2165,7 @@ struct Batch {
   char4* pext;          // per pixel slot: footprint extent of its samples (k_pixel_extent)
   int K;
   long long cap;  // samples per batch: the stride of the shadow-slot arrays
+  long long slot_base;  // merged shadow launch: first slot of this bounce's slot region (0 otherwise)
   // specular recursion (recursiveRaytrace) only, see k_spawn / k_fold
   unsigned* psample;    // pixel sample index of each entry (state.pixelSample)
   uint8_t* incl;        // state.includeLights after the entry's path loop
@@ -2177,7 +2178,7 @@ struct Batch {
   float* sl_aux;        // 4 per slot: scalar factors (and the Dirac light colour)
 };
 __device__ __forceinline__ long long slot_of(const Batch& B, long long c, int k) {
-  return (long long)k * B.cap + c;  // k-major (sample-major c * K + k: C2 7810 against 8047 Mrays/s)
+  return B.slot_base + (long long)k * B.cap + c;  // k-major (sample-major c * K + k: C2 7810 against 8047 Mrays/s)
 }
 
 struct RenderConst {
@@ -2898,6 +2899,92 @@ __global__ void __launch_bounds__(256) k_resolve_bounce(Batch B, RenderConst R,
   }
 }
 
+// ---- merged shadow launch (path tracing without specular recursion,
+// photon maps or transparent shadows, one sub-path): the camera hits' shadow
+// rays and every bounce's go to one any-hit launch per batch instead of one
+// per bounce. Each trace launch carries a fixed cost -- its start and the
+// drain of its last rays, about 0.25-0.3 ms on the headline scene whatever
+// its size (tools/trav_bench.py --sizes) -- so four launches per batch paid
+// it four times. The bounces' shadow rays do not feed the next bounce (its
+// closest rays come from the BSDF sample alone), only the resolve, which then
+// runs once per batch over all bounces in the reference's order: every bounce
+// writes its own slot region (slot_base), path state (pstate, lsel, emit_b,
+// scol_next at (depth-1)*cap) and queue region of slot indices.
+
+// Batch view of bounce `depth`'s slot region and path state (host and device)
+__host__ __device__ inline Batch merged_region(Batch B, int depth) {
+  const long long rs = (long long)B.K * B.cap;
+  B.slot_base = (long long)depth * rs;
+  B.s_idx += depth * rs;
+  if (depth >= 1) {
+    const long long o = (long long)(depth - 1) * B.cap;
+    B.pstate += o;
+    B.lsel += o;
+    B.emit_b += 3 * o;
+    B.scol_next += 3 * o;
+  }
+  return B;
+}
+
+// the regions' queued slot indices, concatenated in region order into one
+// queue (idxm) with its count in low 32 bits of *mword; qw0: region 0's count
+// word, qstride: words between the regions' count words
+__global__ void __launch_bounds__(256) k_concat_shadow(const unsigned* __restrict__ idx, unsigned* __restrict__ idxm,
+                                                       const unsigned long long* __restrict__ qw0, int regions,
+                                                       long long rstride, unsigned long long* __restrict__ mword) {
+  unsigned long long off = 0;
+  for (int r = 0; r < regions; ++r) {
+    const unsigned long long n = qw0[r] & 0xFFFFFFFFull;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (unsigned long long)gridDim.x * blockDim.x)
+      idxm[off + i] = idx[(unsigned long long)r * rstride + i];
+    off += n;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *mword = off;
+}
+
+// k_resolve_primary, then k_resolve_bounce for depth 1..bounces, per camera
+// sample in that order: the same float operations on the same values as the
+// per-bounce resolves. A sample's path entered depth 1 iff its camera hit was
+// diffuse (k_shade_primary's first segment), and depth d+1 iff depth d set
+// PS_CONT, so no stale region state is read.
+__global__ void __launch_bounds__(256) k_resolve_merged(Batch B, RenderConst R, long long nc, int bounces) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc || !(B.prim_hit[c] & PH_DIFFUSE)) return;
+  {
+    c3 dl = C3(0.f, 0.f, 0.f);
+    int k0 = 0;
+    for (int l = 0; l < R.nlights; ++l) {
+      dl = cadd(dl, resolve_light(B, c, k0, l));
+      k0 += c_lights[l].nslots;
+    }
+    B.col[3 * c] = B.col[3 * c] + dl.r;
+    B.col[3 * c + 1] = B.col[3 * c + 1] + dl.g;
+    B.col[3 * c + 2] = B.col[3 * c + 2] + dl.b;
+  }
+  if (bounces < 1) return;
+  c3 thr = C3(B.thr[3 * c], B.thr[3 * c + 1], B.thr[3 * c + 2]);
+  c3 pc = C3(B.pathcol[3 * c], B.pathcol[3 * c + 1], B.pathcol[3 * c + 2]);
+  for (int depth = 1; depth <= bounces; ++depth) {
+    const Batch Bd = merged_region(B, depth);
+    const int ps = Bd.pstate[c];
+    if (!(ps & PS_RESOLVE)) break;
+    c3 lcol = C3(0.f, 0.f, 0.f);
+    if (ps & PS_EST) {
+      const int lnum = R.nlights > 1 ? Bd.lsel[c] : 0;
+      lcol = cscale((float)R.nlights, resolve_light(Bd, c, 0, lnum));
+    }
+    if (depth == 1 && (ps & PS_EMIT))
+      lcol = cadd(lcol, C3(Bd.emit_b[3 * c], Bd.emit_b[3 * c + 1], Bd.emit_b[3 * c + 2]));
+    pc = C3(pc.r + lcol.r * thr.r, pc.g + lcol.g * thr.g, pc.b + lcol.b * thr.b);
+    if (!(ps & PS_CONT)) break;
+    thr = C3(thr.r * Bd.scol_next[3 * c], thr.g * Bd.scol_next[3 * c + 1], thr.b * Bd.scol_next[3 * c + 2]);
+  }
+  B.pathcol[3 * c] = pc.r;
+  B.pathcol[3 * c + 1] = pc.g;
+  B.pathcol[3 * c + 2] = pc.b;
+}
+
 // col += pathCol / nSamples (pathtracer.cc:300-302); final sample (wt = 1)
 __global__ void __launch_bounds__(256) k_finish(Batch B, RenderConst R, long long nc) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3377,7 +3464,7 @@ struct Pipe {
   DBuf<unsigned long long> words;     // per-render: queue-count words, ray segments, accumulators
   DBuf<uint2> ovf;                    // traversal stack overflow (entries deeper than the LDS ring)
   std::vector<hipEvent_t> evpool;     // per-launch timing events of one render
-  DBuf<unsigned> soffs, s_idx;
+  DBuf<unsigned> soffs, s_idx, s_idxm;
   DBuf<float> col, alpha, thr, pathcol, scol_next, wlast, emit_b, sl_contrib;
   DBuf<int> prim_hit, pstate, lsel, qo0, qo1, tile_base;
   DBuf<int4> tiles;
@@ -3413,7 +3500,10 @@ struct Pipe {
     if (ev1) (void)hipEventDestroy(ev1);
     if (stream) (void)hipStreamDestroy(stream);
   }
-  Batch bind(long long maxc, int K, int tiles_per_batch, bool spec = false, bool ts = false) {
+  // regions > 1: the merged shadow launch's slot regions (camera hits + one
+  // per bounce) and per-bounce path state (merged_region)
+  Batch bind(long long maxc, int K, int tiles_per_batch, bool spec = false, bool ts = false, int regions = 1) {
+    const long long nst = std::max(1, regions - 1);  // path-state copies
     soffs.ensure(maxc);
     col.ensure(3 * maxc);
     alpha.ensure(maxc);
@@ -3422,22 +3512,23 @@ struct Pipe {
     p_hits.ensure(maxc);
     thr.ensure(3 * maxc);
     pathcol.ensure(3 * maxc);
-    scol_next.ensure(3 * maxc);
+    scol_next.ensure(3 * maxc * nst);
     wlast.ensure(maxc);
-    emit_b.ensure(3 * maxc);
-    pstate.ensure(maxc);
-    lsel.ensure(maxc);
+    emit_b.ensure(3 * maxc * nst);
+    pstate.ensure(maxc * nst);
+    lsel.ensure(maxc * nst);
     qo0.ensure(maxc);
     qo1.ensure(maxc);
     qr0.ensure(maxc);
     qr1.ensure(maxc);
     qh0.ensure(maxc);
     qh1.ensure(maxc);
-    s_rays.ensure(maxc * K);
-    s_occl.ensure(maxc * K);
-    s_idx.ensure(maxc * K);
-    sl_contrib.ensure(3 * maxc * K);
-    sl_flags.ensure(maxc * K);
+    s_rays.ensure(maxc * K * regions);
+    s_occl.ensure(maxc * K * regions);
+    s_idx.ensure(maxc * K * regions);
+    if (regions > 1) s_idxm.ensure(maxc * K * regions);
+    sl_contrib.ensure(3 * maxc * K * regions);
+    sl_flags.ensure(maxc * K * regions);
     samples.ensure(maxc);
     sxy.ensure(maxc);
     pext.ensure(maxc);  // one per pixel slot; maxc bounds the slots of any spp
@@ -4161,6 +4252,10 @@ int yk_device_open(int32_t ordinal, yk_device** out) {
   d->per_cu_ts = std::max(1, blocks);
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_pm_lookup<false>, 64, 0));
   d->per_cu_lookup[0] = std::max(1, blocks);
+  if (const char* v = std::getenv("YK_VERBOSE"); v && std::atoi(v) > 0)
+    std::fprintf(stderr, "[libyk] %d CUs; resident workgroups per CU: any-hit %d (x%d waves), closest %d (x%d), "
+                 "big %d / %d, transparent-shadow %d\n", d->cus, d->per_cu[0], YK_SHADOW_G, d->per_cu[1],
+                 YK_CLOSEST_G, d->per_cu_big[0], d->per_cu_big[1], d->per_cu_ts);
   upload_qmc();
   *out = d;
   return YK_OK;
@@ -4587,13 +4682,26 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     const long long v = e ? std::atoll(e) : 0;
     return v > 0 ? v : (32ll << 20);
   }();
-  // HBM for the batch buffers of all pipes (YK_BATCH_GB, default 64 of the 288 GB)
-  static const long long batch_bytes = [] {
+  // merged shadow launch (k_resolve_merged): path tracing without specular
+  // recursion, photon maps or transparent shadows, one sub-path; YK_MERGE=0
+  // (read per render: A/B runs, tests) keeps one any-hit launch per bounce
+  const bool merged = [&] {
+    const char* e = std::getenv("YK_MERGE");
+    return !(e && std::atoi(e) == 0) && p->integrator == YK_INTEGRATOR_PATH && !d->spec && !pt_cmap &&
+           !p->transp_shadows && p->path_samples <= 1 && p->bounces >= 1;
+  }();
+  const int regions = merged ? p->bounces + 1 : 1;
+  // HBM for the batch buffers of all pipes (YK_BATCH_GB, default 64 of the
+  // 288 GB, 128 with the merged launch's slot regions)
+  static const long long batch_gb_env = [] {
     const char* e = std::getenv("YK_BATCH_GB");
     const long long v = e ? std::atoll(e) : 0;
-    return (v > 0 && v <= 240 ? v : 64ll) << 30;
+    return (v > 0 && v <= 240) ? v : 0ll;
   }();
-  const long long bytes_per_sample = 400 + 52ll * K;
+  const long long batch_bytes = (batch_gb_env ? batch_gb_env : (merged ? 128ll : 64ll)) << 30;
+  // + per extra region: 54 B per slot (ray, contribution, flag, result,
+  // region and merged queue entries) and 32 B of path state per sample
+  const long long bytes_per_sample = 400 + 52ll * K + (long long)(regions - 1) * (54ll * K + 32);
   const int pipes_cfg = pipes_env();
   const long long target = std::max(1ll << 20, std::min(target_env, batch_bytes / pipes_cfg / bytes_per_sample));
   const long long tile_samples = (long long)F.tile * F.tile * spp;
@@ -4610,7 +4718,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   const long long maxc = (long long)tiles_per_batch * tile_samples;
   // camera-sample indices are 32-bit on the device, shadow-slot indices
   // (k * maxc + c) 32-bit in the shadow queue
-  if (maxc >= (1ll << 31) || maxc * (long long)std::max(K, 1) >= (1ll << 32))
+  if (maxc >= (1ll << 31) || maxc * (long long)std::max(K, 1) * regions >= (1ll << 32))
     return set_error(YK_ERR_UNSUPPORTED, "one tile holds too many samples (tile^2 * spp * shadow slots >= 2^32)");
   const int nbatch = (int)((owned.size() + tiles_per_batch - 1) / tiles_per_batch);
   const int npipes = d->spec ? 1 : std::min(pipes_cfg, std::max(1, nbatch));
@@ -4690,14 +4798,15 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   // All zeroed once; no launch needs a reset or a host round trip.
   const int qwords_per_batch = nsub * (bounces + 1);
   const int launches_per_batch = 2 + 2 * nsub * bounces + (R.pm_fg ? nsub * bounces : 0);
-  const long long words_per_batch = 2ll * qwords_per_batch + 128ll * launches_per_batch;
+  // + the merged shadow queue's count word
+  const long long words_per_batch = 2ll * qwords_per_batch + 128ll * launches_per_batch + 1;
   Batch Bp[kPipes];
   for (int pi = 0; pi < npipes; ++pi) {
     Pipe& P = d->pipe[pi];
     const int nb_here = (nbatch - pi + npipes - 1) / npipes;
     P.words.ensure((size_t)(2 * kAccWords + (d->spec ? 0 : words_per_batch * nb_here)));
     HIPCHK(hipMemsetAsync(P.words.p, 0, P.words.n * sizeof(unsigned long long), P.stream));
-    Bp[pi] = P.bind(maxc, K, tiles_per_batch, R.ps != 0, p->transp_shadows != 0);
+    Bp[pi] = P.bind(maxc, K, tiles_per_batch, R.ps != 0, p->transp_shadows != 0, regions);
     if (R.pm_fg) {
       P.fgl.ensure(3 * maxc);
       P.fglen.ensure(maxc);
@@ -4888,9 +4997,11 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     trace(true, B.p_rays, nullptr, RayCount{nullptr, 0, nc}, B.p_hits, nullptr);
     hipLaunchKernelGGL(d->diff_only ? k_shade_primary<true> : k_shade_primary<false>, dim3(grid_for(nc, YK_PRIMARY_BLOCK)), dim3(YK_PRIMARY_BLOCK), 0, P.stream, d->S, B, R, nc, qw(0, 0));
     HIPCHK(hipGetLastError());
-    trace(false, B.s_rays, B.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, B.s_occl);
-    hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
-    HIPCHK(hipGetLastError());
+    if (!merged) {
+      trace(false, B.s_rays, B.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, B.s_occl);
+      hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
+      HIPCHK(hipGetLastError());
+    }
     if (pm) pm_entries(B, R, nc);
     if (pt_cmap) pt_caustic(B, nc);
     // sub-path index outermost: pathCol is shared across sub-paths and
@@ -4906,14 +5017,26 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
         const unsigned long long* in_w = qw(isub, depth - 1);
         unsigned long long* out_w = qw(isub, depth);
         trace(true, B.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, B.q_hits[qin], nullptr);
-        hipLaunchKernelGGL(d->diff_only ? k_shade_bounce<true> : k_shade_bounce<false>, dim3(grid_for(nc, bounce_block(d->diff_only))), dim3(bounce_block(d->diff_only)), 0, P.stream, d->S, B, R, in_w, depth, isub,
+        const Batch Bd = merged ? merged_region(B, depth) : B;
+        hipLaunchKernelGGL(d->diff_only ? k_shade_bounce<true> : k_shade_bounce<false>, dim3(grid_for(nc, bounce_block(d->diff_only))), dim3(bounce_block(d->diff_only)), 0, P.stream, d->S, Bd, R, in_w, depth, isub,
                            qin, out_w);
         HIPCHK(hipGetLastError());
-        trace(false, B.s_rays, B.s_idx, RayCount{out_w, 0, 0}, nullptr, B.s_occl);
-        hipLaunchKernelGGL(k_resolve_bounce, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, in_w, depth, qin);
-        HIPCHK(hipGetLastError());
+        if (!merged) {
+          trace(false, B.s_rays, B.s_idx, RayCount{out_w, 0, 0}, nullptr, B.s_occl);
+          hipLaunchKernelGGL(k_resolve_bounce, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, in_w, depth, qin);
+          HIPCHK(hipGetLastError());
+        }
         qin ^= 1;
       }
+    }
+    if (merged) {  // one any-hit launch for the camera hits and all bounces, then one resolve
+      unsigned long long* mword = bw + 2ll * qwords_per_batch + 128ll * launches_per_batch;
+      hipLaunchKernelGGL(k_concat_shadow, dim3(1024), dim3(256), 0, P.stream, B.s_idx, P.s_idxm.p, qw(0, 0),
+                         regions, (long long)K * maxc, mword);
+      HIPCHK(hipGetLastError());
+      trace(false, B.s_rays, P.s_idxm.p, RayCount{mword, 0, 0}, nullptr, B.s_occl);
+      hipLaunchKernelGGL(k_resolve_merged, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc, bounces);
+      HIPCHK(hipGetLastError());
     }
     hipLaunchKernelGGL(k_finish, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
     HIPCHK(hipGetLastError());
