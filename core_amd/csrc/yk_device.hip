@@ -784,7 +784,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // tb / lb: the triangle records by prim and in leaf order (S.tris / S.ltris,
 // or their LDS copies: W > 1, 48-B records)
-template <bool CLOSEST, bool BIG = false, bool UNI = false, int W = 1, int SW = W>
+template <bool CLOSEST, bool BIG = false, bool UNI = false, int W = 1>
 __device__ __forceinline__ void coop_leaves(const DScene& S, const float* tb, const float* lb, Trav& st,
                                             uint32_t nref, uint32_t w0,
                                             std::conditional_t<CLOSEST, unsigned long long, unsigned>* keys,
@@ -809,7 +809,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, const float* tb, co
     if (CLOSEST) keys[lane] = ((unsigned long long)m1 << 32) | m1;
     else keys[lane] = m1;  // any-hit keys are reference indices: 32 bits
   }
-  wave_lds_sync<SW>();
+  wave_lds_sync<W>();
   const float zlim = CLOSEST ? st.Z : st.dist;
   if constexpr (!CLOSEST && YK_ANYHIT_DYN) {
     // Any-hit leaves of more than one round (crowded leaves: hair): the
@@ -835,7 +835,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, const float* tb, co
         if (rtot == 0u) break;
         otab[lane] = 0u;
         if (rem > 0u && rpre < 64u) otab[rpre] = (rpre << 8) + (vconst<0x100u>() | (unsigned)lane);
-        wave_lds_sync<SW>();
+        wave_lds_sync<W>();
         // slot 0 always starts a range (the first lane with references left)
         const unsigned ov = dpp_max_scan(otab[lane]);
         int own;
@@ -858,7 +858,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, const float* tb, co
             atomicMin(&keys[own], k);
         }
         if (rem > 0u && rpre < 64u) cons += min(rem, 64u - rpre);
-        wave_lds_sync<SW>();
+        wave_lds_sync<W>();
       }
       if (nref > 0u) {
         const unsigned kk = keys[lane];
@@ -882,7 +882,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, const float* tb, co
     otab[lane] = 0u;
     if (nref > 0u && pre >= base && pre - base < 64u)
       otab[pre - base] = ((BIG ? pre - base : pre) << 8) + (vconst<0x100u>() | (unsigned)lane);
-    wave_lds_sync<SW>();
+    wave_lds_sync<W>();
     const unsigned ov = dpp_max_scan(otab[lane]);
     // slots before the round's first range start continue the range that
     // covered the previous round's last slot
@@ -930,7 +930,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, const float* tb, co
       }
     }
     if (CLOSEST) {
-      wave_lds_sync<SW>();
+      wave_lds_sync<W>();
       // the winner keeps its prim as a code: prim | 1 << 31 for a
       // single-reference leaf, else its leaf-list position, read when the
       // ray finishes (a leaf-list load here put a dependent global load on
@@ -941,7 +941,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, const float* tb, co
       }
     }
   }
-  wave_lds_sync<SW>();
+  wave_lds_sync<W>();
   if (nref > 0u) {
     const unsigned long long kk = CLOSEST ? (unsigned long long)keys[lane] : (keys[lane] == ~0u ? ~0ull : keys[lane]);
     if (CLOSEST) {
@@ -1069,11 +1069,7 @@ size_t small_scene_bytes(size_t nn, size_t ntris, size_t nlref) {
   return 4 * (((6 * nn + 3) & ~(size_t)3) + 12 * (ntris + nlref));  // small_rec_word in 64 bits
 }
 
-// G > 1 (HBM kernels, W == 1): G one-wave ray queries per workgroup that
-// draw their hand-out chunks from one shared super-chunk (wg_hand), so the
-// waves of a CU trace neighbouring queue entries (per-CU locality, VERDICT
-// r05 item 2). WPG: waves per workgroup.
-template <bool CLOSEST, int NSEG, bool TS = false, bool BIG = false, bool UNI = false, int W = 1, int G = 1>
+template <bool CLOSEST, int NSEG, bool TS = false, bool BIG = false, bool UNI = false, int W = 1>
 __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx,
                                            RayCount rc, yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
                                            unsigned long long* __restrict__ work, unsigned long long* __restrict__ ctr,
@@ -1093,37 +1089,27 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   const float *tb, *lb;
   unsigned wv = 0;  // wave of the workgroup
   int lane;
-  static_assert(W == 1 || G == 1, "shared hand-out groups are for the one-wave (HBM) kernels");
-  constexpr int WPG = W > 1 ? W : G;
-  unsigned long long* wg_hand = nullptr;  // G > 1: the workgroup's super-chunk {next, end << 32}
   if constexpr (W == 1) {
     // LDS of the cooperative leaf test first: its owner table then sits at
     // offset 0, and its addresses need no base register
-    __shared__ unsigned a_otab[G][64];
-    __shared__ uint2 a_lds[G][R * 64];
-    __shared__ float a_tmin[G][(CLOSEST || UNI) ? 64 : 1];
-    __shared__ unsigned a_res[G][(!CLOSEST && !TS) ? 128 : 1];
-    __shared__ unsigned a_n0[G][64];
-    __shared__ KeyT a_keys[G][64];
-    __shared__ float4 a_cand[G][CLOSEST ? 64 : 1];
-    if constexpr (G > 1) {
-      __shared__ unsigned long long a_hand;
-      wg_hand = &a_hand;
-      if (threadIdx.x == 0) a_hand = 0ull;  // empty: the first chunk request fetches a super-chunk
-      __syncthreads();
-      wv = (unsigned)__builtin_amdgcn_readfirstlane((int)threadIdx.x) >> 6;
-    }
-    otab = a_otab[wv];
-    lds = a_lds[wv];
-    s_tmin = a_tmin[wv];
-    res_slot = a_res[wv];
-    ray_n0 = a_n0[wv];
-    keys = a_keys[wv];
-    cand = a_cand[wv];
+    __shared__ unsigned a_otab[64];
+    __shared__ uint2 a_lds[R * 64];
+    __shared__ float a_tmin[(CLOSEST || UNI) ? 64 : 1];
+    __shared__ unsigned a_res[(!CLOSEST && !TS) ? 128 : 1];
+    __shared__ unsigned a_n0[64];
+    __shared__ KeyT a_keys[64];
+    __shared__ float4 a_cand[CLOSEST ? 64 : 1];
+    otab = a_otab;
+    lds = a_lds;
+    s_tmin = a_tmin;
+    res_slot = a_res;
+    ray_n0 = a_n0;
+    keys = a_keys;
+    cand = a_cand;
     nbase = reinterpret_cast<const char*>(S.pk);
     tb = S.tris;
     lb = S.ltris;
-    lane = G > 1 ? (int)(threadIdx.x & 63u) : (int)threadIdx.x;
+    lane = threadIdx.x;
   } else {
     __shared__ WaveLds<CLOSEST, UNI, R> s_w[W];
     wv = (unsigned)__builtin_amdgcn_readfirstlane((int)threadIdx.x) >> 6;
@@ -1144,7 +1130,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
     lb = tb + S.ntris * 12u;
     lane = threadIdx.x & 63u;
   }
-  const unsigned gw = blockIdx.x * (unsigned)WPG + wv;  // wave of the launch
+  const unsigned gw = blockIdx.x * (unsigned)W + wv;  // wave of the launch
   unsigned npend = 0;  // wave-uniform
   const long long n = __builtin_amdgcn_readfirstlane((int)rc.get());
   if (gw == 0 && lane == 0 && n > 0) atomicAdd(&ctr[3], (unsigned long long)n);  // rays traced
@@ -1179,7 +1165,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 #endif
   const unsigned kPoolChunk = (unsigned)__builtin_amdgcn_readfirstlane((int)max(
       64u, min(min((unsigned)YK_POOL_CHUNK_MAX, S.chunk_max),
-               (unsigned)(n / ((long long)gridDim.x * WPG * YK_POOL_CHUNKS)) & ~63u)));
+               (unsigned)(n / ((long long)gridDim.x * W * YK_POOL_CHUNKS)) & ~63u)));
   unsigned xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
   constexpr unsigned kAll = (1u << NSEG) - 1u;
@@ -1218,66 +1204,26 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       const unsigned avail = pool_end - pool_next;
       unsigned cb = 0, ce = 0;  // newly grabbed chunk [cb, ce)
       if (avail < cnt && seg_done != kAll) {
-        bool fetch = true;
-        if constexpr (G > 1) {
-          // a chunk of the workgroup's super-chunk: one LDS atomic (adds to the low word)
-          unsigned long long old = 0;
-          if (lane == 0) old = atomicAdd(wg_hand, (unsigned long long)kPoolChunk);
-          const unsigned nx = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)shfl_u64(old, 0));
-          const unsigned en = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(shfl_u64(old, 0) >> 32));
-          if (nx < en) {
-            cb = nx;
-            ce = min(nx + kPoolChunk, en);
-            fetch = false;
-          }
-        }
-        constexpr unsigned kFetch = G > 1 ? (unsigned)G : 1u;  // chunks per queue fetch
-        if (fetch) {
 #pragma unroll 1  // rolled: an unrolled search held every segment's bounds in SGPRs (spilled to VGPR lanes)
-          for (unsigned k = 0; k < (unsigned)NSEG; ++k) {
-            const unsigned sgi = (xcc + k) % (unsigned)NSEG;
-            if (seg_done & (1u << sgi)) continue;
-            const unsigned long long s0 = (unsigned long long)sgi * seg_len;
-            const unsigned long long s1 = min(s0 + seg_len, (unsigned long long)n);
-            unsigned take = kPoolChunk * kFetch;
-            if (YK_TAIL_ZONE > 0 && (in_tail || k > 0)) take = 64u;
-            unsigned long long base = 0;
-            if (lane == 0) base = atomicAdd(work + 16 * sgi, (unsigned long long)take);
-            base = s0 + shfl_u64(base, 0);
-            if (base < s1) {
-              cb = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)base);
-              ce = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)min(base + take, s1));
-              if (YK_TAIL_ZONE > 0 && k == 0 &&
-                  base + (unsigned long long)YK_TAIL_ZONE * kPoolChunk * kFetch * (gridDim.x * WPG / NSEG + 1) >= s1)
-                in_tail = true;
-              break;
-            }
-            seg_done |= 1u << sgi;
+        for (unsigned k = 0; k < (unsigned)NSEG; ++k) {
+          const unsigned sgi = (xcc + k) % (unsigned)NSEG;
+          if (seg_done & (1u << sgi)) continue;
+          const unsigned long long s0 = (unsigned long long)sgi * seg_len;
+          const unsigned long long s1 = min(s0 + seg_len, (unsigned long long)n);
+          unsigned take = kPoolChunk;
+          if (YK_TAIL_ZONE > 0 && (in_tail || k > 0)) take = 64u;
+          unsigned long long base = 0;
+          if (lane == 0) base = atomicAdd(work + 16 * sgi, (unsigned long long)take);
+          base = s0 + shfl_u64(base, 0);
+          if (base < s1) {
+            cb = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)base);
+            ce = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)min(base + take, s1));
+            if (YK_TAIL_ZONE > 0 && k == 0 &&
+                base + (unsigned long long)YK_TAIL_ZONE * kPoolChunk * (gridDim.x * W / NSEG + 1) >= s1)
+              in_tail = true;
+            break;
           }
-          if constexpr (G > 1) {
-            if (ce > cb) {
-              // install the rest of the super-chunk for the workgroup unless
-              // another wave installed one meanwhile (then keep it all)
-              unsigned long long cur = 0;
-              if (lane == 0) cur = __hip_atomic_load(wg_hand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              cur = shfl_u64(cur, 0);
-#pragma unroll 1
-              for (;;) {
-                if ((unsigned)cur < (unsigned)(cur >> 32)) break;  // a live super-chunk: ours stays private
-                const unsigned mine = min(cb + kPoolChunk, ce);
-                const unsigned long long nv = ((unsigned long long)ce << 32) | mine;
-                unsigned long long prev = 0;
-                if (lane == 0) prev = atomicCAS(wg_hand, cur, nv);
-                prev = shfl_u64(prev, 0);
-                if (prev == cur) {
-                  ce = mine;
-                  break;
-                }
-                cur = prev;
-              }
-              ce = (unsigned)__builtin_amdgcn_readfirstlane((int)ce);
-            }
-          }
+          seg_done |= 1u << sgi;
         }
       }
       if (rid < 0 && !exhausted) {
@@ -1358,7 +1304,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       if constexpr (W > 1 && YK_SMALL_LANE_LEAF)
         lane_leaves<CLOSEST, UNI>(tb, lb, st, (live && !paused) ? nref : 0u, w0, cand, s_tmin, ntris, occ);
       else
-        coop_leaves<CLOSEST, BIG, UNI, W, WPG>(S, tb, lb, st, (live && !paused) ? nref : 0u, w0, keys, cand, otab, s_tmin,
+        coop_leaves<CLOSEST, BIG, UNI, W>(S, tb, lb, st, (live && !paused) ? nref : 0u, w0, keys, cand, otab, s_tmin,
                                            ntris, occ);
 #ifdef YK_TRAV_STATS
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -1409,7 +1355,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
           }
           npend += (unsigned)__popcll(fm);
           if (npend >= 64u) {
-            wave_lds_sync<WPG>();
+            wave_lds_sync<W>();
             const int l = lane_fresh();
             const unsigned e = res_slot[l];
 #ifndef YK_NO_SHADOW_RESULTS  // attribution experiment only (PMC WRITE_SIZE without the result stores)
@@ -1417,7 +1363,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 #endif
             if (l + 64u < npend) res_slot[l] = res_slot[l + 64];
             npend -= 64u;
-            wave_lds_sync<WPG>();
+            wave_lds_sync<W>();
           }
         }
       }
@@ -1481,7 +1427,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   }
 #endif
   if (!CLOSEST && !TS && npend) {  // the staged results left
-    wave_lds_sync<WPG>();
+    wave_lds_sync<W>();
     const int l = lane_fresh();
     if ((unsigned)l < npend) {
       const unsigned e = res_slot[l];
@@ -1534,26 +1480,18 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 #ifndef YK_SHADOW_WAVES
 #define YK_SHADOW_WAVES 7
 #endif
-// waves per workgroup sharing one hand-out super-chunk (trace_body G)
-#ifndef YK_SHADOW_G
-#define YK_SHADOW_G 1
-#endif
-#ifndef YK_CLOSEST_G
-#define YK_CLOSEST_G 1
-#endif
-__global__ void __launch_bounds__(64 * YK_CLOSEST_G) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
 k_trace_closest(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                 yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                 unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<true, 8, false, false, false, 1, YK_CLOSEST_G>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth,
-                                                             refill_min);
+  trace_body<true, 8>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
-__global__ void __launch_bounds__(64 * YK_SHADOW_G) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
 k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
                yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false, YK_SHADOW_SEGS, false, false, false, 1, YK_SHADOW_G>(S, rays, idx, n, hits, occl, work, ctr, ovf,
-                                                                        ovf_depth, refill_min);
+  trace_body<false, YK_SHADOW_SEGS>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 // trees with a leaf of 2^17 references or more (coop_leaves BIG)
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
@@ -4036,12 +3974,10 @@ template <bool CLOSEST>
 void enqueue_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* idx, RayCount n, yk_hit* hits,
                    uint8_t* occ, unsigned long long* work, unsigned long long* acc, hipEvent_t ev0, hipEvent_t ev1) {
   const bool small = d->small && !d->big_leaves;
-  // waves per workgroup (per_cu counts workgroups)
-  const int waves = small ? YK_SMALL_W : d->big_leaves ? 1 : CLOSEST ? YK_CLOSEST_G : (d->S.uni ? 1 : YK_SHADOW_G);
+  const int waves = small ? YK_SMALL_W : 1;  // per workgroup
   const long long per_cu = small ? d->per_cu_small[(!CLOSEST && d->S.uni) ? 2 : (int)CLOSEST]
                            : d->big_leaves ? d->per_cu_big[CLOSEST]
-                           : (!CLOSEST && d->S.uni) ? d->per_cu[0] * YK_SHADOW_G  // one-wave groups, same wave count
-                                                    : d->per_cu[CLOSEST];
+                                           : d->per_cu[CLOSEST];
   const long long grid = (long long)d->cus * per_cu;
   const int ovf_depth = std::max(1, stack_depth(d) - (small ? YK_SMALL_RING : (CLOSEST ? kStackLdsC : kStackLds)));
   P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64 * waves);
@@ -4240,9 +4176,9 @@ int yk_device_open(int32_t ordinal, yk_device** out) {
   for (auto& e : d->gather_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   d->stream = d->pipe[0].stream;
   int blocks = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow, 64 * YK_SHADOW_G, 0));
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow, 64, 0));
   d->per_cu[0] = std::max(1, blocks);
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_closest, 64 * YK_CLOSEST_G, 0));
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_closest, 64, 0));
   d->per_cu[1] = std::max(1, blocks);
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow_big, 64, 0));
   d->per_cu_big[0] = std::max(1, blocks);
@@ -4253,9 +4189,9 @@ int yk_device_open(int32_t ordinal, yk_device** out) {
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_pm_lookup<false>, 64, 0));
   d->per_cu_lookup[0] = std::max(1, blocks);
   if (const char* v = std::getenv("YK_VERBOSE"); v && std::atoi(v) > 0)
-    std::fprintf(stderr, "[libyk] %d CUs; resident workgroups per CU: any-hit %d (x%d waves), closest %d (x%d), "
-                 "big %d / %d, transparent-shadow %d\n", d->cus, d->per_cu[0], YK_SHADOW_G, d->per_cu[1],
-                 YK_CLOSEST_G, d->per_cu_big[0], d->per_cu_big[1], d->per_cu_ts);
+    std::fprintf(stderr, "[libyk] %d CUs; resident workgroups per CU: any-hit %d, closest %d, big %d / %d, "
+                 "transparent-shadow %d\n", d->cus, d->per_cu[0], d->per_cu[1], d->per_cu_big[0], d->per_cu_big[1],
+                 d->per_cu_ts);
   upload_qmc();
   *out = d;
   return YK_OK;

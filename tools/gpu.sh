@@ -69,6 +69,11 @@ for s in "$@"; do
     A=""; [ $s = prof_c2 ] && A="$C2"; [ $s = prof_hair ] && A="$HAIR"; [ $s = prof_pm ] && A="$PM"
     timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$s -o p1 -- python3 bench.py $A $P1 > $O/$s.log 2>&1
     echo "$s done" ;;
+  prof1:*)
+    # one-pipe headline frame, rocprofv3 --kernel-trace --stats, with VARIANT[@ENV]
+    v=${s#prof1:}
+    env $(envv $v) YK_LIB=$(lib $v) timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof1_${v//[@=]/_} -o p1 -- python3 bench.py $P1 > $O/prof1_${v//[@=]/_}.log 2>&1
+    echo "prof1 $v done" ;;
   pmc|pmc_c2|pmc_hair)
     A=""; [ $s = pmc_c2 ] && A="$C2"; [ $s = pmc_hair ] && A="$HAIR"
     timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/${s}_fetch -o f -- python3 bench.py $A $P1 > $O/${s}_fetch.log 2>&1
@@ -81,7 +86,8 @@ for s in "$@"; do
     cat $O/tbs_$v.json ;;
   tb:*)
     v=${s#tb:}
-    YK_LIB=$(lib $v) timeout -k 10 200 python -u tools/trav_bench.py --spp 4 > $O/tb_$v.json 2> $O/tb_$v.err
+    env $(envv $v) YK_VERBOSE=1 YK_LIB=$(lib $v) timeout -k 10 200 python -u tools/trav_bench.py --spp 4 > $O/tb_$v.json 2> $O/tb_$v.err
+    grep libyk $O/tb_$v.err || true
     cat $O/tb_$v.json ;;
   ab:*|abc2:*|abpm:*|abhair:*)
     VS=$(echo ${s#*:} | tr , ' ')
