@@ -1172,14 +1172,7 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   const unsigned seg_len = (unsigned)((n + NSEG - 1) / NSEG);
   unsigned pool_next = 0, pool_end = 0;
   unsigned seg_done = 0;  // bit s: segment s has no chunks left
-  // Tail zone (YK_TAIL_ZONE > 0): once a wave has seen its segment's counter
-  // within YK_TAIL_ZONE chunks per wave of the segment's end, or steals from
-  // another segment, it takes 64-ray chunks: a wave that takes a large chunk
-  // as the queue runs out traces it alone while the others drain.
-#ifndef YK_TAIL_ZONE
-#define YK_TAIL_ZONE 0
-#endif
-  bool in_tail = false;
+
   // per-ray watchdog: a valid traversal visits every node at most once, so a
   // ray whose node visits exceed the tree's node count is looping through a
   // corrupt tree; checked every 32nd wave iteration against the lane's node
@@ -1210,17 +1203,12 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
           if (seg_done & (1u << sgi)) continue;
           const unsigned long long s0 = (unsigned long long)sgi * seg_len;
           const unsigned long long s1 = min(s0 + seg_len, (unsigned long long)n);
-          unsigned take = kPoolChunk;
-          if (YK_TAIL_ZONE > 0 && (in_tail || k > 0)) take = 64u;
           unsigned long long base = 0;
-          if (lane == 0) base = atomicAdd(work + 16 * sgi, (unsigned long long)take);
+          if (lane == 0) base = atomicAdd(work + 16 * sgi, (unsigned long long)kPoolChunk);
           base = s0 + shfl_u64(base, 0);
           if (base < s1) {
             cb = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)base);
-            ce = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)min(base + take, s1));
-            if (YK_TAIL_ZONE > 0 && k == 0 &&
-                base + (unsigned long long)YK_TAIL_ZONE * kPoolChunk * (gridDim.x * W / NSEG + 1) >= s1)
-              in_tail = true;
+            ce = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)min(base + kPoolChunk, s1));
             break;
           }
           seg_done |= 1u << sgi;
@@ -1443,10 +1431,12 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
     a += shfl_u64(a, lane ^ off);
     b += shfl_u64(b, lane ^ off);
   }
+#ifndef YK_NO_END_ATOMICS  // attribution experiment only (counters wrong): the cost of the waves' end atomics
   if (lane == 0 && (a | b)) {  // waves that traced nothing add nothing
     atomicAdd(&ctr[0], a);
     atomicAdd(&ctr[1], b);
   }
+#endif
   if (nerr) atomicAdd(&ctr[2], (unsigned long long)nerr);
 }
 
@@ -4628,13 +4618,15 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   }();
   const int regions = merged ? p->bounces + 1 : 1;
   // HBM for the batch buffers of all pipes (YK_BATCH_GB, default 64 of the
-  // 288 GB, 128 with the merged launch's slot regions)
+  // 288 GB, 192 with the merged launch's slot regions: C2's eight slots per
+  // sample in five regions at 128 GB cut its batches from 16M to 12.6M
+  // samples, six batches on four pipes, -5 %; at 192 GB it keeps four)
   static const long long batch_gb_env = [] {
     const char* e = std::getenv("YK_BATCH_GB");
     const long long v = e ? std::atoll(e) : 0;
     return (v > 0 && v <= 240) ? v : 0ll;
   }();
-  const long long batch_bytes = (batch_gb_env ? batch_gb_env : (merged ? 128ll : 64ll)) << 30;
+  const long long batch_bytes = (batch_gb_env ? batch_gb_env : (merged ? 192ll : 64ll)) << 30;
   // + per extra region: 54 B per slot (ray, contribution, flag, result,
   // region and merged queue entries) and 32 B of path state per sample
   const long long bytes_per_sample = 400 + 52ll * K + (long long)(regions - 1) * (54ll * K + 32);
