@@ -2876,9 +2876,16 @@ __global__ void __launch_bounds__(256) k_concat_shadow(const unsigned* __restric
 // per-bounce resolves. A sample's path entered depth 1 iff its camera hit was
 // diffuse (k_shade_primary's first segment), and depth d+1 iff depth d set
 // PS_CONT, so no stale region state is read.
+// k_finish is folded in: the final sample col + pathCol / nSamples (path
+// tracing, diffuse camera hit) with its alpha, the same operations.
 __global__ void __launch_bounds__(256) k_resolve_merged(Batch B, RenderConst R, long long nc, int bounces) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= nc || !(B.prim_hit[c] & PH_DIFFUSE)) return;
+  if (c >= nc) return;
+  c3 col = C3(B.col[3 * c], B.col[3 * c + 1], B.col[3 * c + 2]);
+  if (!(B.prim_hit[c] & PH_DIFFUSE)) {
+    B.samples[c] = make_float4(col.r, col.g, col.b, B.alpha[c]);
+    return;
+  }
   {
     c3 dl = C3(0.f, 0.f, 0.f);
     int k0 = 0;
@@ -2886,11 +2893,8 @@ __global__ void __launch_bounds__(256) k_resolve_merged(Batch B, RenderConst R, 
       dl = cadd(dl, resolve_light(B, c, k0, l));
       k0 += c_lights[l].nslots;
     }
-    B.col[3 * c] = B.col[3 * c] + dl.r;
-    B.col[3 * c + 1] = B.col[3 * c + 1] + dl.g;
-    B.col[3 * c + 2] = B.col[3 * c + 2] + dl.b;
+    col = C3(col.r + dl.r, col.g + dl.g, col.b + dl.b);
   }
-  if (bounces < 1) return;
   c3 thr = C3(B.thr[3 * c], B.thr[3 * c + 1], B.thr[3 * c + 2]);
   c3 pc = C3(B.pathcol[3 * c], B.pathcol[3 * c + 1], B.pathcol[3 * c + 2]);
   for (int depth = 1; depth <= bounces; ++depth) {
@@ -2908,9 +2912,9 @@ __global__ void __launch_bounds__(256) k_resolve_merged(Batch B, RenderConst R, 
     if (!(ps & PS_CONT)) break;
     thr = C3(thr.r * Bd.scol_next[3 * c], thr.g * Bd.scol_next[3 * c + 1], thr.b * Bd.scol_next[3 * c + 2]);
   }
-  B.pathcol[3 * c] = pc.r;
-  B.pathcol[3 * c + 1] = pc.g;
-  B.pathcol[3 * c + 2] = pc.b;
+  const float ns = (float)R.nsub;  // k_finish
+  col = cadd(col, C3(pc.r / ns, pc.g / ns, pc.b / ns));
+  B.samples[c] = make_float4(col.r, col.g, col.b, B.alpha[c]);
 }
 
 // col += pathCol / nSamples (pathtracer.cc:300-302); final sample (wt = 1)
@@ -4965,8 +4969,9 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
       trace(false, B.s_rays, P.s_idxm.p, RayCount{mword, 0, 0}, nullptr, B.s_occl);
       hipLaunchKernelGGL(k_resolve_merged, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc, bounces);
       HIPCHK(hipGetLastError());
+    } else {
+      hipLaunchKernelGGL(k_finish, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
     }
-    hipLaunchKernelGGL(k_finish, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
     HIPCHK(hipGetLastError());
     }  // !d->spec
     // film: in batch order (tile order), whichever pipe ran the batch
