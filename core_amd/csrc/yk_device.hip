@@ -1172,20 +1172,6 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
   const unsigned seg_len = (unsigned)((n + NSEG - 1) / NSEG);
   unsigned pool_next = 0, pool_end = 0;
   unsigned seg_done = 0;  // bit s: segment s has no chunks left
-  // YK_STATIC_FIRST: a wave's first chunk is fixed (segment gw % NSEG, index
-  // gw / NSEG) instead of taken by an atomic -- every wave of the launch
-  // otherwise hits its segment's counter at the same moment; the counters
-  // then hand out what follows the static chunks (static_len)
-#ifndef YK_STATIC_FIRST
-#define YK_STATIC_FIRST 0
-#endif
-  bool first_done = !YK_STATIC_FIRST;
-  // waves that stay (the early exit above) take the static chunks
-  const unsigned g_eff = (unsigned)min((long long)gridDim.x * W, (n + 126) / 64);
-  auto static_len = [&](unsigned sg) -> unsigned long long {
-    return YK_STATIC_FIRST ? (unsigned long long)(g_eff > sg ? (g_eff - 1u - sg) / (unsigned)NSEG + 1u : 0u) * kPoolChunk
-                           : 0ull;
-  };
 
   // per-ray watchdog: a valid traversal visits every node at most once, so a
   // ray whose node visits exceed the tree's node count is looping through a
@@ -1211,25 +1197,12 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
       const unsigned avail = pool_end - pool_next;
       unsigned cb = 0, ce = 0;  // newly grabbed chunk [cb, ce)
       if (avail < cnt && seg_done != kAll) {
-        bool got = false;
-        if (!first_done) {
-          first_done = true;
-          const unsigned sg = gw % (unsigned)NSEG;
-          const unsigned long long s0 = (unsigned long long)sg * seg_len;
-          const unsigned long long s1 = min(s0 + seg_len, (unsigned long long)n);
-          const unsigned long long base = s0 + (unsigned long long)(gw / (unsigned)NSEG) * kPoolChunk;
-          if (base < s1) {
-            cb = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)base);
-            ce = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)min(base + kPoolChunk, s1));
-            got = true;
-          }
-        }
 #pragma unroll 1  // rolled: an unrolled search held every segment's bounds in SGPRs (spilled to VGPR lanes)
-        for (unsigned k = 0; k < (unsigned)NSEG && !got; ++k) {
+        for (unsigned k = 0; k < (unsigned)NSEG; ++k) {
           const unsigned sgi = (xcc + k) % (unsigned)NSEG;
           if (seg_done & (1u << sgi)) continue;
-          const unsigned long long s0 = (unsigned long long)sgi * seg_len + static_len(sgi);
-          const unsigned long long s1 = min((unsigned long long)sgi * seg_len + seg_len, (unsigned long long)n);
+          const unsigned long long s0 = (unsigned long long)sgi * seg_len;
+          const unsigned long long s1 = min(s0 + seg_len, (unsigned long long)n);
           unsigned long long base = 0;
           if (lane == 0) base = atomicAdd(work + 16 * sgi, (unsigned long long)kPoolChunk);
           base = s0 + shfl_u64(base, 0);
@@ -1458,12 +1431,10 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
     a += shfl_u64(a, lane ^ off);
     b += shfl_u64(b, lane ^ off);
   }
-#ifndef YK_NO_END_ATOMICS  // attribution experiment only (counters wrong): the cost of the waves' end atomics
   if (lane == 0 && (a | b)) {  // waves that traced nothing add nothing
     atomicAdd(&ctr[0], a);
     atomicAdd(&ctr[1], b);
   }
-#endif
   if (nerr) atomicAdd(&ctr[2], (unsigned long long)nerr);
 }
 
