@@ -1006,12 +1006,18 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
 // slot (used by the shadow queue, whose rays sit in per-sample slots).
 // Number of rays of a launch: a host value, or a 32-bit field of a device
 // queue-count word (so launches need no host round trip).
+// nsum > 1: the sum of the fields of nsum consecutive words (the merged
+// shadow queue: one count word per slot region)
 struct RayCount {
   const unsigned long long* word;
   int shift;
   long long host;
+  int nsum = 1;
   __device__ __forceinline__ long long get() const {
-    return word ? (long long)((*word >> shift) & 0xFFFFFFFFull) : host;
+    if (!word) return host;
+    long long t = 0;
+    for (int i = 0; i < nsum; ++i) t += (long long)((word[i] >> shift) & 0xFFFFFFFFull);
+    return t;
   }
 };
 
@@ -2092,6 +2098,11 @@ struct Batch {
   int K;
   long long cap;  // samples per batch: the stride of the shadow-slot arrays
   long long slot_base;  // merged shadow launch: first slot of this bounce's slot region (0 otherwise)
+  // merged shadow launch: the regions' queue-count words (region r's count in
+  // the low half of mq_words[r]); a bounce kernel writes its queue entries
+  // after those of the regions before it (complete, earlier in the stream)
+  const unsigned long long* mq_words;
+  int mq_region;
   // specular recursion (recursiveRaytrace) only, see k_spawn / k_fold
   unsigned* psample;    // pixel sample index of each entry (state.pixelSample)
   uint8_t* incl;        // state.includeLights after the entry's path loop
@@ -2681,6 +2692,9 @@ __attribute__((amdgpu_waves_per_eu(DIFF ? YK_BOUNCE_WAVES_D : YK_BOUNCE_WAVES)))
   const long long nq = (long long)(*qin_word >> 32);  // live paths (device-side count)
   const long long qb = (long long)blockIdx.x * blockDim.x;
   if (qb >= nq) return;  // whole block past the queue
+  unsigned qpre = 0;  // merged shadow queue: after the earlier regions' entries
+  if (B.mq_words)
+    for (int r = 0; r < B.mq_region; ++r) qpre += (unsigned)B.mq_words[r];
   long long qi = qb + threadIdx.x;
   bool valid = qi < nq;
   // Escaped paths (most first-bounce rays of an open scene) finish here; the
@@ -2786,7 +2800,7 @@ __attribute__((amdgpu_waves_per_eu(DIFF ? YK_BOUNCE_WAVES_D : YK_BOUNCE_WAVES)))
   }
   unsigned sbase, qn;
   wave_append2<YK_BOUNCE_APPEND_WAVE>(qword, valid ? (unsigned)nr : 0u, emit_next ? 1u : 0u, sbase, qn);
-  if (valid) flush_shadow(B, c, kend, nr, sbase, traced);
+  if (valid) flush_shadow(B, c, kend, nr, sbase + qpre, traced);
   if (emit_next) {
     st_ray(&B.q_rays[qin ^ 1][qn], nxt);
     B.q_owner[qin ^ 1][qn] = (int)c;
@@ -2834,14 +2848,15 @@ __global__ void __launch_bounds__(256) k_resolve_bounce(Batch B, RenderConst R,
 // it four times. The bounces' shadow rays do not feed the next bounce (its
 // closest rays come from the BSDF sample alone), only the resolve, which then
 // runs once per batch over all bounces in the reference's order: every bounce
-// writes its own slot region (slot_base), path state (pstate, lsel, emit_b,
-// scol_next at (depth-1)*cap) and queue region of slot indices.
+// writes its own slot region (slot_base) and path state (pstate, lsel,
+// emit_b, scol_next at (depth-1)*cap), and appends its slot indices to the
+// one queue after those of the regions before it (mq_words).
 
 // Batch view of bounce `depth`'s slot region and path state (host and device)
 __host__ __device__ inline Batch merged_region(Batch B, int depth) {
   const long long rs = (long long)B.K * B.cap;
   B.slot_base = (long long)depth * rs;
-  B.s_idx += depth * rs;
+  B.mq_region = depth;
   if (depth >= 1) {
     const long long o = (long long)(depth - 1) * B.cap;
     B.pstate += o;
@@ -2850,23 +2865,6 @@ __host__ __device__ inline Batch merged_region(Batch B, int depth) {
     B.scol_next += 3 * o;
   }
   return B;
-}
-
-// the regions' queued slot indices, concatenated in region order into one
-// queue (idxm) with its count in low 32 bits of *mword; qw0: region 0's count
-// word, qstride: words between the regions' count words
-__global__ void __launch_bounds__(256) k_concat_shadow(const unsigned* __restrict__ idx, unsigned* __restrict__ idxm,
-                                                       const unsigned long long* __restrict__ qw0, int regions,
-                                                       long long rstride, unsigned long long* __restrict__ mword) {
-  unsigned long long off = 0;
-  for (int r = 0; r < regions; ++r) {
-    const unsigned long long n = qw0[r] & 0xFFFFFFFFull;
-    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (unsigned long long)gridDim.x * blockDim.x)
-      idxm[off + i] = idx[(unsigned long long)r * rstride + i];
-    off += n;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) *mword = off;
 }
 
 // k_resolve_primary, then k_resolve_bounce for depth 1..bounces, per camera
@@ -3394,7 +3392,7 @@ struct Pipe {
   DBuf<unsigned long long> words;     // per-render: queue-count words, ray segments, accumulators
   DBuf<uint2> ovf;                    // traversal stack overflow (entries deeper than the LDS ring)
   std::vector<hipEvent_t> evpool;     // per-launch timing events of one render
-  DBuf<unsigned> soffs, s_idx, s_idxm;
+  DBuf<unsigned> soffs, s_idx;
   DBuf<float> col, alpha, thr, pathcol, scol_next, wlast, emit_b, sl_contrib;
   DBuf<int> prim_hit, pstate, lsel, qo0, qo1, tile_base;
   DBuf<int4> tiles;
@@ -3456,7 +3454,6 @@ struct Pipe {
     s_rays.ensure(maxc * K * regions);
     s_occl.ensure(maxc * K * regions);
     s_idx.ensure(maxc * K * regions);
-    if (regions > 1) s_idxm.ensure(maxc * K * regions);
     sl_contrib.ensure(3 * maxc * K * regions);
     sl_flags.ensure(maxc * K * regions);
     samples.ensure(maxc);
@@ -4629,9 +4626,9 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     return (v > 0 && v <= 240) ? v : 0ll;
   }();
   const long long batch_bytes = (batch_gb_env ? batch_gb_env : (merged ? 192ll : 64ll)) << 30;
-  // + per extra region: 54 B per slot (ray, contribution, flag, result,
-  // region and merged queue entries) and 32 B of path state per sample
-  const long long bytes_per_sample = 400 + 52ll * K + (long long)(regions - 1) * (54ll * K + 32);
+  // + per extra region: 50 B per slot (ray, contribution, flag, result,
+  // queue entry) and 32 B of path state per sample
+  const long long bytes_per_sample = 400 + 52ll * K + (long long)(regions - 1) * (50ll * K + 32);
   const int pipes_cfg = pipes_env();
   const long long target = std::max(1ll << 20, std::min(target_env, batch_bytes / pipes_cfg / bytes_per_sample));
   const long long tile_samples = (long long)F.tile * F.tile * spp;
@@ -4728,8 +4725,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   // All zeroed once; no launch needs a reset or a host round trip.
   const int qwords_per_batch = nsub * (bounces + 1);
   const int launches_per_batch = 2 + 2 * nsub * bounces + (R.pm_fg ? nsub * bounces : 0);
-  // + the merged shadow queue's count word
-  const long long words_per_batch = 2ll * qwords_per_batch + 128ll * launches_per_batch + 1;
+  const long long words_per_batch = 2ll * qwords_per_batch + 128ll * launches_per_batch;
   Batch Bp[kPipes];
   for (int pi = 0; pi < npipes; ++pi) {
     Pipe& P = d->pipe[pi];
@@ -4947,7 +4943,11 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
         const unsigned long long* in_w = qw(isub, depth - 1);
         unsigned long long* out_w = qw(isub, depth);
         trace(true, B.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, B.q_hits[qin], nullptr);
-        const Batch Bd = merged ? merged_region(B, depth) : B;
+        Batch Bd = B;
+        if (merged) {
+          Bd = merged_region(B, depth);
+          Bd.mq_words = qw(0, 0);
+        }
         hipLaunchKernelGGL(d->diff_only ? k_shade_bounce<true> : k_shade_bounce<false>, dim3(grid_for(nc, bounce_block(d->diff_only))), dim3(bounce_block(d->diff_only)), 0, P.stream, d->S, Bd, R, in_w, depth, isub,
                            qin, out_w);
         HIPCHK(hipGetLastError());
@@ -4960,11 +4960,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
       }
     }
     if (merged) {  // one any-hit launch for the camera hits and all bounces, then one resolve
-      unsigned long long* mword = bw + 2ll * qwords_per_batch + 128ll * launches_per_batch;
-      hipLaunchKernelGGL(k_concat_shadow, dim3(1024), dim3(256), 0, P.stream, B.s_idx, P.s_idxm.p, qw(0, 0),
-                         regions, (long long)K * maxc, mword);
-      HIPCHK(hipGetLastError());
-      trace(false, B.s_rays, P.s_idxm.p, RayCount{mword, 0, 0}, nullptr, B.s_occl);
+      trace(false, B.s_rays, B.s_idx, RayCount{qw(0, 0), 0, 0, regions}, nullptr, B.s_occl);
       hipLaunchKernelGGL(k_resolve_merged, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc, bounces);
       HIPCHK(hipGetLastError());
     } else {

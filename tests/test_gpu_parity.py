@@ -260,25 +260,33 @@ def test_shading_instantiations_photon(gpu_device, monkeypatch, diff):
 
 
 @pytest.mark.parametrize("merge", ["0", "1"])
-@pytest.mark.parametrize("case", [("cornell_pt", 64, 64, 0, 0), ("bumpy", 48, 32, 120, 61), ("smooth_inst", 48, 48, 0, 0)],
-                         ids=["cornell", "bumpy", "smooth_inst"])
-def test_merged_shadow_launch(gpu_device, monkeypatch, case, merge):
+@pytest.mark.parametrize("case,over", [
+    (("cornell_pt", 64, 64, 0, 0), {}), (("bumpy", 48, 32, 120, 61), {}), (("smooth_inst", 48, 48, 0, 0), {}),
+    # several lights (estimateOneDirectLight's light choice, lsel per bounce region) and a background
+    (("dirac_pt", 48, 48, 0, 0), {"bounces": 4}),
+    # adaptive passes: pixel sample indices from B.psample in every region
+    (("cornell_pt", 48, 48, 0, 0), {"aa_passes": 3, "aa_inc_samples": 2, "aa_threshold": 0.05})],
+    ids=["cornell", "bumpy", "smooth_inst", "dirac", "aa3"])
+def test_merged_shadow_launch(gpu_device, monkeypatch, case, over, merge):
     """Path tracing with one any-hit launch per batch for the camera hits and
-    every bounce (k_concat_shadow + k_resolve_merged) and with one launch per
-    bounce (YK_MERGE=0): both equal the oracle bit for bit, ray counts
-    included; the merged frame has one any-hit launch per batch."""
+    every bounce (the queue regions written in place + k_resolve_merged) and
+    with one launch per bounce (YK_MERGE=0): both equal the oracle bit for
+    bit, ray counts included; the merged frame has one any-hit launch per
+    batch."""
     monkeypatch.setenv("YK_MERGE", merge)
     s, p, orc = scene(*case)
     q = A.yk_render_params.from_buffer_copy(p)
     q.aa_samples = 4
     q.bounces = 3
+    for k, v in over.items():
+        setattr(q, k, v)
     rgba_o, sums_o, cnt = orc.render(q)
     gpu_device.upload(s)
     film = gpu_device.new_film(q)
     st = gpu_device.render_shard(q, film)
     assert st.closest_rays == cnt["closest"] and st.shadow_rays == cnt["shadow"]
     assert (film.cpu().numpy().view(np.uint32) == sums_o.view(np.uint32)).all()
-    per_batch = st.closest_launches // (q.bounces + 1)  # batches (one closest launch per bounce + camera)
+    per_batch = st.closest_launches // (q.bounces + 1)  # batches x passes (one closest launch per bounce + camera)
     assert st.shadow_launches == (per_batch if merge == "1" else per_batch * (q.bounces + 1))
 
 
