@@ -4064,14 +4064,18 @@ constexpr uint32_t kBigLeaf = 1u << 17;
 
 // Ray hand-out per scene: crowded-leaf trees (costly, uneven rays) take
 // 64-ray chunks. Refill threshold (idle lanes a wave collects before it
-// fetches new rays): 24, and 48 for the any-hit kernels on trees of at most
+// fetches new rays): 24 (closest hit), 16 (any hit), and 48 for the any-hit kernels on trees of at most
 // 2^16 nodes, whose cheap shadow rays make the refill's two dependent loads a
 // larger share of a wave's time. Round 3, headline (1M tris) at 16 / 24 / 32:
 // 2867 / 2915 / 2902 Mrays/s (any-hit kernel alone 2959 / 2971 / 2919); C2
 // (36 tris), both kernels at 16 / 24 / 32 / 40 / 48 / 56 / 64: 8442 / 8669 /
 // 8710 / 8791 / 8788 / 8716 / 8426; closest : any-hit at 40:40 / 24:40 /
 // 24:48 / 32:48 / 24:56 (3 runs each, one box): 8784 / 8851 / 8938 / 8928 /
-// 8889. YK_REFILL / YK_REFILL_SHADOW override (tuning). (Round 3 also tried 4 chunks per wave instead of 16 for trees
+// 8889. Round 6, with the merged shadow launch (one larger any-hit launch
+// per batch), the any-hit kernel on large trees at 12 / 16 / 20 / 24 (two
+// reps, one box): headline 3505-3514 / 3499-3507 / 3484-3495 / 3485-3494,
+// both kernels at 16: 3436-3442; the any-hit threshold is 16 since.
+// YK_REFILL / YK_REFILL_SHADOW override (tuning). (Round 3 also tried 4 chunks per wave instead of 16 for trees
 // of at most 2^16 nodes, as a per-scene value: the runtime divisor made the
 // closest-hit kernel spill 9 VGPRs instead of 4, headline 2904 against 2950,
 // for no C2 gain in the same A/B: 8927 against 8925.)
@@ -4091,7 +4095,7 @@ void set_handout(yk_device* d, size_t nn) {
   const char* e = std::getenv("YK_REFILL_SHADOW");
   const int rs = e ? std::atoi(e) : 0;
   d->refill = refill_env() ? refill_env() : 24;
-  d->refill_shadow = (rs >= 1 && rs <= 64) ? rs : (refill_env() ? refill_env() : (nn <= (1u << 16) ? 48 : 24));
+  d->refill_shadow = (rs >= 1 && rs <= 64) ? rs : (refill_env() ? refill_env() : (nn <= (1u << 16) ? 48 : 16));
   d->S.chunk_max = d->crowded_leaves ? 64u : (unsigned)YK_POOL_CHUNK_MAX;
 }
 
