@@ -2137,6 +2137,7 @@ struct RenderConst {
   float d1;       // 1/spp as renderTile computes it
   int pm_fg;      // photon mapping with final gathering: col += pathCol / nSampl at the finish
   int pm_showmap; // photon mapping show_map: no direct light
+  int merged;     // merged shadow launch: pathCol lives in k_resolve_merged's registers from 0
 };
 
 // ------------------------------------------------------------ kernels
@@ -2573,9 +2574,11 @@ __global__ void __launch_bounds__(YK_PRIMARY_BLOCK) k_shade_primary(DScene S, Ba
       B.emit0[3 * c + 1] = em.g;
       B.emit0[3 * c + 2] = em.b;
     }
-    B.pathcol[3 * c] = 0.f;
-    B.pathcol[3 * c + 1] = 0.f;
-    B.pathcol[3 * c + 2] = 0.f;
+    if (!R.merged) {
+      B.pathcol[3 * c] = 0.f;
+      B.pathcol[3 * c + 1] = 0.f;
+      B.pathcol[3 * c + 2] = 0.f;
+    }
     if (!emit) B.wlast[c] = 0.f;
   }
   unsigned sbase, q;
@@ -2892,7 +2895,7 @@ __global__ void __launch_bounds__(256) k_resolve_merged(Batch B, RenderConst R, 
     col = C3(col.r + dl.r, col.g + dl.g, col.b + dl.b);
   }
   c3 thr = C3(B.thr[3 * c], B.thr[3 * c + 1], B.thr[3 * c + 2]);
-  c3 pc = C3(B.pathcol[3 * c], B.pathcol[3 * c + 1], B.pathcol[3 * c + 2]);
+  c3 pc = C3(0.f, 0.f, 0.f);  // pathCol = 0 (k_shade_primary leaves it unstored for merged batches)
   for (int depth = 1; depth <= bounces; ++depth) {
     const Batch Bd = merged_region(B, depth);
     const int ps = Bd.pstate[c];
@@ -4620,6 +4623,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
            !p->transp_shadows && p->path_samples <= 1 && p->bounces >= 1;
   }();
   const int regions = merged ? p->bounces + 1 : 1;
+  R.merged = merged ? 1 : 0;
   // HBM for the batch buffers of all pipes (YK_BATCH_GB, default 64 of the
   // 288 GB, 192 with the merged launch's slot regions: C2's eight slots per
   // sample in five regions at 128 GB cut its batches from 16M to 12.6M
