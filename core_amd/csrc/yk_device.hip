@@ -782,15 +782,6 @@ __device__ __forceinline__ void wave_lds_sync() {
   }
 }
 
-// Early u < 0 rejection in the leaf tests (mt_intersect EARLY): YK_MT_EARLY 0
-// off, 1 in the small-scene kernels (W > 1, VALU-bound), 2 in every
-// traversal kernel
-#ifndef YK_MT_EARLY
-#define YK_MT_EARLY 0
-#endif
-template <int W>
-constexpr bool kMtEarly = YK_MT_EARLY >= 2 || (YK_MT_EARLY >= 1 && W > 1);
-
 // tb / lb: the triangle records by prim and in leaf order (S.tris / S.ltris,
 // or their LDS copies: W > 1, 48-B records)
 template <bool CLOSEST, bool BIG = false, bool UNI = false, int W = 1>
@@ -862,7 +853,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, const float* tb, co
           asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
                        "+v"(E2.y), "+v"(E2.z));
           float th, u, v;
-          if (mt_intersect<kMtEarly<W>>(V3(A.x, A.y, A.z), V3(E1.x, E1.y, E1.z), V3(E2.x, E2.y, E2.z), ro, rd, th, u,
+          if (mt_intersect(V3(A.x, A.y, A.z), V3(E1.x, E1.y, E1.z), V3(E2.x, E2.y, E2.z), ro, rd, th, u,
                                         v) &&
               th < rz && th >= rtmin)
             atomicMin(&keys[own], k);
@@ -927,7 +918,7 @@ __device__ __forceinline__ void coop_leaves(const DScene& S, const float* tb, co
       ld_tri<TW>(tp, A, E1, E2);
       asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(E1.x), "+v"(E1.y), "+v"(E1.z), "+v"(E2.x),
                    "+v"(E2.y), "+v"(E2.z));
-      if (mt_intersect<kMtEarly<W>>(V3(A.x, A.y, A.z), V3(E1.x, E1.y, E1.z), V3(E2.x, E2.y, E2.z), ro, rd, th, u,
+      if (mt_intersect(V3(A.x, A.y, A.z), V3(E1.x, E1.y, E1.z), V3(E2.x, E2.y, E2.z), ro, rd, th, u,
                                     v)) {
         valid = th < rz && th >= rtmin;
         if (valid) {
@@ -987,7 +978,7 @@ __device__ __forceinline__ void lane_leaves(const float* tb, const float* lb, Tr
     float4 A, E1, E2;
     ld_tri<12u>(tp, A, E1, E2);
     float th, u, v;
-    if (mt_intersect<kMtEarly<2>>(V3(A.x, A.y, A.z), V3(E1.x, E1.y, E1.z), V3(E2.x, E2.y, E2.z), st.o, st.d, th, u,
+    if (mt_intersect(V3(A.x, A.y, A.z), V3(E1.x, E1.y, E1.z), V3(E2.x, E2.y, E2.z), st.o, st.d, th, u,
                                   v)) {
       if (CLOSEST) {
         if (th < st.Z && th >= tmin) {

@@ -260,22 +260,14 @@ __device__ __forceinline__ v3 sample_cos_hemisphere(v3 N, v3 Ru, v3 Rv, float s1
 }
 
 // Moller-Trumbore on a triangle given as (a, e1=b-a, e2=c-a); triangle_inline.h:27-64
-// EARLY: the u < 0 rejection before the (correctly rounded) division, where
-// it is decided exactly: u = RN(tp * RN(1/det)) is negative iff tp and det
-// have opposite signs and the product does not round to -0; with
-// |tp| >= 2^-100 and |det| <= 2^40 (so |RN(1/det)| >= 2^-40) it is at least
-// 2^-140 in magnitude. NaN and the other cases take the division.
-template <bool EARLY = false>
 __device__ __forceinline__ bool mt_intersect(v3 a, v3 e1, v3 e2, v3 from, v3 dir, float& t, float& b1,
                                              float& b2) {
   v3 pvec = vcross(dir, e2);
   float det = vdot(e1, pvec);
   if (det == 0.0f) return false;
-  v3 tvec = vsub(from, a);
-  const float tp = vdot(tvec, pvec);
-  if (EARLY && ((tp < 0.0f) != (det < 0.0f)) && fabsf(tp) >= 0x1p-100f && fabsf(det) <= 0x1p40f) return false;
   float inv_det = 1.0f / det;
-  float u = tp * inv_det;
+  v3 tvec = vsub(from, a);
+  float u = vdot(tvec, pvec) * inv_det;
   if (u < 0.0f || u > 1.0f) return false;
   v3 qvec = vcross(tvec, e1);
   float v = vdot(dir, qvec) * inv_det;
