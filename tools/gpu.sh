@@ -24,6 +24,7 @@
 #   coh:VARIANT          primary-shadow ray-order experiment (tools/coherence_bench.py)
 #   pmctb:VARIANT        PMC counter passes over the traversal microbenchmark (tools/pmc_dump.py summary)
 #   multi                tests/test_multi_device.py + tests/test_0_multi_process.py
+#   shard                projected strong scaling (rank 0's share of the headline frame, N = 1/2/4/8)
 #   pmcw:VARIANT         WRITE_SIZE passes (one-pipe headline frame, traversal microbenchmark)
 #   pmcb:c2|head         the pmctb counter sets over a one-pipe frame, every kernel
 #   mallocs              hipMalloc count of 1 vs 3 yk_render_multi calls (rocprofv3 --hip-trace)
@@ -178,6 +179,10 @@ for f in glob.glob(sys.argv[1] + "/**/*hip_api_trace.csv", recursive=True):
 print(f"{sys.argv[2]} render_multi call(s): {n} hipMalloc* calls")
 PY
     done ;;
+  shard)
+    # projected strong scaling: rank 0's share of the headline frame for N = 1, 2, 4, 8 (tools/exp_shard.py)
+    timeout -k 10 300 python -u tools/exp_shard.py > $O/shard.txt 2> $O/shard.err
+    cat $O/shard.txt ;;
   multi)
     timeout -k 10 600 python -u -m pytest tests/test_multi_device.py tests/test_0_multi_process.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/multi.txt 2>&1
     tail -3 $O/multi.txt ;;
