@@ -100,6 +100,9 @@ class yk_photon_info(C.Structure):
                 ("ms_total", C.c_double)]
 
 
+YK_TILES_LINEAR, YK_TILES_RANDOM = 0, 1
+
+
 class yk_render_params(C.Structure):
     _fields_ = [("integrator", C.c_int32), ("raydepth", C.c_int32), ("path_samples", C.c_int32),
                 ("bounces", C.c_int32), ("caustic_type", C.c_int32), ("width", C.c_int32),
@@ -108,7 +111,7 @@ class yk_render_params(C.Structure):
                 ("aa_pixelwidth", C.c_float), ("tile_size", C.c_int32),
                 ("transp_background", C.c_int32), ("aa_inc_samples", C.c_int32), ("aa_threshold", C.c_float),
                 ("photon", yk_photon_params), ("transp_shadows", C.c_int32), ("shadow_depth", C.c_int32),
-                ("filter_width", C.c_float)]
+                ("filter_width", C.c_float), ("tile_order", C.POINTER(C.c_int32)), ("tile_order_len", C.c_int32)]
 
     def copy(self):
         p = yk_render_params()
@@ -185,6 +188,7 @@ SIGNATURES = {
     "yk_scene_get_camera_state": (C.c_int, [P, C.POINTER(yk_camera_state)]),
     "yk_scene_generate": (C.c_int, [P, C.c_char_p, i32, i32, i32, i32, C.POINTER(yk_render_params)]),
     "yk_render_params_default": (None, [C.POINTER(yk_render_params)]),
+    "yk_tile_order_random": (C.c_int, [C.c_int32, C.c_uint32, C.POINTER(C.c_int32)]),
     "yk_film_filter_from_table": (C.c_int, [fp, C.c_float, C.POINTER(yk_render_params)]),
     "yk_device_count": (C.c_int, [C.POINTER(i32)]),
     "yk_device_set_abort": (C.c_int, [P, ABORT_FN, P]),

@@ -3124,6 +3124,7 @@ struct FilmConst {
   int olo_x, ohi_x, olo_y, ohi_y;  // target-source offset window
   int shard, nshards;
   int tb0, tb1;                  // batch = owned tile ranks [tb0, tb1)
+  const int* rank_of;            // custom tile order: rank of each tile in the shard's list (-1: not owned); null: row-major
   int spp;
   float d1;
   const int* pmap;  // adaptive pass: batch-local first sample of each film pixel, -1 = not resampled
@@ -3167,8 +3168,9 @@ __global__ void __launch_bounds__(256) k_pixel_extent(FilmConst F, const float2*
 
 // imageFilm_t::addSample as a gather (imagefilm.cc:453-511): each thread owns
 // one target pixel and adds every covering sample of the batch in the
-// reference's single-thread order -- tiles row-major, then rows, columns and
-// samples -- so the float sums match the sequential CPU splat bit for bit.
+// reference's single-thread order -- tiles in the order the film hands them
+// out (row-major, or the tile_order list), then rows, columns and samples --
+// so the float sums match the sequential CPU splat bit for bit.
 // Candidate sources are walked in that order directly: the tiles the filter
 // window touches in row-major tile order, inside each its window rows and
 // columns.
@@ -3189,12 +3191,8 @@ __global__ void __launch_bounds__(256) k_film_gather(FilmConst F, const float4* 
   float* px = film + 5 * ((size_t)(ty - F.cy0) * F.w + (tx - F.cx0));
   float aR = px[0], aG = px[1], aB = px[2], aA = px[3], aW = px[4];
   bool any = false;
-  for (int tr = tr0; tr <= tr1; ++tr)
-    for (int tc = tc0; tc <= tc1; ++tc) {
-      const int ti = tr * F.ntx + tc;
-      if (ti % F.nshards != F.shard) continue;
-      const int rank = ti / F.nshards;
-      if (rank < F.tb0 || rank >= F.tb1) continue;
+  // one tile of the batch: its source pixels in the window, rows, columns, samples
+  auto tile = [&](int tr, int tc, int rank) {
       const int X = F.cx0 + tc * F.tile, Y = F.cy0 + tr * F.tile;
       const int W = min(F.tile, F.cx1 - X);
       const int ya = max(sy0, Y), yb = min(sy1, Y + F.tile - 1);
@@ -3255,7 +3253,36 @@ __global__ void __launch_bounds__(256) k_film_gather(FilmConst F, const float4* 
             }
           }
         }
+  };
+  if (F.rank_of) {
+    // custom order (tiles_order "random"): the window's tiles of the batch by
+    // rank, the smallest rank above the previous one each time
+    int last = -1;
+    for (;;) {
+      int best = INT_MAX, btr = 0, btc = 0;
+      for (int r = tr0; r <= tr1; ++r)
+        for (int q = tc0; q <= tc1; ++q) {
+          const int k = F.rank_of[r * F.ntx + q];
+          if (k > last && k >= F.tb0 && k < F.tb1 && k < best) {
+            best = k;
+            btr = r;
+            btc = q;
+          }
+        }
+      if (best == INT_MAX) break;
+      last = best;
+      tile(btr, btc, best);
     }
+  } else {
+    for (int tr = tr0; tr <= tr1; ++tr)  // row-major tiles
+      for (int tc = tc0; tc <= tc1; ++tc) {
+        const int ti = tr * F.ntx + tc;
+        if (ti % F.nshards != F.shard) continue;
+        const int rank = ti / F.nshards;
+        if (rank < F.tb0 || rank >= F.tb1) continue;
+        tile(tr, tc, rank);
+      }
+  }
   if (!any) return;
   px[0] = aR;
   px[1] = aG;
@@ -3599,7 +3626,7 @@ struct yk_device {
   DBuf<float> mstage[kMaxMultiDev];
   // render_pass's tile lists (grow-only, so repeated renders allocate nothing)
   DBuf<int4> tiles_dev;
-  DBuf<int> base_dev, pix_dev, pmap_dev;
+  DBuf<int> base_dev, pix_dev, pmap_dev, rank_dev;
   DBuf<uint8_t> flags_dev;
   hipStream_t mstream[kMaxMultiDev] = {};
   hipEvent_t mevent[kMaxMultiDev] = {};
@@ -4573,8 +4600,25 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   const int nty = (p->height + F.tile - 1) / F.tile;
   const int ntiles = F.ntx * nty;
   if (ntiles >= (1 << 19)) return set_error(YK_ERR_UNSUPPORTED, "too many tiles");
-  std::vector<int> owned;
-  for (int t = shard; t < ntiles; t += nshards) owned.push_back(t);
+  std::vector<int> owned;  // the shard's tiles in the order the film hands them out
+  std::vector<int> rank_of;  // custom order: tile -> rank in `owned`, -1 other shards' tiles
+  if (p->tile_order && p->tile_order_len > 0) {
+    if (p->tile_order_len != ntiles)
+      return set_error(YK_ERR_ARG, "tile_order must list every tile of the render area once");
+    rank_of.assign((size_t)ntiles, -1);
+    std::vector<char> seen((size_t)ntiles, 0);
+    for (int i = 0; i < ntiles; ++i) {
+      const int t = p->tile_order[i];
+      if (t < 0 || t >= ntiles || seen[(size_t)t]) return set_error(YK_ERR_ARG, "tile_order is not a permutation of the tiles");
+      seen[(size_t)t] = 1;
+      if (t % nshards == shard) {
+        rank_of[(size_t)t] = (int)owned.size();
+        owned.push_back(t);
+      }
+    }
+  } else {
+    for (int t = shard; t < ntiles; t += nshards) owned.push_back(t);
+  }
   bool aborted = false;
   RenderConst R{};
   R.spp = spp;
@@ -4727,6 +4771,12 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     if (!pix_all.empty())
       HIPCHK(hipMemcpy(pix_dev.p, pix_all.data(), pix_all.size() * sizeof(int), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(pmap_dev.p, pmap.data(), pmap.size() * sizeof(int), hipMemcpyHostToDevice));
+  }
+  F.rank_of = nullptr;
+  if (!rank_of.empty()) {  // custom tile order: the film gather walks a window's tiles by rank
+    d->rank_dev.ensure(rank_of.size());
+    HIPCHK(hipMemcpy(d->rank_dev.p, rank_of.data(), rank_of.size() * sizeof(int), hipMemcpyHostToDevice));
+    F.rank_of = d->rank_dev.p;
   }
 
   // ---- per-pipe device words: [0, 2 kAccWords) accumulators {closest

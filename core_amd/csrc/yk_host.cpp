@@ -1,6 +1,8 @@
 // Host half of the C-ABI (include/yk_api.h): scene assembly, kd-tree build,
 // fixture generation, error reporting. No GPU needed; exercised by the CPU
 // tests and by the oracle harness.
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <new>
@@ -349,6 +351,26 @@ int yk_scene_get_camera(const yk_scene* s, yk_camera* out) {
   if (!s->s.has_camera || !s->s.camera_has_params)
     return set_error(YK_ERR_STATE, "scene has no parameter-level camera");
   *out = s->s.camera;
+  return YK_OK;
+}
+
+int yk_tile_order_random(int32_t ntiles, uint32_t seed, int32_t* order_out) {
+  if (ntiles < 0 || (ntiles > 0 && !order_out)) return set_error(YK_ERR_ARG, "yk_tile_order_random: bad arguments");
+  // glibc's rand() is random() on the default TYPE_3 generator (a 128-byte
+  // state); the reentrant random_r on a private state of that size, seeded
+  // like srand(seed), gives the same sequence
+  char state[128];
+  random_data rd{};
+  if (initstate_r(seed, state, sizeof state, &rd) != 0) return set_error(YK_ERR_INTERNAL, "initstate_r failed");
+  for (int32_t i = 0; i < ntiles; ++i) order_out[i] = i;
+  // libstdc++ std::random_shuffle(first, last): for i in [first + 1, last):
+  // j = first + rand() % ((i - first) + 1); swap(*i, *j) when i != j
+  for (int32_t i = 1; i < ntiles; ++i) {
+    int32_t r = 0;
+    random_r(&rd, &r);
+    const int32_t j = r % (i + 1);
+    if (j != i) std::swap(order_out[i], order_out[j]);
+  }
   return YK_OK;
 }
 

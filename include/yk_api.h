@@ -152,7 +152,19 @@ typedef struct yk_render_params {
   float filter_width;      /* imageFilm_t::filterw as the film holds it (> 0), taking
                               precedence over aa_pixelwidth; 0: derived from
                               aa_pixelwidth as imagefilm.cc:143-150 does [0]            */
+  /* The order in which the film hands out its tiles (imageFilm_t::nextArea
+   * over its imageSpliter_t, imagefilm.cc:190-195,291-304): tile_order_len
+   * tile indices ty * ntx + tx, a permutation of all of the render area's
+   * tiles; NULL / 0: row-major ("tiles_order" "linear", imagesplitter.cc:
+   * 29-45). For "random" (std::random_shuffle, imagesplitter.cc:48) a plugin
+   * reads the live film's splitter; yk_tile_order_random computes it for a
+   * given rand() seed. Samples are splatted in this order (single-thread
+   * reference order); a shard renders the listed tiles t with
+   * t % nshards == shard, in list order. [NULL, 0]                           */
+  const int32_t* tile_order;
+  int32_t tile_order_len;
 } yk_render_params;
+enum { YK_TILES_LINEAR = 0, YK_TILES_RANDOM = 1 };
 
 /* one ray, 32 bytes: ray_t (ray.h:26-49) without time */
 typedef struct yk_ray {
@@ -262,6 +274,12 @@ int yk_scene_get_camera(const yk_scene* s, yk_camera* out);
 int yk_scene_generate(yk_scene* s, const char* name, int32_t p0, int32_t p1, int32_t resx,
                       int32_t resy, yk_render_params* params_out);
 void yk_render_params_default(yk_render_params* p);
+/* imageSpliter_t's "random" tile order (imagesplitter.cc:48): the row-major
+ * list 0..ntiles-1 shuffled by libstdc++'s std::random_shuffle, whose
+ * rand() is glibc's after srand(seed) -- seed 1 is a process that has not
+ * called srand() or rand() before the film is set up. Uses a private
+ * generator state (the caller's rand() is untouched). */
+int yk_tile_order_random(int32_t ntiles, uint32_t seed, int32_t* order_out);
 /* A live imageFilm_t -> render parameters: identifies the film's filter by
  * comparing its 16x16 filterTable (imagefilm.cc:119-165) with the box /
  * Mitchell / Gauss / Lanczos2 tables libyk builds, bit for bit, and takes its

@@ -2551,9 +2551,14 @@ static int render_tiles(const yk_render_params* P, int shard, int nshards, float
       aa_flags(&F, P->aa_threshold, flags);
       adaptive = 1;
     }
-    for (int ty = 0; ty < ny; ++ty)
-      for (int tx = 0; tx < nx; ++tx) {
-        if ((ty * nx + tx) % nshards != shard) continue;
+    /* tiles in the order the film hands them out: imageFilm_t::nextArea over
+     * its imageSpliter_t (imagefilm.cc:190-195,291-304; imagesplitter.cc:29-53),
+     * row-major ("linear") or the given list (e.g. std::random_shuffle's) */
+    int use_order = P->tile_order && P->tile_order_len == nx * ny;
+    for (int k = 0; k < nx * ny; ++k) {
+        int t = use_order ? P->tile_order[k] : k;
+        int ty = t / nx, tx = t % nx;
+        if (t % nshards != shard) continue;
         int X = F.cx0 + tx * ts, Y = F.cy0 + ty * ts;
         int W = (F.cx0 + F.w - X) < ts ? (F.cx0 + F.w - X) : ts;
         int H = (F.cy0 + F.h - Y) < ts ? (F.cy0 + F.h - Y) : ts;

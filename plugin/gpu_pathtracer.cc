@@ -142,6 +142,7 @@ YK_MEMBER(FilmFilterW, imageFilm_t, float, filterw)
 YK_MEMBER(FilmTable, imageFilm_t, float*, filterTable)
 YK_MEMBER(FilmTileSize, imageFilm_t, int, tileSize)
 YK_MEMBER(FilmPremult, imageFilm_t, bool, premultAlpha)
+YK_MEMBER(FilmSplitter, imageFilm_t, imageSpliter_t*, splitter)
 #define GET(obj, Tag) ((obj).*member_of<Tag>::ptr)
 
 // pointLight_t, directionalLight_t and constBackground_t are defined inside
@@ -437,8 +438,24 @@ class gpuTiledIntegrator_t : public tiledIntegrator_t {
     if (yk_film_filter_from_table(GET(*film, FilmTable), GET(*film, FilmFilterW), &params) != YK_OK) return fail();
     if (GET(*film, FilmPremult)) return unsupported("premultiplied alpha films are not on the GPU path");
     if (scene->doDepth()) return unsupported("depth passes are not on the GPU path");
+    // as tiledIntegrator_t::render does (integrator.cc:148): clear the film and
+    // build its tile splitter, whose order ("tiles_order": row-major, or
+    // std::random_shuffle for "random", imagesplitter.cc:29-53) is the order
+    // imageFilm_t::nextArea hands the tiles out and so the splat order
+    film->init(params.aa_passes);
+    std::vector<int32_t> order;
+    if (imageSpliter_t* sp = GET(*film, FilmSplitter)) {
+      const int ts = params.tile_size, ntx = (w + ts - 1) / ts;
+      renderArea_t a;
+      for (int n = 0; sp->getArea(n, a); ++n)
+        order.push_back((int32_t)(((a.Y - params.ystart) / ts) * ntx + (a.X - params.xstart) / ts));
+    }
+    params.tile_order = order.empty() ? nullptr : order.data();
+    params.tile_order_len = (int32_t)order.size();
     std::vector<float> sums((size_t)w * h * 5);
     const int rc = yk_render_multi(devs.data(), (int32_t)devs.size(), &params, sums.data(), nullptr);
+    params.tile_order = nullptr;  // `order` ends with this call
+    params.tile_order_len = 0;
     if (rc != YK_OK && rc != YK_ERR_ABORTED) return fail();  // aborted: keep what was rendered, as renderTile does
     for (int j = 0; j < h; ++j)
       for (int i = 0; i < w; ++i) {
