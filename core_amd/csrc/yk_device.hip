@@ -1243,8 +1243,10 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
           } else if (CLOSEST) {
             // the miss record from constants materialised here (hoisted out of
             // the loop, the compiler kept the 16-B constant in 4 VGPRs)
+#ifndef YK_NO_CLOSEST_RESULTS  // attribution experiment only (PMC WRITE_SIZE without the hit-record stores)
             const unsigned m1 = vconst<0xFFFFFFFFu>(), z = vconst<0u>();
             hits[r] = yk_hit{(int)m1, __uint_as_float(z), __uint_as_float(z), __uint_as_float(z)};
+#endif
           } else {
             occl[r] = 0;
             if (TS) {
@@ -1330,7 +1332,9 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
               p = (p & 0x80000000u) ? p & 0x7FFFFFFFu : S.leaf[p];  // the prim code of coop_leaves / lane_leaves
               h = yk_hit{(int)p, c.x, c.y, c.z};
             }
+#ifndef YK_NO_CLOSEST_RESULTS
             hits[rid] = h;
+#endif
           } else {
             fin = true;
             fin_rid = rid;

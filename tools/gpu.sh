@@ -145,6 +145,11 @@ EOF
     done
     python3 tools/pmc_dump.py $P > $P/summary.txt
     echo "pmctb $v done" ;;
+  pmcw1:*)
+    # WRITE_SIZE of the one-pipe headline frame only, library VARIANT (write attribution)
+    v=${s#pmcw1:}
+    YK_LIB=$(lib $v) timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmcw1_${v}_frame -o w -- python3 bench.py $P1 > $O/pmcw1_${v}_frame.log 2>&1
+    echo "pmcw1 $v done" ;;
   pmcw:*)
     # WRITE_SIZE of the one-pipe headline frame and of the traversal
     # microbenchmark with library VARIANT (write-traffic attribution)
