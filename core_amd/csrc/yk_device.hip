@@ -1078,8 +1078,45 @@ size_t small_scene_bytes(size_t nn, size_t ntris, size_t nlref) {
   return 4 * (((6 * nn + 3) & ~(size_t)3) + 12 * (ntris + nlref));  // small_rec_word in 64 bits
 }
 
-template <bool CLOSEST, int NSEG, bool TS = false, bool BIG = false, bool UNI = false, int W = 1>
-__device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx,
+// w of a shadow ray whose tmin is its origin record's (Batch comment): tmax,
+// or the sentinel for tmax < 0 (no distance limit); a NaN tmax is stored as
+// the positive quiet NaN, never as the sentinel
+constexpr unsigned kTmaxInf = 0xFFC00000u;  // negative quiet NaN
+__device__ __forceinline__ float shadow_w(float tmax) {
+  return tmax < 0.f ? __uint_as_float(kTmaxInf) : (tmax != tmax ? __uint_as_float(0x7FC00000u) : tmax);
+}
+// the shadow ray of slot record dw and origin record o (inverse of the
+// encodings above; every value read back is the one the shading computed)
+__device__ __forceinline__ yk_ray unpack_shadow(float4 dw, float4 o) {
+  yk_ray r;
+  r.from[0] = o.x;
+  r.from[1] = o.y;
+  r.from[2] = o.z;
+  r.dir[0] = dw.x;
+  r.dir[1] = dw.y;
+  r.dir[2] = dw.z;
+  const bool inf = __float_as_uint(dw.w) == kTmaxInf, mis = !inf && dw.w < 0.f;
+  r.tmin = mis ? YK_MIN_RAYDIST : o.w;
+  r.tmax = inf ? -1.f : (mis ? -dw.w : dw.w);
+  return r;
+}
+
+// The rays of a trace launch: whole 32-B rays, or (the SPLIT any-hit kernels,
+// batches with split = 1) the shadow-slot records {dir, w} and the origin
+// records {P, tmin} (Batch comment). A split queue entry e holds the slot's k
+// above its origin index: origin e & omask, slot (e >> kshift) * kstride +
+// (e & omask). (A modulo of the slot index instead spilled two more
+// registers inside the any-hit kernel's loop, and one kernel serving both
+// forms a third: the forms are separate instantiations.)
+struct RaySrc {
+  const yk_ray* rays;
+  const float4* sdir;
+  const float4* sorg;
+  unsigned omask, kshift, kstride;
+};
+
+template <bool CLOSEST, int NSEG, bool TS = false, bool BIG = false, bool UNI = false, int W = 1, bool SPLIT = false>
+__device__ __forceinline__ void trace_body(DScene S, RaySrc src, const unsigned* __restrict__ idx,
                                            RayCount rc, yk_hit* __restrict__ hits, uint8_t* __restrict__ occl,
                                            unsigned long long* __restrict__ work, unsigned long long* __restrict__ ctr,
                                            uint2* __restrict__ ovf, int ovf_depth, int refill_min,
@@ -1233,8 +1270,16 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
         if (q < 0) {
           exhausted = (seg_done == kAll);  // nothing left anywhere; else retry at the next refill
         } else {
-          const int r = idx ? (int)idx[q] : (int)q;
-          const yk_ray ray = rays[r];
+          int r;
+          yk_ray ray;
+          if constexpr (!SPLIT) {
+            r = idx ? (int)idx[q] : (int)q;
+            ray = src.rays[r];
+          } else {
+            const unsigned e = idx ? idx[q] : (unsigned)q, oi = e & src.omask;
+            r = (int)((e >> src.kshift) * src.kstride + oi);
+            ray = unpack_shadow(src.sdir[r], src.sorg[oi]);
+          }
           if (TS) st.ts_max = ts_depth;
           if (trav_begin<CLOSEST, TS, UNI>(S, st, ray)) {
             rid = r;
@@ -1483,74 +1528,90 @@ __device__ __forceinline__ void trace_body(DScene S, const yk_ray* __restrict__ 
 #endif
 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
-k_trace_closest(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+k_trace_closest(DScene S, RaySrc src, const unsigned* __restrict__ idx, RayCount n,
                 yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                 unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<true, 8>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+  trace_body<true, 8>(S, src, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
-k_trace_shadow(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+k_trace_shadow(DScene S, RaySrc src, const unsigned* __restrict__ idx, RayCount n,
                yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false, YK_SHADOW_SEGS>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+  trace_body<false, YK_SHADOW_SEGS>(S, src, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+}
+// the same over a batch's split shadow slots (RaySrc)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
+k_trace_shadow_split(DScene S, RaySrc src, const unsigned* __restrict__ idx, RayCount n,
+                     yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
+                     unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
+  trace_body<false, YK_SHADOW_SEGS, false, false, false, 1, true>(S, src, idx, n, hits, occl, work, ctr, ovf,
+                                                                   ovf_depth, refill_min);
 }
 // trees with a leaf of 2^17 references or more (coop_leaves BIG)
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
-k_trace_closest_big(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+k_trace_closest_big(DScene S, RaySrc src, const unsigned* __restrict__ idx, RayCount n,
                     yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                     unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<true, 8, false, true>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+  trace_body<true, 8, false, true>(S, src, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
-k_trace_shadow_big(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+k_trace_shadow_big(DScene S, RaySrc src, const unsigned* __restrict__ idx, RayCount n,
                    yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                    unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false, 1, false, true>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+  trace_body<false, 1, false, true>(S, src, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 // universal-mode scenes (kdTree_t<primitive_t>::IntersectS: t > tmin)
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
-k_trace_shadow_uni(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+k_trace_shadow_uni(DScene S, RaySrc src, const unsigned* __restrict__ idx, RayCount n,
                    yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                    unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false, 1, false, false, true>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth,
+  trace_body<false, 1, false, false, true>(S, src, idx, n, hits, occl, work, ctr, ovf, ovf_depth,
                                                         refill_min);
 }
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
-k_trace_shadow_big_uni(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+k_trace_shadow_big_uni(DScene S, RaySrc src, const unsigned* __restrict__ idx, RayCount n,
                        yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                        unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false, 1, false, true, true>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
+  trace_body<false, 1, false, true, true>(S, src, idx, n, hits, occl, work, ctr, ovf, ovf_depth, refill_min);
 }
 // transparent shadows (scene_t::isShadowed(state, ray, maxDepth, filt),
 // scene.cc:904-928 -> IntersectTS): occlusion + filter colour per ray
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5)))
-k_trace_shadow_ts(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+k_trace_shadow_ts(DScene S, RaySrc src, const unsigned* __restrict__ idx, RayCount n,
                   uint8_t* __restrict__ occl, float* __restrict__ tsf, int ts_depth, unsigned long long* __restrict__ work,
                   unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false, 1, true>(S, rays, idx, n, nullptr, occl, work, ctr, ovf, ovf_depth, refill_min, tsf,
+  trace_body<false, 1, true>(S, src, idx, n, nullptr, occl, work, ctr, ovf, ovf_depth, refill_min, tsf,
                                     ts_depth);
 }
 // small scenes (traversal data in LDS, YK_SMALL_W waves per workgroup;
 // dynamic LDS = small_scene_bytes)
 __global__ void __launch_bounds__(64 * YK_SMALL_W) __attribute__((amdgpu_waves_per_eu(YK_CLOSEST_WAVES)))
-k_trace_closest_small(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+k_trace_closest_small(DScene S, RaySrc src, const unsigned* __restrict__ idx, RayCount n,
                       yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                       unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<true, 8, false, false, false, YK_SMALL_W>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth,
+  trace_body<true, 8, false, false, false, YK_SMALL_W>(S, src, idx, n, hits, occl, work, ctr, ovf, ovf_depth,
                                                        refill_min);
 }
 __global__ void __launch_bounds__(64 * YK_SMALL_W) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
-k_trace_shadow_small(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+k_trace_shadow_small(DScene S, RaySrc src, const unsigned* __restrict__ idx, RayCount n,
                      yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                      unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false, YK_SHADOW_SEGS, false, false, false, YK_SMALL_W>(S, rays, idx, n, hits, occl, work, ctr, ovf,
+  trace_body<false, YK_SHADOW_SEGS, false, false, false, YK_SMALL_W>(S, src, idx, n, hits, occl, work, ctr, ovf,
                                                                      ovf_depth, refill_min);
 }
 __global__ void __launch_bounds__(64 * YK_SMALL_W) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
-k_trace_shadow_uni_small(DScene S, const yk_ray* __restrict__ rays, const unsigned* __restrict__ idx, RayCount n,
+k_trace_shadow_small_split(DScene S, RaySrc src, const unsigned* __restrict__ idx, RayCount n,
+                           yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
+                           unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth,
+                           int refill_min) {
+  trace_body<false, YK_SHADOW_SEGS, false, false, false, YK_SMALL_W, true>(S, src, idx, n, hits, occl, work, ctr,
+                                                                           ovf, ovf_depth, refill_min);
+}
+__global__ void __launch_bounds__(64 * YK_SMALL_W) __attribute__((amdgpu_waves_per_eu(YK_SHADOW_WAVES)))
+k_trace_shadow_uni_small(DScene S, RaySrc src, const unsigned* __restrict__ idx, RayCount n,
                          yk_hit* __restrict__ hits, uint8_t* __restrict__ occl, unsigned long long* __restrict__ work,
                          unsigned long long* __restrict__ ctr, uint2* __restrict__ ovf, int ovf_depth, int refill_min) {
-  trace_body<false, 1, false, false, true, YK_SMALL_W>(S, rays, idx, n, hits, occl, work, ctr, ovf, ovf_depth,
+  trace_body<false, 1, false, false, true, YK_SMALL_W>(S, src, idx, n, hits, occl, work, ctr, ovf, ovf_depth,
                                                        refill_min);
 }
 
@@ -2072,11 +2133,29 @@ enum : int { PS_ALIVE = 1, PS_RESOLVE = 2, PS_CONT = 4, PS_EST = 8, PS_EMIT = 25
 
 // Per-batch device state. Camera sample c owns K shadow slots k = 0..K-1:
 // doLightEstimation's i-th light sample is slot k0+i, its i-th BSDF (MIS)
-// sample slot k0+n+i. Slot (c, k) is stored at k * cap + c (slot_of): the
-// lanes of a wave, consecutive samples writing the same k, then fill whole
-// cache lines (at c * K + k every lane's 32-B ray landed in its own line). Shadow rays are written straight into their slot and
-// only the slot index goes through the compacted queue, so the resolve step
-// reads results in the reference's summation order without any sorting.
+// sample slot k0+n+i. Slot (c, k) of region r (the merged launch's bounce
+// depth, else 0) is stored at k * kstride + r * cap + c (slot_of,
+// kstride = regions * cap): the lanes of a wave, consecutive samples writing
+// the same k, then fill whole cache lines (at c * K + k every lane's record
+// landed in its own line). Shadow rays are written straight into their slot
+// and only the slot index goes through the compacted queue, so the resolve
+// step reads results in the reference's summation order without any sorting.
+//
+// Shadow rays in two parts (every shadow ray of a shading point starts at
+// its P, mcintegrator.cc:103-191): per slot 16 B {dir, w}, per shading point
+// 16 B {P, tmin}, written once when the point emits any ray, as the record
+// of slot k = K (so the origin of slot s is record K * kstride + s mod
+// kstride, and the shading kernels need no further pointer). w encodes tmax and
+// which tmin applies (shadow_w / unpack_shadow): a light-sample ray's tmax
+// (>= 0) with the origin's tmin (shadowBias), the sentinel kTmaxInf for
+// tmax < 0 (directional lights), or -t for a BSDF (MIS) ray, whose tmin is
+// YK_MIN_RAYDIST and whose light hit t is > 1e-10 (light_hit). A path
+// vertex with the C2 light's four light samples writes 4 * 16 + 16 B of
+// rays instead of 4 * 32. Scenes whose lights take one sample each (the
+// headline: one light ray and at most one MIS ray per vertex) gain nothing
+// from it and keep whole 32-B rays at the slot index (split = 0, K < 4;
+// YK_SPLIT=0/1 forces either form): the two-array fetch costs the any-hit
+// kernel 2 % there.
 struct Batch {
   int* prim_hit;        // PH_* flags of the camera ray
   unsigned* soffs;      // samplingOffs (fnv of pixel)
@@ -2094,17 +2173,21 @@ struct Batch {
   int* q_owner[2];      // camera sample of each bounce-queue entry
   yk_ray* q_rays[2];    // bounce queues (ping-pong)
   yk_hit* q_hits[2];
-  yk_ray* s_rays;       // K per camera sample
+  float4* s_dir;        // split: K + 1 per camera sample (and region): {dir, w}, then {P, tmin} at k = K;
+                        // else K yk_ray (32 B) per camera sample (and region)
+  int split;            // shadow rays as {dir, w} + origin records (1) or whole rays (0)
   uint8_t* s_occl;      // K per camera sample
-  unsigned* s_idx;      // compacted shadow queue of slot indices
+  unsigned* s_idx;      // compacted shadow queue: slot index, or (split) k << kshift | origin index r * cap + c
   float* sl_contrib;    // 3 floats per slot
   uint8_t* sl_flags;    // 1 per slot
   float4* samples;      // final RGBA per camera sample
   float2* sxy;          // (dx, dy) of the sample inside its pixel
   char4* pext;          // per pixel slot: footprint extent of its samples (k_pixel_extent)
   int K;
-  long long cap;  // samples per batch: the stride of the shadow-slot arrays
-  long long slot_base;  // merged shadow launch: first slot of this bounce's slot region (0 otherwise)
+  long long cap;  // samples per batch
+  long long kstride;    // slot stride of k: regions * cap
+  int kshift;           // queue entries: bits of the origin index (kstride <= 2^kshift)
+  long long slot_base;  // merged shadow launch: this bounce's region offset depth * cap (0 otherwise)
   // merged shadow launch: the regions' queue-count words (region r's count in
   // the low half of mq_words[r]); a bounce kernel writes its queue entries
   // after those of the regions before it (complete, earlier in the stream)
@@ -2122,7 +2205,7 @@ struct Batch {
   float* sl_aux;        // 4 per slot: scalar factors (and the Dirac light colour)
 };
 __device__ __forceinline__ long long slot_of(const Batch& B, long long c, int k) {
-  return B.slot_base + (long long)k * B.cap + c;  // k-major (sample-major c * K + k: C2 7810 against 8047 Mrays/s)
+  return B.slot_base + (long long)k * B.kstride + c;  // k-major (sample-major c * K + k: C2 7810 against 8047 Mrays/s)
 }
 
 struct RenderConst {
@@ -2317,13 +2400,31 @@ __device__ __forceinline__ void put_aux(const Batch& B, long long slot, float a,
   *reinterpret_cast<float4*>(B.sl_aux + 4 * slot) = make_float4(a, b, c, d);
 }
 
-// a shadow ray of slot `slot`, stored for the any-hit launch: bit kbit of
-// `traced`, one queued ray
-__device__ __forceinline__ int emit_shadow(const Batch& B, long long slot, const yk_ray& sr, int kbit,
+__device__ __forceinline__ void st_f4(float4* p, float a, float b, float c, float d) {
+  typedef float f4n __attribute__((ext_vector_type(4)));
+  const f4n v = {a, b, c, d};
+  __builtin_nontemporal_store(v, reinterpret_cast<f4n*>(p));
+}
+// a shadow ray of slot `slot` from P (tmin shadowBias, or YK_MIN_RAYDIST for
+// a BSDF sample: MIS), stored for the any-hit launch (Batch comment): bit kbit
+// of `traced`, one queued ray
+template <bool MIS>
+__device__ __forceinline__ int emit_shadow(const Batch& B, long long slot, v3 P, v3 dir, float tmax, int kbit,
                                            unsigned long long& traced) {
-  st_ray(&B.s_rays[slot], sr);
+  if (B.split) {
+    st_f4(&B.s_dir[slot], dir.x, dir.y, dir.z, MIS ? -tmax : shadow_w(tmax));
+  } else {
+    yk_ray sr;
+    put_ray(sr, P, dir, MIS ? YK_MIN_RAYDIST : YK_SHADOW_BIAS, tmax);
+    st_ray(reinterpret_cast<yk_ray*>(B.s_dir) + slot, sr);
+  }
   if (kbit < 64) traced |= 1ull << kbit;
   return 1;
+}
+// split form: the origin record of sample c's shading point at this region,
+// written once when the point emitted any shadow ray
+__device__ __forceinline__ void put_org(const Batch& B, long long c, v3 P) {
+  if (B.split) st_f4(&B.s_dir[slot_of(B, c, B.K)], P.x, P.y, P.z, YK_SHADOW_BIAS);
 }
 
 // mcIntegrator_t::doLightEstimation (area light), mcintegrator.cc:73-195, split
@@ -2346,12 +2447,7 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
       put_slot(B, slot, 0, black);
       return 0;
     }
-    int nq;
-    {
-      yk_ray sr;
-      put_ray(sr, sp.P, ldir, YK_SHADOW_BIAS, ltmax);
-      nq = emit_shadow(B, slot, sr, k0, traced);
-    }
+    const int nq = emit_shadow<false>(B, slot, sp.P, ldir, ltmax, k0, traced);
     const c3 surf = mat_eval<!DIFF>(M, sp, wo, ldir);
     const float f = fabsf(vdot(sp.N, ldir));
     if (B.ts) {  // lcol *= scol first (mcintegrator.cc:94): keep the parts
@@ -2382,11 +2478,7 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
       put_slot(B, slot, 0, black);
       continue;
     }
-    {
-      yk_ray sr;
-      put_ray(sr, sp.P, ldir, YK_SHADOW_BIAS, ltmax);
-      nr += emit_shadow(B, slot, sr, k0 + i, traced);
-    }
+    nr += emit_shadow<false>(B, slot, sp.P, ldir, ltmax, k0 + i, traced);
     if (!(lpdf > 1e-6f)) {
       put_slot(B, slot, SL_TRACED, black);
       continue;
@@ -2427,11 +2519,7 @@ __device__ __forceinline__ int gen_light(const Batch& B, long long c, int k0, in
       put_slot(B, slot, 0, black);
       continue;
     }
-    {
-      yk_ray sr;
-      put_ray(sr, sp.P, bdir, YK_MIN_RAYDIST, bt);
-      nr += emit_shadow(B, slot, sr, k0 + n + i, traced);
-    }
+    nr += emit_shadow<true>(B, slot, sp.P, bdir, bt, k0 + n + i, traced);  // bt > 1e-10
     if (!(lightPdf > 1e-6f)) {
       put_slot(B, slot, SL_TRACED, black);
       continue;
@@ -2460,7 +2548,7 @@ __device__ __forceinline__ void flush_shadow(const Batch& B, long long c, int ke
   for (int k = 0; k < kend; ++k) {
     const long long slot = slot_of(B, c, k);
     const bool t = k < 64 ? ((traced >> k) & 1ull) != 0ull : (B.sl_flags[slot] & SL_TRACED) != 0;
-    if (t) B.s_idx[r++] = (unsigned)slot;
+    if (t) B.s_idx[r++] = B.split ? ((unsigned)k << B.kshift) | (unsigned)(B.slot_base + c) : (unsigned)slot;
   }
 }
 
@@ -2557,6 +2645,7 @@ __global__ void __launch_bounds__(YK_PRIMARY_BLOCK) k_shade_primary(DScene S, Ba
           k0 += c_lights[l].nslots;
         }
         kend = k0;
+        if (nr) put_org(B, c, sp.P);
         if (R.integrator == YK_INTEGRATOR_PATH) {
           B.wlast[c] = 0.f;
           seg = path_first_segment<DIFF>(B, R, c, sp, M, dir, 0);
@@ -2757,6 +2846,7 @@ __attribute__((amdgpu_waves_per_eu(DIFF ? YK_BOUNCE_WAVES_D : YK_BOUNCE_WAVES)))
         if (R.nlights == 1) nr = gen_light<DIFF>(B, c, 0, 0, sp, pwo, s, B.soffs[c], 0u, traced);
         else nr = gen_light<DIFF>(B, c, 0, lnum, sp, pwo, s, B.soffs[c], (unsigned)lnum, traced);
         kend = c_lights[lnum].nslots;
+        if (nr) put_org(B, c, sp.P);
         if (R.nlights > 1) B.lsel[c] = lnum;  // one light: the resolve knows it is light 0
         ps |= PS_EST;
       }
@@ -2864,8 +2954,7 @@ __global__ void __launch_bounds__(256) k_resolve_bounce(Batch B, RenderConst R,
 
 // Batch view of bounce `depth`'s slot region and path state (host and device)
 __host__ __device__ inline Batch merged_region(Batch B, int depth) {
-  const long long rs = (long long)B.K * B.cap;
-  B.slot_base = (long long)depth * rs;
+  B.slot_base = (long long)depth * B.cap;
   B.mq_region = depth;
   if (depth >= 1) {
     const long long o = (long long)(depth - 1) * B.cap;
@@ -3433,7 +3522,8 @@ struct Pipe {
   DBuf<float> col, alpha, thr, pathcol, scol_next, wlast, emit_b, sl_contrib;
   DBuf<int> prim_hit, pstate, lsel, qo0, qo1, tile_base;
   DBuf<int4> tiles;
-  DBuf<yk_ray> p_rays, qr0, qr1, s_rays;
+  DBuf<yk_ray> p_rays, qr0, qr1;
+  DBuf<float4> s_dir;  // shadow slots (and origins) in either form (Batch)
   DBuf<yk_hit> p_hits, qh0, qh1;
   DBuf<uint8_t> sl_flags, s_occl;
   DBuf<float4> samples;
@@ -3488,7 +3578,7 @@ struct Pipe {
     qr1.ensure(maxc);
     qh0.ensure(maxc);
     qh1.ensure(maxc);
-    s_rays.ensure(maxc * K * regions);
+    s_dir.ensure(maxc * std::max(K + 1, 2 * K) * regions);  // the split form, or K 32-B rays
     s_occl.ensure(maxc * K * regions);
     s_idx.ensure(maxc * K * regions);
     sl_contrib.ensure(3 * maxc * K * regions);
@@ -3518,7 +3608,7 @@ struct Pipe {
     B.q_rays[1] = qr1.p;
     B.q_hits[0] = qh0.p;
     B.q_hits[1] = qh1.p;
-    B.s_rays = s_rays.p;
+    B.s_dir = s_dir.p;
     B.s_occl = s_occl.p;
     B.s_idx = s_idx.p;
     B.sl_contrib = sl_contrib.p;
@@ -3528,6 +3618,9 @@ struct Pipe {
     B.pext = pext.p;
     B.K = K;
     B.cap = maxc;
+    B.kstride = maxc * regions;
+    B.kshift = 0;
+    while ((1ll << B.kshift) < B.kstride) ++B.kshift;
     if (ts) {
       s_filt.ensure(3 * maxc * K);
       sl_aux.ensure(4 * maxc * K);
@@ -3568,6 +3661,7 @@ struct yk_device {
   // small scenes: traversal data copied to LDS per workgroup (install_traversal)
   bool small = false;
   size_t small_bytes = 0;
+  int per_cu_split[2] = {1, 1};  // the split-slot any-hit kernels: waves (large trees), workgroups (small scenes)
   int per_cu_small[3] = {1, 1, 1};  // resident workgroups (YK_SMALL_W waves) per CU: any-hit, closest, universal any-hit
   hipStream_t stream = nullptr;  // = pipe[0].stream (ray queries, film resolve)
   bool uploaded = false;
@@ -3996,19 +4090,30 @@ int refill_env() {
 // Enqueues one persistent traversal launch; no host synchronisation.
 // work: 128 zeroed words (per-XCD segment counters); acc: this kernel kind's
 // accumulators {nodes, triangle tests, errors, rays}. ev: timing pair or null.
+// RaySrc of whole 32-B rays / of a batch's shadow slots
+inline RaySrc ray_src(const yk_ray* r) { return RaySrc{r, nullptr, nullptr, 0u, 0u, 0u}; }
+inline RaySrc shadow_src(const Batch& B) {
+  if (!B.split) return ray_src(reinterpret_cast<const yk_ray*>(B.s_dir));
+  return RaySrc{nullptr, B.s_dir, B.s_dir + (long long)B.K * B.kstride, (1u << B.kshift) - 1u, (unsigned)B.kshift,
+                (unsigned)B.kstride};
+}
+
 template <bool CLOSEST>
-void enqueue_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* idx, RayCount n, yk_hit* hits,
+void enqueue_trace(yk_device* d, Pipe& P, RaySrc rays, const unsigned* idx, RayCount n, yk_hit* hits,
                    uint8_t* occ, unsigned long long* work, unsigned long long* acc, hipEvent_t ev0, hipEvent_t ev1) {
   const bool small = d->small && !d->big_leaves;
   const int waves = small ? YK_SMALL_W : 1;  // per workgroup
-  const long long per_cu = small ? d->per_cu_small[(!CLOSEST && d->S.uni) ? 2 : (int)CLOSEST]
+  const bool split = !CLOSEST && rays.rays == nullptr;  // render batches with split slots (never uni / big)
+  const long long per_cu = split ? d->per_cu_split[small ? 1 : 0]
+                           : small ? d->per_cu_small[(!CLOSEST && d->S.uni) ? 2 : (int)CLOSEST]
                            : d->big_leaves ? d->per_cu_big[CLOSEST]
                                            : d->per_cu[CLOSEST];
   const long long grid = (long long)d->cus * per_cu;
   const int ovf_depth = std::max(1, stack_depth(d) - (small ? YK_SMALL_RING : (CLOSEST ? kStackLdsC : kStackLds)));
   P.ovf.ensure((size_t)ovf_depth * (size_t)grid * 64 * waves);
   if (ev0) HIPCHK(hipEventRecord(ev0, P.stream));
-  auto kern = small ? (CLOSEST ? k_trace_closest_small : d->S.uni ? k_trace_shadow_uni_small : k_trace_shadow_small)
+  auto kern = split ? (small ? k_trace_shadow_small_split : k_trace_shadow_split)
+              : small ? (CLOSEST ? k_trace_closest_small : d->S.uni ? k_trace_shadow_uni_small : k_trace_shadow_small)
               : CLOSEST ? (d->big_leaves ? k_trace_closest_big : k_trace_closest)
                         : (d->S.uni ? (d->big_leaves ? k_trace_shadow_big_uni : k_trace_shadow_uni)
                                     : (d->big_leaves ? k_trace_shadow_big : k_trace_shadow));
@@ -4019,7 +4124,7 @@ void enqueue_trace(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* id
 }
 
 // Transparent-shadow any-hit launch (k_trace_shadow_ts): occlusion + filter.
-void enqueue_trace_ts(yk_device* d, Pipe& P, const yk_ray* rays, const unsigned* idx, RayCount n, uint8_t* occ,
+void enqueue_trace_ts(yk_device* d, Pipe& P, RaySrc rays, const unsigned* idx, RayCount n, uint8_t* occ,
                       float* filt, int max_depth, unsigned long long* work, unsigned long long* acc, hipEvent_t ev0,
                       hipEvent_t ev1) {
   const long long grid = (long long)d->cus * d->per_cu_ts;
@@ -4051,7 +4156,7 @@ void launch_trace(yk_device* d, Pipe& P, const yk_ray* rays, long long n, yk_hit
     HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_spill_stores), &z, sizeof z, 0, hipMemcpyHostToDevice, P.stream));
   }
 #endif
-  enqueue_trace<CLOSEST>(d, P, rays, nullptr, RayCount{nullptr, 0, n}, hits, occ, work, acc, P.ev0, P.ev1);
+  enqueue_trace<CLOSEST>(d, P, ray_src(rays), nullptr, RayCount{nullptr, 0, n}, hits, occ, work, acc, P.ev0, P.ev1);
   unsigned long long h[13];
   HIPCHK(hipMemcpyAsync(h, acc, sizeof h, hipMemcpyDeviceToHost, P.stream));
   HIPCHK(hipStreamSynchronize(P.stream));
@@ -4181,6 +4286,9 @@ void install_traversal(yk_device* d, size_t nn, size_t nleaf, uint32_t max_leaf_
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow_uni_small, 64 * YK_SMALL_W,
                                                         d->small_bytes));
     d->per_cu_small[2] = std::max(1, blocks);
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow_small_split, 64 * YK_SMALL_W,
+                                                        d->small_bytes));
+    d->per_cu_split[1] = std::max(1, blocks);
   }
 }
 
@@ -4208,6 +4316,8 @@ int yk_device_open(int32_t ordinal, yk_device** out) {
   int blocks = 0;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow, 64, 0));
   d->per_cu[0] = std::max(1, blocks);
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow_split, 64, 0));
+  d->per_cu_split[0] = std::max(1, blocks);
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_closest, 64, 0));
   d->per_cu[1] = std::max(1, blocks);
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_shadow_big, 64, 0));
@@ -4433,8 +4543,8 @@ int yk_trace_shadow_filtered(yk_device* d, const yk_ray* d_rays, int64_t n, uint
   unsigned long long* work = P.counters.p;
   unsigned long long* acc = P.counters.p + 128;
   HIPCHK(hipMemsetAsync(work, 0, 136 * sizeof(unsigned long long), P.stream));
-  enqueue_trace_ts(d, P, d_rays, nullptr, RayCount{nullptr, 0, n}, d_occ, d_filter, max_depth, work, acc, P.ev0,
-                   P.ev1);
+  enqueue_trace_ts(d, P, ray_src(d_rays), nullptr, RayCount{nullptr, 0, n}, d_occ, d_filter, max_depth,
+                   work, acc, P.ev0, P.ev1);
   unsigned long long h[4];
   HIPCHK(hipMemcpyAsync(h, acc, sizeof h, hipMemcpyDeviceToHost, P.stream));
   HIPCHK(hipStreamSynchronize(P.stream));
@@ -4685,9 +4795,18 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     return (v > 0 && v <= 240) ? v : 0ll;
   }();
   const long long batch_bytes = (batch_gb_env ? batch_gb_env : (merged ? 192ll : 64ll)) << 30;
-  // + per extra region: 50 B per slot (ray, contribution, flag, result,
-  // queue entry) and 32 B of path state per sample
-  const long long bytes_per_sample = 400 + 52ll * K + (long long)(regions - 1) * (50ll * K + 32);
+  // shadow rays as direction records + one origin per shading point when the
+  // lights take several samples (Batch comment); YK_SPLIT=0/1 (read per
+  // render: A/B runs, tests) forces either form
+  const bool split = [&] {
+    const char* e = std::getenv("YK_SPLIT");
+    return (e ? std::atoi(e) != 0 : K >= 4) && !d->S.uni && !d->big_leaves && !p->transp_shadows;
+  }();
+  // per region: 50 B per slot (32-B ray, contribution, flag, result, queue
+  // entry), 34 B + a 16-B origin per sample in the split form; + 32 B of path
+  // state per sample and extra region
+  const long long region_bytes = split ? 34ll * K + 16 : 50ll * K;
+  const long long bytes_per_sample = 400 + 2ll * K + region_bytes + (long long)(regions - 1) * (region_bytes + 32);
   const int pipes_cfg = pipes_env();
   const long long target = std::max(1ll << 20, std::min(target_env, batch_bytes / pipes_cfg / bytes_per_sample));
   const long long tile_samples = (long long)F.tile * F.tile * spp;
@@ -4700,11 +4819,19 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   // headline and hair unchanged); photon mapping keeps full batches (its
   // 16-spp bench frame in 4 batches instead of 1: 1572 -> 1537)
   const long long tiles_fill = (d->spec || pm) ? LLONG_MAX : ((long long)owned.size() + pipes_cfg - 1) / pipes_cfg;
-  const int tiles_per_batch = (int)std::max<long long>(1, std::min(target_spec / tile_samples, tiles_fill));
-  const long long maxc = (long long)tiles_per_batch * tile_samples;
+  int tiles_per_batch = (int)std::max<long long>(1, std::min(target_spec / tile_samples, tiles_fill));
   // camera-sample indices are 32-bit on the device, shadow-slot indices
-  // (k * maxc + c) 32-bit in the shadow queue
-  if (maxc >= (1ll << 31) || maxc * (long long)std::max(K, 1) * regions >= (1ll << 32))
+  // (k * kstride + r * maxc + c) 32-bit, and a shadow-queue entry holds k
+  // above the origin index r * maxc + c in 32 bits (Batch)
+  auto index_fits = [&](long long mc) {
+    int kshift = 0;
+    while ((1ll << kshift) < mc * regions) ++kshift;
+    return mc < (1ll << 31) && mc * (long long)std::max(K, 1) * regions < (1ll << 32) && kshift <= 31 &&
+           ((long long)std::max(K - 1, 0) << kshift) < (1ll << 32);
+  };
+  while (tiles_per_batch > 1 && !index_fits((long long)tiles_per_batch * tile_samples)) tiles_per_batch /= 2;
+  const long long maxc = (long long)tiles_per_batch * tile_samples;
+  if (!index_fits(maxc))
     return set_error(YK_ERR_UNSUPPORTED, "one tile holds too many samples (tile^2 * spp * shadow slots >= 2^32)");
   const int nbatch = (int)((owned.size() + tiles_per_batch - 1) / tiles_per_batch);
   const int npipes = d->spec ? 1 : std::min(pipes_cfg, std::max(1, nbatch));
@@ -4798,6 +4925,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     P.words.ensure((size_t)(2 * kAccWords + (d->spec ? 0 : words_per_batch * nb_here)));
     HIPCHK(hipMemsetAsync(P.words.p, 0, P.words.n * sizeof(unsigned long long), P.stream));
     Bp[pi] = P.bind(maxc, K, tiles_per_batch, R.ps != 0, p->transp_shadows != 0, regions);
+    Bp[pi].split = split ? 1 : 0;
     if (R.pm_fg) {
       P.fgl.ensure(3 * maxc);
       P.fglen.ensure(maxc);
@@ -4852,7 +4980,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     unsigned long long* bw = d->spec ? d->spec_words.p : P.words.p + 2 * kAccWords + words_per_batch * (bi / npipes);
     auto qw = [&](int isub, int depth) { return bw + isub * (bounces + 1) + depth; };
     int launch = 0;
-    auto trace = [&](bool closest, const yk_ray* rays, const unsigned* idx, RayCount n, yk_hit* hits,
+    auto trace = [&](bool closest, RaySrc rays, const unsigned* idx, RayCount n, yk_hit* hits,
                      uint8_t* occ) {
       unsigned long long* work = bw + 2ll * qwords_per_batch + 128ll * launch++;
       const hipEvent_t e0 = P.event(evn[pi]), e1 = P.event(evn[pi] + 1);
@@ -4880,13 +5008,13 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
         for (int it = 0; it <= p->photon.fg_bounces; ++it) {
           const unsigned long long* in_w = qw(isub, it);
           unsigned long long* out_w = qw(isub, it + 1);
-          trace(true, Bc.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, Bc.q_hits[qin], nullptr);
+          trace(true, ray_src(Bc.q_rays[qin]), nullptr, RayCount{in_w, 32, 0}, Bc.q_hits[qin], nullptr);
           unsigned long long* lk_w = qw(isub, it) + qwords_per_batch;  // lookup-queue count
           hipLaunchKernelGGL(d->diff_only ? k_fg_hit<true> : k_fg_hit<false>, dim3(grid_for(n, YK_APPEND_BLOCK)), dim3(YK_APPEND_BLOCK), 0,
                              P.stream, d->S, Bc, Rc, PMC, in_w, it, isub, qin,
                              P.fgl.p, P.fglen.p, out_w, P.lkq.p, lk_w);
           HIPCHK(hipGetLastError());
-          if (it < p->photon.fg_bounces) trace(false, Bc.s_rays, Bc.s_idx, RayCount{out_w, 0, 0}, nullptr, Bc.s_occl);
+          if (it < p->photon.fg_bounces) trace(false, shadow_src(Bc), Bc.s_idx, RayCount{out_w, 0, 0}, nullptr, Bc.s_occl);
           {
             const bool lds = lookup_lds(d);
             unsigned long long* work = bw + 2ll * qwords_per_batch + 128ll * launch++;
@@ -4924,10 +5052,10 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
       auto shade_entries = [&](const Batch& Bc, const RenderConst& Rc, long long n, long long node_base) {
         HIPCHK(hipMemsetAsync(d->spec_words.p, 0, d->spec_words.n * sizeof(unsigned long long), P.stream));
         launch = 0;
-        trace(true, Bc.p_rays, nullptr, RayCount{nullptr, 0, n}, Bc.p_hits, nullptr);
+        trace(true, ray_src(Bc.p_rays), nullptr, RayCount{nullptr, 0, n}, Bc.p_hits, nullptr);
         hipLaunchKernelGGL(d->diff_only ? k_shade_primary<true> : k_shade_primary<false>, dim3(grid_for(n, YK_PRIMARY_BLOCK)), dim3(YK_PRIMARY_BLOCK), 0, P.stream, d->S, Bc, Rc, n, qw(0, 0));
         HIPCHK(hipGetLastError());
-        trace(false, Bc.s_rays, Bc.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, Bc.s_occl);
+        trace(false, shadow_src(Bc), Bc.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, Bc.s_occl);
         hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(n)), dim3(256), 0, P.stream, Bc, Rc, n);
         HIPCHK(hipGetLastError());
         for (int isub = 0; isub < (path ? nsub : 0); ++isub) {
@@ -4940,11 +5068,11 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
           for (int depth = 1; depth <= bounces; ++depth) {
             const unsigned long long* in_w = qw(isub, depth - 1);
             unsigned long long* out_w = qw(isub, depth);
-            trace(true, Bc.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, Bc.q_hits[qin], nullptr);
+            trace(true, ray_src(Bc.q_rays[qin]), nullptr, RayCount{in_w, 32, 0}, Bc.q_hits[qin], nullptr);
             hipLaunchKernelGGL(d->diff_only ? k_shade_bounce<true> : k_shade_bounce<false>, dim3(grid_for(n, bounce_block(d->diff_only))), dim3(bounce_block(d->diff_only)), 0, P.stream, d->S, Bc, Rc, in_w, depth,
                                isub, qin, out_w);
             HIPCHK(hipGetLastError());
-            trace(false, Bc.s_rays, Bc.s_idx, RayCount{out_w, 0, 0}, nullptr, Bc.s_occl);
+            trace(false, shadow_src(Bc), Bc.s_idx, RayCount{out_w, 0, 0}, nullptr, Bc.s_occl);
             hipLaunchKernelGGL(k_resolve_bounce, dim3(grid_for(n)), dim3(256), 0, P.stream, Bc, Rc, in_w, depth,
                                qin);
             HIPCHK(hipGetLastError());
@@ -4985,11 +5113,11 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
       HIPCHK(hipGetLastError());
     }
     if (!d->spec) {
-    trace(true, B.p_rays, nullptr, RayCount{nullptr, 0, nc}, B.p_hits, nullptr);
+    trace(true, ray_src(B.p_rays), nullptr, RayCount{nullptr, 0, nc}, B.p_hits, nullptr);
     hipLaunchKernelGGL(d->diff_only ? k_shade_primary<true> : k_shade_primary<false>, dim3(grid_for(nc, YK_PRIMARY_BLOCK)), dim3(YK_PRIMARY_BLOCK), 0, P.stream, d->S, B, R, nc, qw(0, 0));
     HIPCHK(hipGetLastError());
     if (!merged) {
-      trace(false, B.s_rays, B.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, B.s_occl);
+      trace(false, shadow_src(B), B.s_idx, RayCount{qw(0, 0), 0, 0}, nullptr, B.s_occl);
       hipLaunchKernelGGL(k_resolve_primary, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc);
       HIPCHK(hipGetLastError());
     }
@@ -5007,7 +5135,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
       for (int depth = 1; depth <= bounces; ++depth) {
         const unsigned long long* in_w = qw(isub, depth - 1);
         unsigned long long* out_w = qw(isub, depth);
-        trace(true, B.q_rays[qin], nullptr, RayCount{in_w, 32, 0}, B.q_hits[qin], nullptr);
+        trace(true, ray_src(B.q_rays[qin]), nullptr, RayCount{in_w, 32, 0}, B.q_hits[qin], nullptr);
         Batch Bd = B;
         if (merged) {
           Bd = merged_region(B, depth);
@@ -5017,7 +5145,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
                            qin, out_w);
         HIPCHK(hipGetLastError());
         if (!merged) {
-          trace(false, B.s_rays, B.s_idx, RayCount{out_w, 0, 0}, nullptr, B.s_occl);
+          trace(false, shadow_src(B), B.s_idx, RayCount{out_w, 0, 0}, nullptr, B.s_occl);
           hipLaunchKernelGGL(k_resolve_bounce, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, in_w, depth, qin);
           HIPCHK(hipGetLastError());
         }
@@ -5025,7 +5153,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
       }
     }
     if (merged) {  // one any-hit launch for the camera hits and all bounces, then one resolve
-      trace(false, B.s_rays, B.s_idx, RayCount{qw(0, 0), 0, 0, regions}, nullptr, B.s_occl);
+      trace(false, shadow_src(B), B.s_idx, RayCount{qw(0, 0), 0, 0, regions}, nullptr, B.s_occl);
       hipLaunchKernelGGL(k_resolve_merged, dim3(grid_for(nc)), dim3(256), 0, P.stream, B, R, nc, bounces);
       HIPCHK(hipGetLastError());
     } else {

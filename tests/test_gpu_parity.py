@@ -259,6 +259,13 @@ def test_shading_instantiations_photon(gpu_device, monkeypatch, diff):
     assert (film.cpu().numpy().view(np.uint32) == sums_o.view(np.uint32)).all()
 
 
+# shadow-slot forms: whole 32-B rays, split records (direction + one origin
+# per shading point; the default for lights of several samples, cornell), and
+# split records through the HBM any-hit kernel (YK_SMALL=0)
+FORMS = {"full": {"YK_SPLIT": "0"}, "split": {"YK_SPLIT": "1"}, "split_hbm": {"YK_SPLIT": "1", "YK_SMALL": "0"}}
+
+
+@pytest.mark.parametrize("form", list(FORMS))
 @pytest.mark.parametrize("merge", ["0", "1"])
 @pytest.mark.parametrize("case,over", [
     (("cornell_pt", 64, 64, 0, 0), {}), (("bumpy", 48, 32, 120, 61), {}), (("smooth_inst", 48, 48, 0, 0), {}),
@@ -267,13 +274,15 @@ def test_shading_instantiations_photon(gpu_device, monkeypatch, diff):
     # adaptive passes: pixel sample indices from B.psample in every region
     (("cornell_pt", 48, 48, 0, 0), {"aa_passes": 3, "aa_inc_samples": 2, "aa_threshold": 0.05})],
     ids=["cornell", "bumpy", "smooth_inst", "dirac", "aa3"])
-def test_merged_shadow_launch(gpu_device, monkeypatch, case, over, merge):
+def test_merged_shadow_launch(gpu_device, monkeypatch, case, over, merge, form):
     """Path tracing with one any-hit launch per batch for the camera hits and
     every bounce (the queue regions written in place + k_resolve_merged) and
-    with one launch per bounce (YK_MERGE=0): both equal the oracle bit for
-    bit, ray counts included; the merged frame has one any-hit launch per
-    batch."""
+    with one launch per bounce (YK_MERGE=0), each with both shadow-slot forms:
+    all equal the oracle bit for bit, ray counts included; the merged frame
+    has one any-hit launch per batch."""
     monkeypatch.setenv("YK_MERGE", merge)
+    for k, v in FORMS[form].items():
+        monkeypatch.setenv(k, v)
     s, p, orc = scene(*case)
     q = A.yk_render_params.from_buffer_copy(p)
     q.aa_samples = 4

@@ -11,6 +11,8 @@
 #   bench                headline bench.py (1M tris, 1080p, 256 spp)
 #   c2 | pm | hair       BASELINE configs[1] Cornell / photon mapping / C5 hair benches
 #   prof                 rocprofv3 --kernel-trace --stats of the one-pipe headline frame
+#   prof1:V / prof1c2:V  the same (headline / Cornell) with a variant's library (VARIANT[@ENV])
+#   pmcw1:V / pmcw1c2:V  WRITE_SIZE of the one-pipe headline / Cornell frame with a variant's library
 #   prof_c2 | prof_hair | prof_pm  the same for the Cornell / hair / photon-mapping frames
 #   pmc                  FETCH_SIZE and WRITE_SIZE passes of the one-pipe headline frame
 #   pmc_c2 | pmc_hair    the same for Cornell / hair
@@ -75,6 +77,16 @@ for s in "$@"; do
     v=${s#prof1:}
     env $(envv $v) YK_LIB=$(lib $v) timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof1_${v//[@=]/_} -o p1 -- python3 bench.py $P1 > $O/prof1_${v//[@=]/_}.log 2>&1
     echo "prof1 $v done" ;;
+  prof1c2:*)
+    # one-pipe Cornell (C2) frame, rocprofv3 --kernel-trace --stats, with VARIANT[@ENV]
+    v=${s#prof1c2:}
+    env $(envv $v) YK_LIB=$(lib $v) timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof1c2_${v//[@=]/_} -o p1 -- python3 bench.py $C2 $P1 > $O/prof1c2_${v//[@=]/_}.log 2>&1
+    echo "prof1c2 $v done" ;;
+  pmcw1c2:*)
+    # WRITE_SIZE of the one-pipe Cornell frame, library VARIANT
+    v=${s#pmcw1c2:}
+    YK_LIB=$(lib $v) timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmcw1c2_${v}_frame -o w -- python3 bench.py $C2 $P1 > $O/pmcw1c2_${v}_frame.log 2>&1
+    echo "pmcw1c2 $v done" ;;
   pmc|pmc_c2|pmc_hair)
     A=""; [ $s = pmc_c2 ] && A="$C2"; [ $s = pmc_hair ] && A="$HAIR"
     timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/${s}_fetch -o f -- python3 bench.py $A $P1 > $O/${s}_fetch.log 2>&1
