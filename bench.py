@@ -211,7 +211,7 @@ def main():
         dist.destroy_process_group()
         return
 
-    roofline = roofline_line(args, w, ms_c, ms_s, rst, elapsed, pm_info is None, small)
+    roofline = roofline_line(args, w, ms_c, ms_s, rst, elapsed, pm_info is None, small, shadow_split(dev, p))
 
     cpu = None
     if not args.no_cpu:
@@ -265,16 +265,12 @@ def main():
         dist.destroy_process_group()
 
 
-def small_scene_bytes(dev):
-    """Bytes of the LDS copy of the traversal data when the resident scene runs
-    the small-scene kernels (k_trace_*_small), else 0 (read-only query of the
-    test-hooks header, enabled for this call)."""
+def _hook(fn, *args):
+    """A read-only query of the test-hooks header, enabled for this call."""
     old = os.environ.get("YK_DEBUG_HOOKS")
     os.environ["YK_DEBUG_HOOKS"] = "1"
     try:
-        b = C.c_int64(0)
-        A.check(A.lib().yk_debug_small_scene(dev._p, C.byref(b)))
-        return int(b.value)
+        A.check(fn(*args))
     finally:
         if old is None:
             del os.environ["YK_DEBUG_HOOKS"]
@@ -282,7 +278,23 @@ def small_scene_bytes(dev):
             os.environ["YK_DEBUG_HOOKS"] = old
 
 
-def roofline_line(args, w, ms_c, ms_s, rst, elapsed, pt, small=0):
+def small_scene_bytes(dev):
+    """Bytes of the LDS copy of the traversal data when the resident scene runs
+    the small-scene kernels (k_trace_*_small), else 0."""
+    b = C.c_int64(0)
+    _hook(A.lib().yk_debug_small_scene, dev._p, C.byref(b))
+    return int(b.value)
+
+
+def shadow_split(dev, p):
+    """True when a render with params p stores split shadow slots (16-B
+    direction records, any-hit kernels k_trace_shadow[_small]_split)."""
+    v = C.c_int32(0)
+    _hook(A.lib().yk_debug_shadow_form, dev._p, C.byref(p), C.byref(v))
+    return bool(v.value)
+
+
+def roofline_line(args, w, ms_c, ms_s, rst, elapsed, pt, small=0, split=False):
     """Roofline of the dominant traversal kernel. Durations come from the
     serialised roofline frame (rst) when it ran, else from the timed frames'
     HIP events (overlapped by the other pipes: a lower bound on the rate).
@@ -302,7 +314,7 @@ def roofline_line(args, w, ms_c, ms_s, rst, elapsed, pt, small=0):
     kc = dict(name="k_trace_closest" + sfx, launches=cnt[6], ms=ms[0], bytes=algorithmic_bytes(cnt[0], cnt[2], cnt[3], 16))
     # H = 4 B for the shadow result, as SURVEY.md §8(d) prices it (the kernel
     # stores 1 B)
-    ks = dict(name="k_trace_shadow" + sfx, launches=cnt[7], ms=ms[1], bytes=algorithmic_bytes(cnt[1], cnt[4], cnt[5], 4))
+    ks = dict(name="k_trace_shadow" + sfx + ("_split" if split else ""), launches=cnt[7], ms=ms[1], bytes=algorithmic_bytes(cnt[1], cnt[4], cnt[5], 4))
     for k in (kc, ks):
         k["gbs"] = k["bytes"] / (k["ms"] * 1e-3) / 1e9 if k["ms"] > 0 else 0.0
         k["avg_ms"] = k["ms"] / max(k["launches"], 1)

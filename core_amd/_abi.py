@@ -213,6 +213,7 @@ SIGNATURES = {
     "yk_debug_qmc_probe": (C.c_int, [P, C.c_int32, P, P, i64, P]),
     "yk_debug_small_scene": (C.c_int, [P, C.POINTER(i64)]),
     "yk_debug_shading_kind": (C.c_int, [P, C.POINTER(C.c_int32)]),
+    "yk_debug_shadow_form": (C.c_int, [P, C.POINTER(yk_render_params), C.POINTER(C.c_int32)]),
 }
 
 _lib = None

@@ -4142,6 +4142,17 @@ void enqueue_trace_ts(yk_device* d, Pipe& P, RaySrc rays, const unsigned* idx, R
 bool lookup_lds(const yk_device* d) { return d->rm_depth <= kLdsPStack && d->rm_nnodes < 65536; }
 size_t lookup_lds_bytes(int depth) { return (size_t)std::max(1, depth) * 64 * (sizeof(float) + sizeof(unsigned short)); }
 
+// Shadow rays as direction records + one origin per shading point (Batch
+// comment) when the lights take several samples (K >= 4) and the scene runs
+// the kernels that have the split form (not universal, big-leaf or
+// transparent-shadow); YK_SPLIT=0/1 (read per render: A/B runs, tests)
+// forces either form where it exists
+bool shadow_split(const yk_device* d, const yk_render_params* p) {
+  const char* e = std::getenv("YK_SPLIT");
+  const int K = std::max(1, d->sum_light_slots);
+  return (e ? std::atoi(e) != 0 : K >= 4) && !d->S.uni && !d->big_leaves && !p->transp_shadows;
+}
+
 // Ray-query entry points: one launch, synchronised, statistics added to st.
 template <bool CLOSEST>
 void launch_trace(yk_device* d, Pipe& P, const yk_ray* rays, long long n, yk_hit* hits, uint8_t* occ, yk_stats* st) {
@@ -4795,13 +4806,7 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
     return (v > 0 && v <= 240) ? v : 0ll;
   }();
   const long long batch_bytes = (batch_gb_env ? batch_gb_env : (merged ? 192ll : 64ll)) << 30;
-  // shadow rays as direction records + one origin per shading point when the
-  // lights take several samples (Batch comment); YK_SPLIT=0/1 (read per
-  // render: A/B runs, tests) forces either form
-  const bool split = [&] {
-    const char* e = std::getenv("YK_SPLIT");
-    return (e ? std::atoi(e) != 0 : K >= 4) && !d->S.uni && !d->big_leaves && !p->transp_shadows;
-  }();
+  const bool split = shadow_split(d, p);
   // per region: 50 B per slot (32-B ray, contribution, flag, result, queue
   // entry), 34 B + a 16-B origin per sample in the split form; + 32 B of path
   // state per sample and extra region

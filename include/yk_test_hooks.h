@@ -54,6 +54,12 @@ int yk_debug_small_scene(yk_device* d, int64_t* bytes);
  * loop. YK_ERR_UNSUPPORTED unless YK_DEBUG_HOOKS=1. */
 int yk_debug_shading_kind(yk_device* d, int32_t* diff_only);
 
+/* Which form a render of the resident scene with params p gives its shadow
+ * slots: *split = 1 for 16-B direction records plus one origin per shading
+ * point (any-hit kernels k_trace_shadow[_small]_split), 0 for whole 32-B
+ * rays. YK_ERR_UNSUPPORTED unless YK_DEBUG_HOOKS=1. */
+int yk_debug_shadow_form(yk_device* d, const yk_render_params* p, int32_t* split);
+
 #ifdef __cplusplus
 }
 #endif

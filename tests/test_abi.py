@@ -26,7 +26,7 @@ def test_every_declared_symbol_is_exported_and_bound():
         assert hasattr(raw, n), f"libyk.so does not export {n}"
         assert n in A.SIGNATURES, f"_abi.SIGNATURES lacks {n}"
     hooks = declared_functions("yk_test_hooks.h")
-    assert hooks == ["yk_debug_qmc_probe", "yk_debug_shading_kind", "yk_debug_small_scene",
+    assert hooks == ["yk_debug_qmc_probe", "yk_debug_shading_kind", "yk_debug_shadow_form", "yk_debug_small_scene",
                      "yk_device_debug_set_node"] and not set(hooks) & set(names)
     for n in hooks:
         assert hasattr(raw, n) and n in A.SIGNATURES

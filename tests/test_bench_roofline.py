@@ -55,7 +55,7 @@ def test_wall_figure_prices_shadow_result_at_4_bytes():
 
 def test_small_scene_fractions_labelled():
     rst = _stats(10**8, 5 * 10**8, 10**9, 10**9, 10**9, 10**9, 10, 2, 10.0, 30.0)
-    out = bench.roofline_line(_args(), [0.0] * 9, 0, 0, rst, 1.0, False, small=7800)
-    assert out["kernel"] == "k_trace_shadow_small"
+    out = bench.roofline_line(_args(), [0.0] * 9, 0, 0, rst, 1.0, False, small=7800, split=True)
+    assert out["kernel"] == "k_trace_shadow_small_split"
     assert "lds" in out and out["lds"]["scene_copy_bytes"] == 7800
     assert "LDS reads" in out["hbm"]["note"] and "LDS reads" in out["l2"]["note"]

@@ -6,6 +6,8 @@ walks exactly the reference's node sequence (kdtree.cc:675-947).
 Rendering: film sums (R,G,B,A,weight per pixel) bit-exact on 1-device runs;
 ray counts (scene_t::intersect / isShadowed calls) exact.
 """
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -263,6 +265,31 @@ def test_shading_instantiations_photon(gpu_device, monkeypatch, diff):
 # per shading point; the default for lights of several samples, cornell), and
 # split records through the HBM any-hit kernel (YK_SMALL=0)
 FORMS = {"full": {"YK_SPLIT": "0"}, "split": {"YK_SPLIT": "1"}, "split_hbm": {"YK_SPLIT": "1", "YK_SMALL": "0"}}
+
+
+def test_shadow_form_choice(gpu_device, monkeypatch):
+    """The split form is the default for lights of several samples (cornell's
+    area light: 4 samples, K = 8), whole rays for one sample per light
+    (bumpy: K = 2), for transparent shadows, and under YK_SPLIT=0."""
+    monkeypatch.setenv("YK_DEBUG_HOOKS", "1")
+    monkeypatch.delenv("YK_SPLIT", raising=False)
+
+    def form(name, **over):
+        s, p, _ = scene(name, 32, 32, *((60, 31) if name == "bumpy" else ()))
+        q = A.yk_render_params.from_buffer_copy(p)
+        for k, v in over.items():
+            setattr(q, k, v)
+        gpu_device.upload(s)
+        v = C.c_int32(-1)
+        A.check(A.lib().yk_debug_shadow_form(gpu_device._p, C.byref(q), C.byref(v)))
+        return v.value
+
+    assert form("cornell_pt") == 1 and form("bumpy") == 0
+    assert form("cornell_pt", transp_shadows=1) == 0
+    monkeypatch.setenv("YK_SPLIT", "0")
+    assert form("cornell_pt") == 0
+    monkeypatch.setenv("YK_SPLIT", "1")
+    assert form("bumpy") == 1
 
 
 @pytest.mark.parametrize("form", list(FORMS))
