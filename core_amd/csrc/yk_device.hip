@@ -4818,12 +4818,14 @@ static int render_pass(yk_device* d, const yk_render_params* p, int32_t shard, i
   if (d->spec && spec_worst * tile_samples * kNodeBytes > (48ll << 30))
     return set_error(YK_ERR_UNSUPPORTED, "raydepth too large for the tile size / spp (node store > 48 GB)");
   const long long target_spec = d->spec ? std::min(target, (12ll << 30) / (kNodeBytes * spec_worst)) : target;
-  // path tracing / direct light: at least one batch per pipeline when the
-  // frame has the tiles for it -- a frame of 2 full batches (C2: 1024 tiles
-  // of 64K samples) leaves two pipelines idle (C2 8388 -> 8700 Mrays/s,
-  // headline and hair unchanged); photon mapping keeps full batches (its
-  // 16-spp bench frame in 4 batches instead of 1: 1572 -> 1537)
-  const long long tiles_fill = (d->spec || pm) ? LLONG_MAX : ((long long)owned.size() + pipes_cfg - 1) / pipes_cfg;
+  // at least one batch per pipeline when the frame has the tiles for it -- a
+  // frame of 2 full batches (C2: 1024 tiles of 64K samples) leaves two
+  // pipelines idle (C2 8388 -> 8700 Mrays/s, headline and hair unchanged);
+  // photon mapping too since round 6 (its 16-spp bench frame in 4 batches
+  // instead of 1: 2123-2129 against 2086-2090 Mrays/s; 6 or 8 batches lost:
+  // 1874-1944; round 2 had measured 1572 -> 1537 before the final-gather
+  // pipeline took its present form)
+  const long long tiles_fill = d->spec ? LLONG_MAX : ((long long)owned.size() + pipes_cfg - 1) / pipes_cfg;
   int tiles_per_batch = (int)std::max<long long>(1, std::min(target_spec / tile_samples, tiles_fill));
   // camera-sample indices are 32-bit on the device, shadow-slot indices
   // (k * kstride + r * maxc + c) 32-bit, and a shadow-queue entry holds k
