@@ -11,6 +11,7 @@
 #   bench                headline bench.py (1M tris, 1080p, 256 spp)
 #   c2 | pm | hair       BASELINE configs[1] Cornell / photon mapping / C5 hair benches
 #   prof                 rocprofv3 --kernel-trace --stats of the one-pipe headline frame
+#   prof4                kernel trace of one 4-pipe headline frame (overlap analysis)
 #   prof1:V / prof1c2:V  the same (headline / Cornell) with a variant's library (VARIANT[@ENV])
 #   pmcw1:V / pmcw1c2:V  WRITE_SIZE of the one-pipe headline / Cornell frame with a variant's library
 #   prof_c2 | prof_hair | prof_pm  the same for the Cornell / hair / photon-mapping frames
@@ -77,6 +78,10 @@ for s in "$@"; do
     v=${s#prof1:}
     env $(envv $v) YK_LIB=$(lib $v) timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof1_${v//[@=]/_} -o p1 -- python3 bench.py $P1 > $O/prof1_${v//[@=]/_}.log 2>&1
     echo "prof1 $v done" ;;
+  prof4)
+    # kernel trace of one 4-pipe headline frame (pipeline overlap / idle analysis)
+    timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof4 -o p4 -- python3 bench.py --steps 1 --warmup 1 --no-cpu --no-roofline-frame > $O/prof4.log 2>&1
+    echo "prof4 done" ;;
   prof1c2:*)
     # one-pipe Cornell (C2) frame, rocprofv3 --kernel-trace --stats, with VARIANT[@ENV]
     v=${s#prof1c2:}
