@@ -106,6 +106,21 @@ def dirac_lights(resx, resy, integrator="cornell_pt", with_dirac=True):
     return s, p
 
 
+def many_light_slots(resx, resy, integrator="cornell_pt", samples=(40, 3)):
+    """Cornell box (its ceiling light: 4 samples) + two more area lights of
+    `samples` samples each: K = 2 * (4 + 40 + 3) = 94 shadow slots per shading
+    point, past the 64 a slot bit mask covers, with light-sample blocks at
+    uneven offsets k0."""
+    s = Scene()
+    p = s.generate(integrator, resx, resy)
+    s.add_area_light((-0.6, 1.6, 0.6), (-0.3, 1.6, 0.6), (-0.6, 1.6, 0.9), color=(0.9, 0.8, 0.6), power=2.0,
+                     samples=samples[0])
+    s.add_area_light((0.5, 0.3, 0.9), (0.8, 0.3, 0.9), (0.5, 0.6, 0.9), color=(0.5, 0.7, 1.0), power=1.5,
+                     samples=samples[1])
+    s.build()
+    return s, p
+
+
 def specular(resx, resy, integrator="cornell_pt", raydepth=3, caustic=False, nu=16, nv=10, emit=0.0):
     """Cornell box + a mirror sphere, a glass-like sphere (fresnel mirror +
     transparency with a transmit filter) and a translucent sphere:

@@ -15,7 +15,7 @@ from core_amd import _abi as A
 from core_amd.scene import probe_scene
 from oracle.oracle import Oracle
 from tests.raygen import edge_rays, random_rays
-from tests.scenes import dirac_lights, dof_cornell, smooth_instanced, specular
+from tests.scenes import dirac_lights, dof_cornell, many_light_slots, smooth_instanced, specular
 
 pytestmark = pytest.mark.gpu
 
@@ -265,6 +265,29 @@ def test_shading_instantiations_photon(gpu_device, monkeypatch, diff):
 # per shading point; the default for lights of several samples, cornell), and
 # split records through the HBM any-hit kernel (YK_SMALL=0)
 FORMS = {"full": {"YK_SPLIT": "0"}, "split": {"YK_SPLIT": "1"}, "split_hbm": {"YK_SPLIT": "1", "YK_SMALL": "0"}}
+
+
+@pytest.mark.parametrize("form", ["full", "split"])
+@pytest.mark.parametrize("gen,merge", [("cornell_pt", "1"), ("cornell_pt", "0"), ("cornell_dl", "0")])
+def test_many_light_slots(gpu_device, monkeypatch, gen, merge, form):
+    """Three area lights (4 + 40 + 3 samples: 94 shadow slots per shading
+    point, beyond the 64-bit traced mask, so flush_shadow reads the later
+    slots' flags; split queue entries with 7 bits of k): path tracing merged
+    and per bounce, direct lighting, both slot forms -- films and ray counts
+    equal the oracle's bit for bit."""
+    monkeypatch.setenv("YK_MERGE", merge)
+    monkeypatch.setenv("YK_SPLIT", "1" if form == "split" else "0")
+    s, p = many_light_slots(24, 24, gen)
+    q = A.yk_render_params.from_buffer_copy(p)
+    q.aa_samples = 2
+    q.bounces = 3
+    orc = Oracle(s)
+    _, sums_o, cnt = orc.render(q)
+    gpu_device.upload(s)
+    film = gpu_device.new_film(q)
+    st = gpu_device.render_shard(q, film)
+    assert st.closest_rays == cnt["closest"] and st.shadow_rays == cnt["shadow"]
+    assert (film.cpu().numpy().view(np.uint32) == sums_o.view(np.uint32)).all()
 
 
 def test_shadow_form_choice(gpu_device, monkeypatch):
