@@ -173,6 +173,33 @@ def test_render_bit_exact(gpu_device, name, case, crop, over):
     assert st.closest_nodes == cnt["closest_nodes"] and st.shadow_tris == cnt["shadow_tris"]
 
 
+OTHER_FORM_CASES = ["pt_cornell_aa3", "pt_spec_aa2_mitchell", "pt_cornell_2sub", "pt_bumpy_tile16", "pt_hair",
+                    "pt_dirac_bg", "dl_dirac_bg", "pt_spec_rd5_caustic", "dl_spec_rd3", "pt_dof_ring_aa2"]
+
+
+@pytest.mark.parametrize("name", OTHER_FORM_CASES)
+def test_render_bit_exact_other_slot_form(gpu_device, monkeypatch, name):
+    """The render cases above in the shadow-slot form their scene does not
+    take by default (split records where whole rays are the default, and the
+    reverse; yk_debug_shadow_form): films, ray and work counts bit-exact."""
+    _, case, crop, over = next(c for c in RENDER_CASES if c[0] == name)
+    s, p, _ = scene(*case)
+    q = A.yk_render_params.from_buffer_copy(p)
+    for k, v in over.items():
+        setattr(q, k, v)
+    monkeypatch.setenv("YK_DEBUG_HOOKS", "1")
+    monkeypatch.delenv("YK_SPLIT", raising=False)
+    gpu_device.upload(s)
+    v = C.c_int32(-1)
+    A.check(A.lib().yk_debug_shadow_form(gpu_device._p, C.byref(q), C.byref(v)))
+    monkeypatch.setenv("YK_SPLIT", "0" if v.value else "1")
+    sums_o, sums_g, rgba_o, rgba_g, cnt, st = _render_pair(gpu_device, case, crop, **over)
+    assert st.closest_rays == cnt["closest"] and st.shadow_rays == cnt["shadow"]
+    assert (sums_g.view(np.uint32) == sums_o.view(np.uint32)).all()
+    assert (rgba_g.view(np.uint32) == rgba_o.view(np.uint32)).all()
+    assert st.closest_nodes == cnt["closest_nodes"] and st.shadow_tris == cnt["shadow_tris"]
+
+
 SMALL_CASES = [  # (scene, YK_SMALL): "0" = HBM kernels, "1" = default size limit, else a forced limit
     (("cornell_pt", 64, 64, 0, 0), "0"), (("cornell_pt", 64, 64, 0, 0), "1"),
     (("bumpy", 64, 64, 10, 7), "47104"), (("bumpy", 64, 64, 10, 7), "0"),
@@ -286,6 +313,30 @@ def test_many_light_slots(gpu_device, monkeypatch, gen, merge, form):
     gpu_device.upload(s)
     film = gpu_device.new_film(q)
     st = gpu_device.render_shard(q, film)
+    assert st.closest_rays == cnt["closest"] and st.shadow_rays == cnt["shadow"]
+    assert (film.cpu().numpy().view(np.uint32) == sums_o.view(np.uint32)).all()
+
+
+@pytest.mark.parametrize("form", ["full", "split"])
+def test_many_light_slots_photon(gpu_device, monkeypatch, form):
+    """The same three lights under photon mapping with final gathering (the
+    gather paths' estimateOneDirectLight picks one light per vertex, k0 = 0):
+    photon counts, film and ray counts bit-exact in both slot forms."""
+    monkeypatch.setenv("YK_SPLIT", "1" if form == "split" else "0")
+    s, p = many_light_slots(24, 24, "cornell_pt")
+    q = A.yk_render_params.from_buffer_copy(p)
+    q.integrator = A.YK_INTEGRATOR_PHOTON
+    q.photon.photons = 3000
+    q.photon.fg_samples = 3
+    q.aa_samples = 2
+    orc = Oracle(s)
+    info_o = orc.photon_build(q)
+    gpu_device.upload(s)
+    info = gpu_device.photon_build(q)
+    assert info.diffuse_photons == info_o["diffuse_photons"]
+    film = gpu_device.new_film(q)
+    st = gpu_device.render_shard(q, film)
+    _, sums_o, cnt = orc.render(q)
     assert st.closest_rays == cnt["closest"] and st.shadow_rays == cnt["shadow"]
     assert (film.cpu().numpy().view(np.uint32) == sums_o.view(np.uint32)).all()
 
