@@ -29,7 +29,7 @@
 #   multi                tests/test_multi_device.py + tests/test_0_multi_process.py
 #   shard                projected strong scaling (rank 0's share of the headline frame, N = 1/2/4/8)
 #   pmcw:VARIANT         WRITE_SIZE passes (one-pipe headline frame, traversal microbenchmark)
-#   pmcb:c2|head         the pmctb counter sets over a one-pipe frame, every kernel
+#   pmcb:c2|head|hair    the pmctb counter sets over a one-pipe frame, every kernel
 #   mallocs              hipMalloc count of 1 vs 3 yk_render_multi calls (rocprofv3 --hip-trace)
 set -e
 cd $GRAFT_REPO_ROOT
@@ -177,7 +177,7 @@ EOF
   pmcb:*)
     # the pmctb counter sets over a one-pipe frame (c2 | head), all kernels
     sc=${s#pmcb:}
-    A=""; [ $sc = c2 ] && A="$C2"
+    A=""; [ $sc = c2 ] && A="$C2"; [ $sc = hair ] && A="$HAIR"
     P=$O/pmcb_$sc
     mkdir -p $P
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/kt -o kt -- python3 bench.py $A $P1 > $P/kt.log 2>&1
