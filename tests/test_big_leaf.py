@@ -145,3 +145,37 @@ def test_crowded_leaf_any_hit_rounds(gpu_device, mode):
     assert (gocc == occ).all(), f"{(gocc != occ).sum()} mismatches"
     assert 0 < occ.sum() < len(occ)
     assert st.shadow_nodes == cnt[0] and st.shadow_tris == cnt[1]
+
+
+def _bundles(rays, copies=16, jitter=2e-4, seed=3):
+    """Each ray repeated `copies` times with its direction jittered: bundles of
+    near-identical rays, so the lanes of a wave share their leaves (the
+    grouped pair order's case: coherent camera rays on hair)."""
+    rng = np.random.default_rng(seed)
+    r = np.repeat(rays, copies, axis=0)
+    d = r[:, 3:6] + rng.uniform(-jitter, jitter, (len(r), 3)).astype(np.float32)
+    r[:, 3:6] = d / np.linalg.norm(d, axis=1, keepdims=True).astype(np.float32)
+    return r
+
+
+@pytest.mark.gpu
+def test_crowded_leaf_closest_bundles(gpu_device):
+    """A 600-reference leaf traced by bundles of coherent rays (the lanes of a
+    wave share the leaf, as hair's camera rays do) and by random rays: the
+    oracle's prim, t, b1, b2 -- the duplicated triangles tie exactly in t, so
+    the lowest reference index must win across the cooperative rounds -- and
+    its node and triangle-test counts."""
+    from oracle.oracle import Oracle
+    s = crowded_scene(A.YK_MODE_TRIANGLE)
+    orc = Oracle(s)
+    rays = np.concatenate([_bundles(_rays(s, n_aim=400, n_rand=0, seed=11)), _rays(s, n_aim=300, n_rand=300, seed=12)])
+    prim, t, b1, b2, cnt = orc.intersect(rays)
+    gpu_device.upload(s)
+    st = A.yk_stats()
+    gp, gt, gb1, gb2 = gpu_device.split_hits(gpu_device.trace_closest(gpu_device.rays_to_device(rays), st))
+    assert (gp == prim).all(), f"{(gp != prim).sum()} prim mismatches"
+    assert (prim >= 36).sum() > 1000
+    hit = prim >= 0
+    for a, b in ((gt, t), (gb1, b1), (gb2, b2)):
+        assert (a[hit].view(np.uint32) == b[hit].view(np.uint32)).all()
+    assert st.closest_nodes == cnt[0] and st.closest_tris == cnt[1]
